@@ -1,0 +1,88 @@
+"""ctypes binding of the C ABI in ``include/drsa_amd.h`` (``lib/libdrsa_amd.so``).
+
+This is the only door between the Python host layer and the HIP kernels.  There is
+no CPU fallback: if the library is missing or a call fails, an exception is raised.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libdrsa_amd.so")
+
+_lib: Optional[C.CDLL] = None
+
+_vp, _fp, _ip = C.c_void_p, C.c_void_p, C.c_void_p
+_i64, _i32, _sz, _f32, _f64 = C.c_int64, C.c_int, C.c_size_t, C.c_float, C.c_double
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "drsa_amd_last_error": (C.c_char_p, []),
+    "drsa_amd_version": (_i32, []),
+    "drsa_amd_drsa_workspace_bytes": (_sz, [_i64, _i32, _i32]),
+    "drsa_amd_drsa_partial": (_i32, [_fp, _fp, _i64, _i32, _i32, _fp, _fp, _vp, _sz, _vp]),
+    "drsa_amd_drsa_finish": (_i32, [_fp, _i64, _i32, _i32, _fp, _fp, _fp, _i32, _ip, _vp]),
+    "drsa_amd_drsa_step": (_i32, [_fp, _fp, _i64, _i32, _i32, _fp, _fp, _fp, _vp, _sz, _vp]),
+    "drsa_amd_drsa_objective": (_i32, [_fp, _fp, _i64, _i32, _i32, _fp, _fp, _vp, _sz, _vp]),
+    "drsa_amd_drsa_run": (_i32, [_fp, _fp, _i64, _i32, _i32, _fp, _fp, _i32, _fp, _ip, _vp, _sz, _i32, _vp]),
+    "drsa_amd_polar": (_i32, [_fp, _i32, _fp, _ip, _vp]),
+}
+
+
+class DrsaAmdError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH) -> C.CDLL:
+    """Load the HIP library (idempotent).  Raises if it is missing — never falls back."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise DrsaAmdError(
+            f"drsa_amd HIP library not found at {path}; build it with "
+            f"`python -m drsa_audio_amd.build` (hipcc, gfx950). There is no CPU fallback.")
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def lib() -> C.CDLL:
+    return _lib if _lib is not None else load()
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().drsa_amd_last_error().decode(errors="replace")
+        raise DrsaAmdError(f"{what or 'drsa_amd'} failed (rc={rc}): {msg}")
+
+
+def require_gpu(t: torch.Tensor, name: str, dtype=torch.float32) -> None:
+    if not t.is_cuda:
+        raise DrsaAmdError(f"{name}: tensor must live on the GPU (HIP device); got {t.device}. "
+                           "drsa_audio_amd has no CPU path.")
+    if dtype is not None and t.dtype != dtype:
+        raise DrsaAmdError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise DrsaAmdError(f"{name}: tensor must be contiguous")
+
+
+def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def stream_ptr(device: Optional[torch.device] = None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def call(name: str, *args) -> None:
+    fn = getattr(lib(), name)
+    check(fn(*args), name)

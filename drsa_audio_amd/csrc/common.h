@@ -1,0 +1,76 @@
+// Shared helpers for the drsa_amd HIP library (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// ---------------------------------------------------------------------------
+// status / error reporting across the C ABI (never throws)
+// ---------------------------------------------------------------------------
+namespace drsa {
+void set_error(const char* fmt, ...);
+}  // namespace drsa
+
+#define DRSA_OK 0
+#define DRSA_EINVAL (-1)
+#define DRSA_EWORKSPACE (-2)
+#define DRSA_EUNSUPPORTED (-3)
+
+#define DRSA_REQUIRE(cond, ...)           \
+  do {                                    \
+    if (!(cond)) {                        \
+      drsa::set_error(__VA_ARGS__);       \
+      return DRSA_EINVAL;                 \
+    }                                     \
+  } while (0)
+
+#define DRSA_HIP(call)                                                     \
+  do {                                                                     \
+    hipError_t _e = (call);                                                \
+    if (_e != hipSuccess) {                                                \
+      drsa::set_error("%s:%d %s: %s", __FILE__, __LINE__, #call,           \
+                      hipGetErrorString(_e));                              \
+      return (int)_e;                                                      \
+    }                                                                      \
+  } while (0)
+
+#define DRSA_LAUNCH_CHECK() DRSA_HIP(hipGetLastError())
+
+// ---------------------------------------------------------------------------
+// device helpers
+// ---------------------------------------------------------------------------
+// fp32-input MFMA, 16x16x4 (exact f32 fma chain, k-ordered).
+//   A operand: lane l holds A[i = l&15][k = l>>4]
+//   B operand: lane l holds B[k = l>>4][j = l&15]
+//   C/D:       lane l, reg r holds C[row = (l>>4)*4 + r][col = l&15]
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// fp32-input MFMA, 32x32x2.
+//   A operand: lane l holds A[i = l&31][k = l>>5]
+//   B operand: lane l holds B[k = l>>5][j = l&31]
+//   C/D:       lane l, reg r holds C[row = (r&3) + 8*(r>>2) + 4*(l>>5)][col = l&31]
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// zennit Stabilizer: t + eps * (sign(t) + [t == 0])
+__device__ __forceinline__ float stab(float t, float eps) {
+  float sgn = (t > 0.f) ? 1.f : ((t < 0.f) ? -1.f : 0.f);
+  float z = (t == 0.f) ? 1.f : 0.f;
+  return t + (z + sgn) * eps;
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+
+// xor-shuffle within a wave (64 lanes) via ds_bpermute
+__device__ __forceinline__ float shfl_xor(float v, int mask) {
+  return __shfl_xor(v, mask, 64);
+}

@@ -1,0 +1,216 @@
+"""Generate golden fixtures under tests/golden/ by running the REFERENCE code.
+
+Runs only in the build container (needs /root/reference).  Never imported by the
+product, never run on the GPU box.  The reference's ``cxai/xai/drsa/drsa.py`` has an
+import typo (``from pathilib import Path``, drsa.py:4, defect D1); a one-line
+``sys.modules['pathilib']`` shim supplies the name, the file itself is unmodified.
+
+Fixtures written (all small, numpy ``.npz`` / ``.npy``, no pickles):
+* drsa_fixture.npz  — generalized_fmean/objective_fn values, obj_val + autograd grad,
+                      orthogonalize, 10-step SubspaceOptimizer.run trajectories and
+                      final U for a tiny (N=256, d=16, K=4) and a C3-width
+                      (N=1000, d=64, K=4) problem, drsa.main's initial-U schedule.
+* u64_seed42.npy    — ortho_group.rvs(64) after np.random.seed(42) (bench U, drsa.py:265-272).
+* model_fixture.npz — module names of the GTZAN-128 / toy / ProjectionModel nets,
+                      parameter checksums after torch.manual_seed(0) (reference
+                      VGGType), ProjectionModel forward outputs.
+* preprocessing_fixture.npz — get_vectors_from_maps / normalize_vectors /
+                      compute_context_vectors on fixed small maps (reference
+                      preprocessing formulas; module itself needs zennit, so these
+                      are evaluated from the reference source text — see below).
+
+Input data are generated with numpy ``default_rng`` (PCG64: stable across numpy
+versions), so the tests regenerate them from the seed instead of storing them.
+"""
+from __future__ import annotations
+
+import os
+import pathlib
+import sys
+import tempfile
+import types
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+OUT = pathlib.Path(__file__).resolve().parent.parent / "tests" / "golden"
+
+
+def _import_reference():
+    sys.modules.setdefault("pathilib", types.SimpleNamespace(Path=pathlib.Path))
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    from cxai.xai.drsa import drsa as rdrsa
+    from cxai.model import create_model as rcm
+    from cxai.model import modify_model as rmm
+    return rdrsa, rcm, rmm
+
+
+def drsa_inputs(N: int, d: int, seed: int):
+    """Synthetic DRSA data: A = |N(0,1)| (post-ReLU-like), C ~ N(0,1), both normalised
+    with preprocessing.normalize_vectors semantics (v / rms / d^{1/4})."""
+    rng = np.random.default_rng(seed)
+    A = np.abs(rng.standard_normal((N, d))).astype(np.float32)
+    C = rng.standard_normal((N, d)).astype(np.float32)
+
+    def norm(v):
+        t = torch.from_numpy(v)
+        E = torch.sqrt(torch.mean(torch.square(t)))
+        return (t / E / d ** 0.25).numpy()
+    return norm(A), norm(C)
+
+
+def _drsa(rdrsa):
+    out = {}
+    # generalized_fmean / objective_fn on a fixed [N, K] input
+    rng = np.random.default_rng(7)
+    X = np.abs(rng.standard_normal((50, 4))).astype(np.float32)
+    out["fmean_in"] = X
+    out["fmean_p2"] = rdrsa.generalized_fmean(torch.from_numpy(X), 2).numpy()
+    out["fmean_p05"] = rdrsa.generalized_fmean(torch.from_numpy(X), 0.5).numpy()
+    out["objective"] = rdrsa.objective_fn(torch.from_numpy(X)).numpy()
+
+    for tag, (N, d, K, seed, steps) in {"small": (256, 16, 4, 11, 10),
+                                         "c3w": (1000, 64, 4, 12, 10)}.items():
+        A, C = drsa_inputs(N, d, seed)
+        np.random.seed(100 + seed)
+        from scipy.stats import ortho_group
+        U0 = ortho_group.rvs(d).astype(np.float32)
+        At, Ct, Ut = map(torch.from_numpy, (A, C, U0))
+        Ug = Ut.clone().requires_grad_(True)
+        f = rdrsa.SubspaceOptimizer.obj_val(At, Ct, Ug, rdrsa.objective_fn, K, d // K)
+        f.backward()
+        out[f"{tag}_meta"] = np.array([N, d, K, seed, steps])
+        out[f"{tag}_U0"] = U0
+        out[f"{tag}_A_checksum"] = np.array([A.sum(dtype=np.float64), C.sum(dtype=np.float64)])
+        out[f"{tag}_f0"] = np.array(float(f.detach()))
+        out[f"{tag}_G0"] = Ug.grad.numpy().copy()
+        out[f"{tag}_orth0"] = rdrsa.orthogonalize((Ut + Ug.grad).detach()).numpy()
+        with tempfile.TemporaryDirectory() as td:
+            opt = rdrsa.SubspaceOptimizer(Ut.clone(), At, Ct, td, num_concepts=K,
+                                          device=torch.device("cpu"))
+            losses = []
+            orig_save = opt.save_train_stats
+            opt.save_train_stats = lambda arr: losses.extend(float(a) for a in arr)
+            opt.save_model = lambda: None
+            opt.run(steps=steps)
+            out[f"{tag}_traj"] = np.array(losses)
+            out[f"{tag}_Ufinal"] = opt.U.detach().numpy().copy()
+
+    # drsa.main initial-U schedule: record the U handed to each run's optimiser
+    seen = []
+    cls = rdrsa.SubspaceOptimizer
+    orig_init, orig_run = cls.__init__, cls.run
+
+    def rec_init(self, U, *a, **k):
+        seen.append(U.detach().numpy().copy())
+        orig_init(self, U, *a, **k)
+    cls.__init__ = rec_init
+    cls.run = lambda self, steps=2000: None
+    try:
+        A, C = drsa_inputs(64, 16, 5)
+        with tempfile.TemporaryDirectory() as td:
+            rdrsa.main(torch.from_numpy(A), torch.from_numpy(C), td, num_concepts=4,
+                       steps=1, runs=3, seed=42, device=torch.device("cpu"))
+    finally:
+        cls.__init__, cls.run = orig_init, orig_run
+    out["main_U_runs"] = np.stack(seen)
+    return out
+
+
+def _models(rcm, rmm):
+    out = {}
+    torch.manual_seed(0)
+    gtzan = rcm.VGGType(n_filters=(32, 32, 64, 64, 128), n_dense=128,
+                        pool_kernels=((2, 2),) * 5, dropout=0.4, input_size=(128, 128),
+                        conv_bn=False, dense_bn=False, block_depth=1)
+    gtzan.eval()
+    names = [n for n, _ in gtzan.named_modules() if n.count(".") == 1]
+    out["gtzan_names"] = np.array(names)
+    out["gtzan_param_names"] = np.array([n for n, _ in gtzan.named_parameters()])
+    out["gtzan_param_sums"] = np.array([float(p.double().sum()) for p in gtzan.parameters()])
+    out["gtzan_param_abs"] = np.array([float(p.double().abs().sum()) for p in gtzan.parameters()])
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal((2, 1, 128, 128)).astype(np.float32)
+    out["gtzan_x"] = x
+    with torch.no_grad():
+        out["gtzan_logits"] = gtzan(torch.from_numpy(x)).numpy()
+    np.random.seed(42)
+    from scipy.stats import ortho_group
+    U = torch.tensor(ortho_group.rvs(64), dtype=torch.float32)
+    pm = rmm.ProjectionModel(gtzan, 7, U, 4, case="gtzan")
+    pm.eval()
+    out["proj_names"] = np.array([n for n, _ in pm.named_modules() if n.count(".") == 1])
+    with torch.no_grad():
+        out["proj_logits"] = pm(torch.from_numpy(x)).numpy()
+        h = pm.features[:9](torch.from_numpy(x))           # ... relu7 -> projection
+        out["proj_h"] = h[:, :64].numpy()               # first 64 positions only
+    # toy (only runnable through ProjectionModel, defect D6)
+    torch.manual_seed(0)
+    toy = rcm.VGGType(n_filters=(8, 8, 16, 16, 16), n_dense=32, n_classes=2,
+                      pool_kernels=((2, 2),) * 5, dropout=0.0, input_size=(64, 64),
+                      conv_bn=False, dense_bn=False, block_depth=1)
+    toy.eval()
+    out["toy_names"] = np.array([n for n, _ in toy.named_modules() if n.count(".") == 1])
+    out["toy_param_sums"] = np.array([float(p.double().sum()) for p in toy.parameters()])
+    Ut = torch.eye(16)
+    pmt = rmm.ProjectionModel(toy, 7, Ut, 1, case="toy")
+    xt = rng.standard_normal((1, 1, 64, 64)).astype(np.float32)
+    out["toy_x"] = xt
+    with torch.no_grad():
+        out["toy_logits"] = pmt(torch.from_numpy(xt)).numpy()
+    # VGGish-BN shape contract (C5)
+    torch.manual_seed(0)
+    vgg = rcm.VGGType(n_filters=(64, 64, 100, 128, 128), n_dense=100,
+                      pool_kernels=((2, 4), (2, 2), (2, 2), (2, 2), (2, 2)), dropout=0.3,
+                      input_size=(128, 256), conv_bn=True, dense_bn=True)
+    out["vggish_names"] = np.array([n for n, _ in vgg.named_modules() if n.count(".") == 1])
+    out["vggish_param_sums"] = np.array([float(p.double().sum()) for p in vgg.parameters()])
+    return out
+
+
+def _preprocessing():
+    """preprocessing.py imports zennit (absent), so its pure-torch helpers cannot be
+    imported; they are evaluated here by exec'ing ONLY their function source text
+    extracted from the reference file (no module import, nothing persisted)."""
+    import ast
+    src = pathlib.Path(REF, "cxai/xai/drsa/preprocessing.py").read_text()
+    tree = ast.parse(src)
+    keep = {"compute_context_vectors", "normalize_vectors", "get_vectors_from_maps"}
+    ns = {"torch": torch, "np": np, "Tuple": tuple}
+    for node in tree.body:
+        if isinstance(node, ast.FunctionDef) and node.name in keep:
+            mod = ast.Module(body=[node], type_ignores=[])
+            exec(compile(mod, "preprocessing.py", "exec"), ns)
+    rng = np.random.default_rng(9)
+    maps_a = np.maximum(rng.standard_normal((3, 8, 6, 6)), 0).astype(np.float32)
+    maps_r = rng.standard_normal((3, 8, 6, 6)).astype(np.float32)
+    idx = np.stack([rng.choice(36, 5, replace=False) for _ in range(3)])
+    va = ns["get_vectors_from_maps"](torch.from_numpy(maps_a), idx)
+    vr = ns["get_vectors_from_maps"](torch.from_numpy(maps_r), idx)
+    ctx = ns["compute_context_vectors"](va, vr)
+    return {"maps_a": maps_a, "maps_r": maps_r, "idx": idx, "vec_a": va.numpy(),
+            "vec_r": vr.numpy(), "ctx": ctx.numpy(),
+            "norm_a": ns["normalize_vectors"](va).numpy(),
+            "norm_ctx": ns["normalize_vectors"](ctx).numpy()}
+
+
+def main():
+    OUT.mkdir(parents=True, exist_ok=True)
+    rdrsa, rcm, rmm = _import_reference()
+    np.savez_compressed(OUT / "drsa_fixture.npz", **_drsa(rdrsa))
+    np.random.seed(42)
+    from scipy.stats import ortho_group
+    np.save(OUT / "u64_seed42.npy", ortho_group.rvs(64).astype(np.float32))
+    np.savez_compressed(OUT / "model_fixture.npz", **_models(rcm, rmm))
+    np.savez_compressed(OUT / "preprocessing_fixture.npz", **_preprocessing())
+    with open(OUT / "VERSIONS.txt", "w") as fh:
+        import scipy
+        fh.write(f"torch {torch.__version__}\nnumpy {np.__version__}\nscipy {scipy.__version__}\n"
+                 f"python {sys.version.split()[0]}\n")
+    print("fixtures written to", OUT)
+
+
+if __name__ == "__main__":
+    main()
