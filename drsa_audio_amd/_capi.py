@@ -30,7 +30,24 @@ SIGNATURES = {
     "drsa_amd_drsa_objective": (_i32, [_fp, _fp, _i64, _i32, _i32, _fp, _fp, _vp, _sz, _vp]),
     "drsa_amd_drsa_run": (_i32, [_fp, _fp, _i64, _i32, _i32, _fp, _fp, _i32, _fp, _ip, _vp, _sz, _i32, _vp]),
     "drsa_amd_polar": (_i32, [_fp, _i32, _fp, _ip, _vp]),
+    "drsa_amd_subspace_relevances": (_i32, [_fp, _fp, _i64, _i64, _i32, _i32, _fp, _fp, _vp]),
+    "drsa_amd_conv_weight_floats": (_sz, [_i32, _i32, _i32]),
+    "drsa_amd_conv_fwd": (_i32, [_fp, _fp, _fp, _fp, _fp, _vp, _fp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
+    "drsa_amd_conv_bwd": (_i32, [_fp, _vp, _fp, _fp, _fp, _fp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
+                                 _i32, _f32, _vp]),
+    "drsa_amd_linear_fwd": (_i32, [_fp, _fp, _fp, _fp, _fp, _i32, _i32, _i32, _vp]),
+    "drsa_amd_linear_bwd": (_i32, [_fp, _ip, _i32, _fp, _i32, _i32, _f32, _fp, _fp, _i32, _fp, _i32, _f32, _fp,
+                                   _i32, _i32, _i32, _vp]),
+    "drsa_amd_projection_fwd": (_i32, [_fp, _fp, _fp, _fp, _fp, _vp, _i32, _i32, _i32, _i32, _i32, _vp]),
+    "drsa_amd_projection_bwd": (_i32, [_fp, _vp, _fp, _fp, _fp, _fp, _fp, _fp, _i32, _i32, _i32, _i32, _i32,
+                                       _f32, _f32, _i32, _vp]),
+    "drsa_amd_first_layer_bwd": (_i32, [_fp, _vp, _fp, _fp, _i32, _i32, _i32, _i32, _i32, _vp]),
+    "drsa_amd_first_layer_den": (_i32, [_fp, _fp, _fp, _i32, _i32, _i32, _i32, _vp]),
+    "drsa_amd_heatmap_sort": (_i32, [_fp, _i32, _i32, _i32, _fp, _fp, _fp, _fp, _vp, _vp]),
 }
+
+XM_NONE, XM_MUL, XM_SPLIT = 0, 1, 2
+POST_NONE, POST_DIV, POST_MASK = 0, 1, 2
 
 
 class DrsaAmdError(RuntimeError):

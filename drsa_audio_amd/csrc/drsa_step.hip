@@ -267,18 +267,31 @@ __device__ void lds_matmul_tn(const float* X, const float* Y, float* Z, int ld) 
 }
 
 template <int D>
-__device__ void lds_matmul_nn(const float* X, const float* Y, float* Z, int ld) {
-  // Z = X Y
+__device__ void lds_matmul_nn_inplace(float* X, const float* Y, int ld) {
+  // X <- X Y.  Each wave keeps its output tiles in registers until every wave has
+  // finished reading X, then overwrites X (saves a third D x D LDS matrix).
   constexpr int NB = D / 16;
+  constexpr int NT = (NB * NB + 3) / 4;
   const int lane = lane_id(), w = wave_id();
-  for (int t = w; t < NB * NB; t += 4) {
+  f32x4 acc[NT];
+#pragma unroll
+  for (int q = 0; q < NT; ++q) {
+    acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int t = w + 4 * q;
+    if (t >= NB * NB) break;
     const int ib = t / NB, jb = t % NB;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int k0 = 0; k0 < D; k0 += 4) {
       const int kk = k0 + (lane >> 4);
-      acc = mfma16(X[(16 * ib + (lane & 15)) * ld + kk], Y[kk * ld + 16 * jb + (lane & 15)], acc);
+      acc[q] = mfma16(X[(16 * ib + (lane & 15)) * ld + kk], Y[kk * ld + 16 * jb + (lane & 15)], acc[q]);
     }
-    for (int r = 0; r < 4; ++r) Z[(16 * ib + (lane >> 4) * 4 + r) * ld + 16 * jb + (lane & 15)] = acc[r];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NT; ++q) {
+    const int t = w + 4 * q;
+    if (t >= NB * NB) break;
+    const int ib = t / NB, jb = t % NB;
+    for (int r = 0; r < 4; ++r) X[(16 * ib + (lane >> 4) * 4 + r) * ld + 16 * jb + (lane & 15)] = acc[q][r];
   }
 }
 
@@ -303,9 +316,8 @@ __device__ float block_sum(float v, float* scratch) {
 }
 
 template <int D>
-__device__ void polar_ns(float* X, float* P, float* T, float* scratch, float tol, int max_iter,
-                         int* iters_out) {
-  // in: X = V (LDS, ld D+1); out: X = polar factor
+__device__ void polar_ns(float* X, float* P, float* scratch, float tol, int max_iter, int* iters_out) {
+  // in: X = V (LDS, ld D+1); out: X = polar factor.  X <- X (1.5 I - 0.5 X^T X).
   constexpr int ld = D + 1;
   const int tid = threadIdx.x;
   __syncthreads();
@@ -338,17 +350,11 @@ __device__ void polar_ns(float* X, float* P, float* T, float* scratch, float tol
       const int r = i / D, c = i % D;
       const float pv = P[r * ld + c];
       err = fmaxf(err, fabsf(pv - (r == c ? 1.f : 0.f)));
-      T[r * ld + c] = (r == c ? 1.5f : 0.f) - 0.5f * pv;
+      P[r * ld + c] = (r == c ? 1.5f : 0.f) - 0.5f * pv;   // T, in place
     }
     err = block_max(err, scratch + 32);
     if (err < tol) break;
-    __syncthreads();
-    lds_matmul_nn<D>(X, T, P, ld);   // P <- X T
-    __syncthreads();
-    for (int i = tid; i < D * D; i += blockDim.x) {
-      const int r = i / D, c = i % D;
-      X[r * ld + c] = P[r * ld + c];
-    }
+    lds_matmul_nn_inplace<D>(X, P, ld);
   }
   if (iters_out && tid == 0) *iters_out = it;
   __syncthreads();
@@ -364,8 +370,7 @@ __global__ __launch_bounds__(256) void drsa_finish_kernel(
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* X = smem;
   float* P = X + D * ld;
-  float* T = P + D * ld;
-  float* scratch = T + D * ld;   // 64 floats
+  float* scratch = P + D * ld;   // 64 floats
   __shared__ float cvec[128];
   __shared__ float fsh;
   const int tid = threadIdx.x;
@@ -392,7 +397,7 @@ __global__ __launch_bounds__(256) void drsa_finish_kernel(
     const int r = i / D, c = i % D;
     X[r * ld + c] = U[i] + gs[i] * cvec[c / DK];
   }
-  polar_ns<D>(X, P, T, scratch, tol, max_iter, iters_out);
+  polar_ns<D>(X, P, scratch, tol, max_iter, iters_out);
   for (int i = tid; i < D * D; i += blockDim.x) {
     const int r = i / D, c = i % D;
     U_out[i] = X[r * ld + c];
@@ -408,11 +413,51 @@ __global__ __launch_bounds__(256) void polar_kernel(const float* __restrict__ V,
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* X = smem;
   float* P = X + D * ld;
-  float* T = P + D * ld;
-  float* scratch = T + D * ld;
+  float* scratch = P + D * ld;
   for (int i = threadIdx.x; i < D * D; i += blockDim.x) X[(i / D) * ld + i % D] = V[i];
-  polar_ns<D>(X, P, T, scratch, tol, max_iter, iters_out);
+  polar_ns<D>(X, P, scratch, tol, max_iter, iters_out);
   for (int i = threadIdx.x; i < D * D; i += blockDim.x) U_out[i] = X[(i / D) * ld + i % D];
+}
+
+// ---------------------------------------------------------------------------
+// compute_subspace_relevances (explainer.py:206-242):
+//   r[b][k] = sum_n sum_{j in block k} (a_n U)_j (c_n U)_j   (no ReLU)
+// One workgroup per instance b; thread t owns rows t, t+256, ...; fixed-order reduction.
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256) void subspace_relevance_kernel(const float* __restrict__ act,
+                                                                 const float* __restrict__ ctx, int64_t N, int K,
+                                                                 const float* __restrict__ U, float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* Us = sm;              // [D][D]
+  float* red = Us + D * D;     // [256][K]
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int dk = D / K;
+  for (int i = tid; i < D * D; i += 256) Us[i] = U[i];
+  for (int k = 0; k < K; ++k) red[tid * K + k] = 0.f;
+  __syncthreads();
+  const float* A = act + (size_t)b * N * D;
+  const float* C = ctx + (size_t)b * N * D;
+  for (int64_t n = tid; n < N; n += 256) {
+    float av[D], cv[D];
+#pragma unroll
+    for (int c = 0; c < D; ++c) { av[c] = A[n * D + c]; cv[c] = C[n * D + c]; }
+    for (int j = 0; j < D; ++j) {
+      float xa = 0.f, xc = 0.f;
+#pragma unroll
+      for (int c = 0; c < D; ++c) {
+        xa = fmaf(av[c], Us[c * D + j], xa);
+        xc = fmaf(cv[c], Us[c * D + j], xc);
+      }
+      red[tid * K + j / dk] += xa * xc;
+    }
+  }
+  __syncthreads();
+  if (tid < K) {
+    float acc = 0.f;
+    for (int t = 0; t < 256; ++t) acc += red[t * K + tid];
+    out[(size_t)b * K + tid] = acc;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -502,7 +547,7 @@ int dispatch_partial(const float* A, const float* C, int64_t N, int d, int K, co
 }
 
 template <int D>
-size_t finish_lds() { return (3 * (size_t)D * (D + 1) + 64) * sizeof(float); }
+size_t finish_lds() { return (2 * (size_t)D * (D + 1) + 64) * sizeof(float); }
 
 template <int D>
 int launch_finish(const float* gs, double n_total, int K, const float* U, float* U_out, float* f_out,
@@ -700,4 +745,27 @@ int drsa_amd_polar(const float* V, int d, float* U_out, int* iters_out, void* st
   }
 }
 
+int drsa_amd_subspace_relevances(const float* act, const float* ctx, int64_t B, int64_t N, int d, int K,
+                                 const float* U, float* out, void* stream) {
+  DRSA_REQUIRE(d == 16 || d == 32 || d == 64 || d == 128, "subspace_relevances: unsupported d=%d", d);
+  DRSA_REQUIRE(K > 0 && K <= 128 && d % K == 0, "subspace_relevances: K must divide d");
+  hipStream_t s = (hipStream_t)stream;
+  auto go = [&](auto tag) -> int {
+    constexpr int D = decltype(tag)::value;
+    const size_t lds = ((size_t)D * D + 256 * (size_t)K) * sizeof(float);
+    DRSA_HIP(hipFuncSetAttribute((const void*)subspace_relevance_kernel<D>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(subspace_relevance_kernel<D>, dim3((unsigned)B), dim3(256), lds, s, act, ctx, N, K, U, out);
+    DRSA_LAUNCH_CHECK();
+    return DRSA_OK;
+  };
+  switch (d) {
+    case 16: return go(std::integral_constant<int, 16>{});
+    case 32: return go(std::integral_constant<int, 32>{});
+    case 64: return go(std::integral_constant<int, 64>{});
+    default: return go(std::integral_constant<int, 128>{});
+  }
+}
+
 }  // extern "C"
+

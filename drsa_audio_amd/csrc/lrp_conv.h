@@ -1,0 +1,24 @@
+// Internal kernel-argument structs for the LRP engine (not part of the public ABI).
+#pragma once
+#include <stdint.h>
+
+enum XMode { XM_NONE = 0, XM_MUL = 1, XM_SPLIT = 2 };
+enum PostMode { POST_NONE = 0, POST_DIV = 1, POST_MASK = 2 };
+
+struct ConvArgs {
+  const float* in;          // A source: NCHW input (dense) or g at pool resolution (sparse)
+  const uint8_t* in_amax;   // pool argmax (0..3) of the sparse source, per sample
+  const float* wts;         // [NG][9 * cin_p][cout_p], k = (ky*3 + kx) * cin_p + ci
+  const float* bias;        // forward: [3][cout_p] = (b, b+, b-)
+  const float* den_map;     // forward, WSquare/Flat: [cout][H][W] input-independent denominator
+  const float* x;           // backward: activation at output resolution (per sample)
+  const float* den;         // backward POST_DIV: next layer's denominator at output resolution
+  float* out;
+  uint8_t* out_amax;
+  float* out_den;
+  int H, W;                 // output resolution
+  int cin, cout;            // real channel counts (<= padded template sizes)
+  int clones;               // batch index / clones = sample index
+  int xmode, post;
+  float eps;
+};

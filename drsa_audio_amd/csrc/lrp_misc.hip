@@ -1,0 +1,548 @@
+// LRP engine kernels besides the 3x3 conv:
+//   * dense head   (classifier Linear layers; Epsilon rule, reference constants.py:35-37)
+//   * projection   (ProjectionModel virtual layers, reference modify_model.py:75-123, with the
+//                   composite of explainer.py:198-203: Epsilon on invprojection, SubspaceHook mask,
+//                   Epsilon on projection; SubspaceHook.backward = attribute.py:53-60)
+//   * first layer  (WSquare / Flat backward, reference constants.py:29,42; zennit 0.5.1)
+//   * denominator map of WSquare / Flat (input independent)
+//   * heatmap split / per-subspace sums / descending sort (explainer.py:99-176)
+#include "common.h"
+#include "lrp_conv.h"
+
+namespace {
+
+// ===========================================================================
+// dense head: C[M][N] = A[M][K] B[K][N] on fp32 MFMA 16x16x4, 32x32 workgroup tile
+//   forward : A = x,  B[k][n] = W[n][k];  z = acc + b;  optional a = relu(z)
+//   backward: A[m][n] = g = prologue(R | seed, z), B[n][k] = W[n][k];  out = epilogue(acc, x, den)
+// ===========================================================================
+constexpr int LT = 32;   // workgroup tile (M and N)
+constexpr int LK = 32;   // K chunk
+
+struct LinArgs {
+  const float* A;        // fwd: x [M][K]; bwd: R [M][Kg] (ignored when seed)
+  const float* W;        // [Nout][Kin] (torch Linear weight)
+  const float* bias;     // fwd
+  const float* z;        // bwd: forward output of this layer [M][Kg]
+  const int* cls;        // bwd seed: class per row (nullable -> not seed)
+  const float* x;        // bwd: forward input of this layer [M][N]
+  const float* den;      // bwd POST_DIV: next (lower) layer denominator, same indexing as out
+  float* out;            // fwd: z [M][N]; bwd: R_in or g_next [M][N]
+  float* out_relu;       // fwd: relu(z) (nullable)
+  int M, N, K;           // GEMM dims
+  int bwd;
+  int one_hot, relu_mask, rule_eps, xmode, post;
+  float eps, eps_post;
+};
+
+__global__ __launch_bounds__(256) void linear_kernel(LinArgs a) {
+  __shared__ float As[LT][LK + 1];
+  __shared__ float Bs[LK][LT + 1];
+  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int m0 = blockIdx.x * LT, n0 = blockIdx.y * LT;
+  const int wm = (w & 1) * 16, wn = (w >> 1) * 16;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < a.K; k0 += LK) {
+    __syncthreads();
+    for (int idx = tid; idx < LT * LK; idx += 256) {
+      const int r = idx / LK, c = idx % LK;
+      const int m = m0 + r, k = k0 + c;
+      float v = 0.f;
+      if (m < a.M && k < a.K) {
+        if (!a.bwd) {
+          v = a.A[(size_t)m * a.K + k];
+        } else {
+          // g = [z > 0]? R / stab(z) (rule Epsilon) or R (plain); R = seed or incoming relevance
+          const float zz = a.z[(size_t)m * a.K + k];
+          float R;
+          if (a.cls) {
+            const bool hit = (k == a.cls[m]);
+            R = hit ? (a.one_hot ? 1.f : zz) : 0.f;
+          } else {
+            R = a.A[(size_t)m * a.K + k];
+          }
+          if (a.relu_mask && !(zz > 0.f)) R = 0.f;
+          v = a.rule_eps ? R / stab(zz, a.eps) : R;
+        }
+      }
+      As[r][c] = v;
+    }
+    for (int idx = tid; idx < LK * LT; idx += 256) {
+      const int r = idx / LT, c = idx % LT;
+      const int k = k0 + r, n = n0 + c;
+      float v = 0.f;
+      if (k < a.K && n < a.N) v = a.bwd ? a.W[(size_t)k * a.N + n] : a.W[(size_t)n * a.K + k];
+      Bs[r][c] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < LK; kk += 4) {
+      const float av = As[wm + (lane & 15)][kk + (lane >> 4)];
+      const float bv = Bs[kk + (lane >> 4)][wn + (lane & 15)];
+      acc = mfma16(av, bv, acc);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = m0 + wm + (lane >> 4) * 4 + r, n = n0 + wn + (lane & 15);
+    if (m >= a.M || n >= a.N) continue;
+    const size_t o = (size_t)m * a.N + n;
+    if (!a.bwd) {
+      const float zz = acc[r] + (a.bias ? a.bias[n] : 0.f);
+      a.out[o] = zz;
+      if (a.out_relu) a.out_relu[o] = zz > 0.f ? zz : (zz != zz ? zz : 0.f);
+    } else {
+      float R = acc[r];
+      if (a.xmode == XM_MUL) R = a.x[o] * R;
+      if (a.post == POST_DIV) {
+        const float xv = a.x[o];
+        R = (xv > 0.f) ? R / stab(a.den[o], a.eps_post) : 0.f;
+      } else if (a.post == POST_MASK) {
+        R = (a.x[o] > 0.f) ? R : 0.f;
+      }
+      a.out[o] = R;
+    }
+  }
+}
+
+// ===========================================================================
+// projection forward: h = a_vec U, a' = h U^T, optional 2x2 max-pool of a'
+//   a [B][D][H][W] -> h [B][H*W][D], ap [B][D][H][W], pooled [B][D][H/2][W/2] + argmax
+//   workgroup = 8x8 pixel tile (64 pixels), 4 waves; D in {16,...,128} (multiple of 16)
+// ===========================================================================
+template <int D>
+__global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __restrict__ a, const float* __restrict__ U,
+                                                            float* __restrict__ h, float* __restrict__ ap,
+                                                            float* __restrict__ pooled, uint8_t* __restrict__ amax,
+                                                            int H, int W, int pool) {
+  constexpr int P = 64, LD = D + 1;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* Us = sm;               // [D][LD]
+  float* as = Us + D * LD;      // [D][P]   (channel-major tile)
+  float* hs = as + D * P;       // [P][LD]
+  float* aps = as;              // [D][P]   (reuses the a tile after the first GEMM)
+  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int tiles_x = W / 8;
+  const int ty0 = (blockIdx.x / tiles_x) * 8, tx0 = (blockIdx.x % tiles_x) * 8;
+  const int b = blockIdx.y;
+  const int HW = H * W;
+  for (int i = tid; i < D * D; i += 256) Us[(i / D) * LD + i % D] = U[i];
+  for (int i = tid; i < D * P; i += 256) {
+    const int c = i / P, p = i % P;
+    const int y = ty0 + p / 8, x = tx0 + p % 8;
+    as[c * P + p] = a[((size_t)b * D + c) * HW + y * W + x];
+  }
+  __syncthreads();
+  constexpr int NB = D / 16, TILES = (P / 16) * NB;   // 16x16 output tiles of [P][D]
+  // h[p][j] = sum_c a[c][p] U[c][j]
+  for (int t = w; t < TILES; t += 4) {
+    const int pb = t / NB, jb = t % NB;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < D; k0 += 4) {
+      const int c = k0 + (lane >> 4);
+      acc = mfma16(as[c * P + pb * 16 + (lane & 15)], Us[c * LD + jb * 16 + (lane & 15)], acc);
+    }
+    for (int r = 0; r < 4; ++r) {
+      const int p = pb * 16 + (lane >> 4) * 4 + r, j = jb * 16 + (lane & 15);
+      hs[p * LD + j] = acc[r];
+      const int y = ty0 + p / 8, x = tx0 + p % 8;
+      h[((size_t)b * HW + y * W + x) * D + j] = acc[r];
+    }
+  }
+  __syncthreads();
+  // a'[p][c] = sum_j h[p][j] U[c][j]
+  for (int t = w; t < TILES; t += 4) {
+    const int pb = t / NB, cb = t % NB;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < D; k0 += 4) {
+      const int j = k0 + (lane >> 4);
+      acc = mfma16(hs[(pb * 16 + (lane & 15)) * LD + j], Us[(cb * 16 + (lane & 15)) * LD + j], acc);
+    }
+    for (int r = 0; r < 4; ++r) {
+      const int p = pb * 16 + (lane >> 4) * 4 + r, c = cb * 16 + (lane & 15);
+      aps[c * P + p] = acc[r];
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < D * P; i += 256) {
+    const int c = i / P, p = i % P;
+    const int y = ty0 + p / 8, x = tx0 + p % 8;
+    ap[((size_t)b * D + c) * HW + y * W + x] = aps[c * P + p];
+  }
+  if (pool) {
+    const int H2 = H / 2, W2 = W / 2;
+    for (int i = tid; i < D * 16; i += 256) {
+      const int c = i / 16, q = i % 16;
+      const int qy = q / 4, qx = q % 4;
+      const int p0 = (2 * qy) * 8 + 2 * qx;
+      float v[4] = {aps[c * P + p0], aps[c * P + p0 + 1], aps[c * P + p0 + 8], aps[c * P + p0 + 9]};
+      int am = 0;
+      float m = v[0];
+      for (int s = 1; s < 4; ++s)
+        if (v[s] > m || (v[s] != v[s] && m == m)) { m = v[s]; am = s; }
+      const size_t o = ((size_t)b * D + c) * H2 * W2 + (ty0 / 2 + qy) * W2 + tx0 / 2 + qx;
+      pooled[o] = m;
+      amax[o] = (uint8_t)am;
+    }
+  }
+}
+
+// ===========================================================================
+// projection backward (per sample, fans out to K+1 relevance clones):
+//   R_a'  = pool-backward(gp, argmax)               (or dense R when no pool follows)
+//   g1    = R_a' / stab(a', eps_proj)               Epsilon on invprojection
+//   R_h   = h (.) (g1 U)
+//   g2    = R_h / stab(h, eps_proj)                  Epsilon on projection (after the mask)
+//   clone 0: v = g2 U^T ; clone k: v = g2[block k-1] U[:, block k-1]^T   (SubspaceHook mask)
+//   G_q   = [a > 0] (a (.) v) / stab(den, eps_den)   ReLU-backward + the conv rule's division below
+// ===========================================================================
+template <int D>
+__global__ __launch_bounds__(256) void projection_bwd_kernel(
+    const float* __restrict__ gp, const uint8_t* __restrict__ amax, const float* __restrict__ ap,
+    const float* __restrict__ h, const float* __restrict__ a, const float* __restrict__ den,
+    const float* __restrict__ U, float* __restrict__ G, int H, int W, int K, float eps_proj, float eps_den,
+    int sparse, int has_den, int fanout) {
+  constexpr int P = 64, LD = D + 1;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* Us = sm;               // [D][LD]
+  float* g1 = Us + D * LD;      // [D][P]
+  float* g2 = g1 + D * P;       // [P][LD]
+  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int tiles_x = W / 8;
+  const int ty0 = (blockIdx.x / tiles_x) * 8, tx0 = (blockIdx.x % tiles_x) * 8;
+  const int b = blockIdx.y;
+  const int HW = H * W;
+  const int dk = D / K;
+  for (int i = tid; i < D * D; i += 256) Us[(i / D) * LD + i % D] = U[i];
+  for (int i = tid; i < D * P; i += 256) {
+    const int c = i / P, p = i % P;
+    const int y = ty0 + p / 8, x = tx0 + p % 8;
+    float R;
+    if (sparse) {
+      const int H2 = H / 2, W2 = W / 2;
+      const size_t q = ((size_t)b * D + c) * H2 * W2 + (y >> 1) * W2 + (x >> 1);
+      R = (amax[q] == (((y & 1) << 1) | (x & 1))) ? gp[q] : 0.f;
+    } else {
+      R = gp[((size_t)b * D + c) * HW + y * W + x];
+    }
+    g1[c * P + p] = R / stab(ap[((size_t)b * D + c) * HW + y * W + x], eps_proj);
+  }
+  __syncthreads();
+  constexpr int NB = D / 16, TILES = (P / 16) * NB;
+  // t[p][j] = sum_c g1[c][p] U[c][j];  R_h = h (.) t;  g2 = R_h / stab(h)
+  for (int t = w; t < TILES; t += 4) {
+    const int pb = t / NB, jb = t % NB;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < D; k0 += 4) {
+      const int c = k0 + (lane >> 4);
+      acc = mfma16(g1[c * P + pb * 16 + (lane & 15)], Us[c * LD + jb * 16 + (lane & 15)], acc);
+    }
+    for (int r = 0; r < 4; ++r) {
+      const int p = pb * 16 + (lane >> 4) * 4 + r, j = jb * 16 + (lane & 15);
+      const int y = ty0 + p / 8, x = tx0 + p % 8;
+      const float hv = h[((size_t)b * HW + y * W + x) * D + j];
+      const float Rh = hv * acc[r];
+      g2[p * LD + j] = Rh / stab(hv, eps_proj);
+    }
+  }
+  __syncthreads();
+  // clones: q = 0 (all blocks), q = 1..K (block q-1).  fanout: write all K+1 clones of this
+  // sample; otherwise the row IS clone (b mod (K+1)) of a user-replicated batch (explainer.py:92).
+  const int nq = fanout ? (K + 1) : 1;
+  for (int t = w; t < nq * TILES; t += 4) {
+    const int q = fanout ? t / TILES : b % (K + 1), tt = t % TILES;
+    const int pb = tt / NB, cb = tt % NB;
+    const int j0 = q == 0 ? 0 : (q - 1) * dk, j1 = q == 0 ? D : q * dk;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k0 = j0; k0 < j1; k0 += 4) {
+      const int j = k0 + (lane >> 4);
+      const bool ok = j < j1;
+      const float av = ok ? g2[(pb * 16 + (lane & 15)) * LD + j] : 0.f;
+      const float bv = ok ? Us[(cb * 16 + (lane & 15)) * LD + j] : 0.f;
+      acc = mfma16(av, bv, acc);
+    }
+    for (int r = 0; r < 4; ++r) {
+      const int p = pb * 16 + (lane >> 4) * 4 + r, c = cb * 16 + (lane & 15);
+      const int y = ty0 + p / 8, x = tx0 + p % 8;
+      const size_t os = ((size_t)b * D + c) * HW + y * W + x;
+      const float av = a[os];
+      float Rv = av * acc[r];
+      float g;
+      if (has_den) g = (av > 0.f) ? Rv / stab(den[os], eps_den) : 0.f;
+      else g = (av > 0.f) ? Rv : 0.f;
+      const size_t orow = fanout ? (size_t)b * (K + 1) + q : (size_t)b;
+      G[(orow * D + c) * HW + y * W + x] = g;
+    }
+  }
+}
+
+// ===========================================================================
+// first layer backward (WSquare / Flat, one input channel):
+//   R[y][x] = sum_co sum_{dy,dx} G[co][y+dy][x+dx] * W2[co][1-dy][1-dx]
+//   G from pool-sparse (gp, argmax) or dense; 16 x 64 output tile, 4 pixels per thread
+// ===========================================================================
+constexpr int FL_TH = 16, FL_TW = 64, FL_CC = 8;
+
+__global__ __launch_bounds__(256) void first_layer_bwd_kernel(const float* __restrict__ g, const uint8_t* __restrict__ amax,
+                                                              const float* __restrict__ w2, float* __restrict__ out,
+                                                              int C, int H, int W, int clones) {
+  constexpr int HY = FL_TH + 2, HX = FL_TW + 2, RS = FL_TW + 4;
+  __shared__ float hal[FL_CC][HY][RS];
+  __shared__ float wsh[FL_CC][9];
+  const int tid = threadIdx.x;
+  const int tiles_x = (W + FL_TW - 1) / FL_TW;
+  const int ty0 = (blockIdx.x / tiles_x) * FL_TH, tx0 = (blockIdx.x % tiles_x) * FL_TW;
+  const int bq = blockIdx.y, bs = bq / clones;
+  const int ly = tid / 16, lx = (tid % 16) * 4;   // 16 rows x 16 threads, 4 px each
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  const int H2 = H / 2, W2 = W / 2;
+  for (int c0 = 0; c0 < C; c0 += FL_CC) {
+    __syncthreads();
+    for (int idx = tid; idx < FL_CC * HY * HX; idx += 256) {
+      const int ci = idx / (HY * HX), rem = idx % (HY * HX);
+      const int hy = rem / HX, hx = rem % HX;
+      const int gy = ty0 - 1 + hy, gx = tx0 - 1 + hx, c = c0 + ci;
+      float v = 0.f;
+      if (c < C && gy >= 0 && gy < H && gx >= 0 && gx < W) {
+        if (amax) {
+          const size_t q = (((size_t)bq * C + c) * H2 + (gy >> 1)) * W2 + (gx >> 1);
+          const size_t qa = (((size_t)bs * C + c) * H2 + (gy >> 1)) * W2 + (gx >> 1);
+          v = (amax[qa] == (((gy & 1) << 1) | (gx & 1))) ? g[q] : 0.f;
+        } else {
+          v = g[(((size_t)bq * C + c) * H + gy) * W + gx];
+        }
+      }
+      hal[ci][hy][hx] = v;
+    }
+    for (int idx = tid; idx < FL_CC * 9; idx += 256) {
+      const int ci = idx / 9, t = idx % 9;
+      wsh[ci][t] = (c0 + ci < C) ? w2[(c0 + ci) * 9 + t] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ci = 0; ci < FL_CC; ++ci) {
+#pragma unroll
+      for (int dy = -1; dy <= 1; ++dy) {
+        float row[6];
+#pragma unroll
+        for (int e = 0; e < 6; ++e) row[e] = hal[ci][ly + 1 + dy][lx + e];
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+          const float wv = wsh[ci][(1 - dy) * 3 + (1 - dx)];
+#pragma unroll
+          for (int p = 0; p < 4; ++p) acc[p] = fmaf(row[p + 1 + dx], wv, acc[p]);
+        }
+      }
+    }
+  }
+  const int y = ty0 + ly;
+  if (y < H) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int x = tx0 + lx + p;
+      if (x < W) out[((size_t)bq * H + y) * W + x] = acc[p];
+    }
+  }
+}
+
+// den[co][y][x] = sum_ci sum_{in-bounds taps} w2[co][ci][ky][kx] * 1 + b2[co]
+__global__ void first_layer_den_kernel(const float* __restrict__ w2, const float* __restrict__ b2, float* __restrict__ den,
+                                       int C, int CI, int H, int W) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)C * H * W) return;
+  const int co = (int)(i / ((size_t)H * W));
+  const int y = (int)((i / W) % H), x = (int)(i % W);
+  float acc = 0.f;
+  for (int ci = 0; ci < CI; ++ci)
+    for (int ky = 0; ky < 3; ++ky)
+      for (int kx = 0; kx < 3; ++kx) {
+        const int yy = y + ky - 1, xx = x + kx - 1;
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W) acc = fmaf(1.f, w2[((co * CI + ci) * 3 + ky) * 3 + kx], acc);
+      }
+  den[i] = acc + (b2 ? b2[co] : 0.f);
+}
+
+// ===========================================================================
+// heatmap finalisation (per sample): hm [B][K+1][H*W]
+//   std_out [B][HW], std_rel [B], sub_out [B][K][HW] sorted by descending relevance,
+//   rel [B][K] sorted, mask [B][K] int64 (numpy argsort(...)[..., ::-1] semantics:
+//   stable ascending order reversed, i.e. ties -> larger index first)
+// ===========================================================================
+__global__ __launch_bounds__(256) void heatmap_sort_kernel(const float* __restrict__ hm, int K, int HW,
+                                                           float* __restrict__ std_out, float* __restrict__ std_rel,
+                                                           float* __restrict__ sub_out, float* __restrict__ rel,
+                                                           int64_t* __restrict__ mask) {
+  __shared__ float red[4];
+  __shared__ float sums[65];
+  __shared__ int order[64];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float* base = hm + (size_t)b * (K + 1) * HW;
+  for (int q = 0; q <= K; ++q) {
+    const float* src = base + (size_t)q * HW;
+    float s = 0.f;
+    for (int i = tid * 4; i < HW; i += 256 * 4) {
+      const float4 v = *reinterpret_cast<const float4*>(src + i);
+      s += (v.x + v.y) + (v.z + v.w);
+    }
+    for (int m = 32; m >= 1; m >>= 1) s += shfl_xor(s, m);
+    __syncthreads();
+    if (lane_id() == 0) red[wave_id()] = s;
+    __syncthreads();
+    if (tid == 0) sums[q] = (red[0] + red[1]) + (red[2] + red[3]);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    // descending; ties: larger original index first
+    for (int k = 0; k < K; ++k) order[k] = k;
+    for (int i = 1; i < K; ++i) {
+      const int cur = order[i];
+      int j = i - 1;
+      while (j >= 0) {
+        const float a = sums[1 + order[j]], c = sums[1 + cur];
+        const bool before = (c > a) || (c == a && cur > order[j]);
+        if (!before) break;
+        order[j + 1] = order[j];
+        --j;
+      }
+      order[j + 1] = cur;
+    }
+    std_rel[b] = sums[0];
+    for (int k = 0; k < K; ++k) {
+      rel[(size_t)b * K + k] = sums[1 + order[k]];
+      mask[(size_t)b * K + k] = order[k];
+    }
+  }
+  __syncthreads();
+  for (int i = tid * 4; i < HW; i += 256 * 4)
+    *reinterpret_cast<float4*>(std_out + (size_t)b * HW + i) = *reinterpret_cast<const float4*>(base + i);
+  for (int k = 0; k < K; ++k) {
+    const float* src = base + (size_t)(1 + order[k]) * HW;
+    float* dst = sub_out + ((size_t)b * K + k) * HW;
+    for (int i = tid * 4; i < HW; i += 256 * 4)
+      *reinterpret_cast<float4*>(dst + i) = *reinterpret_cast<const float4*>(src + i);
+  }
+}
+
+template <typename F>
+int with_lds(F* fn, size_t lds) {
+  DRSA_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  return DRSA_OK;
+}
+
+template <int D>
+size_t proj_fwd_lds() { return ((size_t)D * (D + 1) + D * 64 + 64 * (D + 1)) * sizeof(float); }
+template <int D>
+size_t proj_bwd_lds() { return ((size_t)D * (D + 1) + D * 64 + 64 * (D + 1)) * sizeof(float); }
+
+}  // namespace
+
+extern "C" {
+
+int drsa_amd_linear_fwd(const float* x, const float* Wt, const float* bias, float* z_out, float* relu_out, int M,
+                        int N, int K, void* stream) {
+  DRSA_REQUIRE(M > 0 && N > 0 && K > 0, "linear_fwd: bad shape");
+  LinArgs a{};
+  a.A = x; a.W = Wt; a.bias = bias; a.out = z_out; a.out_relu = relu_out; a.M = M; a.N = N; a.K = K; a.bwd = 0;
+  hipLaunchKernelGGL(linear_kernel, dim3((M + LT - 1) / LT, (N + LT - 1) / LT), dim3(256), 0, (hipStream_t)stream, a);
+  DRSA_LAUNCH_CHECK();
+  return DRSA_OK;
+}
+
+// out[M][Kin] = epi( g[M][Nout] W[Nout][Kin] ),  g = prologue(R or seed, z)
+int drsa_amd_linear_bwd(const float* R, const int* seed_cls, int one_hot, const float* z, int relu_mask, int rule_eps,
+                        float eps, const float* Wt, const float* x, int xmode, const float* den, int post,
+                        float eps_post, float* out, int M, int Nout, int Kin, void* stream) {
+  DRSA_REQUIRE(M > 0 && Nout > 0 && Kin > 0, "linear_bwd: bad shape");
+  DRSA_REQUIRE(R || seed_cls, "linear_bwd: need R or a seed");
+  DRSA_REQUIRE(xmode == XM_NONE || x, "linear_bwd: xmode needs x");
+  DRSA_REQUIRE(post == POST_NONE || (x && (den || post == POST_MASK)), "linear_bwd: POST_DIV needs x and den");
+  LinArgs a{};
+  a.A = R; a.cls = seed_cls; a.one_hot = one_hot; a.z = z; a.relu_mask = relu_mask; a.rule_eps = rule_eps;
+  a.eps = eps; a.W = Wt; a.x = x; a.xmode = xmode; a.den = den; a.post = post; a.eps_post = eps_post; a.out = out;
+  a.M = M; a.N = Kin; a.K = Nout; a.bwd = 1;
+  hipLaunchKernelGGL(linear_kernel, dim3((M + LT - 1) / LT, (Kin + LT - 1) / LT), dim3(256), 0, (hipStream_t)stream, a);
+  DRSA_LAUNCH_CHECK();
+  return DRSA_OK;
+}
+
+int drsa_amd_projection_fwd(const float* a, const float* U, float* h, float* ap, float* pooled, uint8_t* amax, int B,
+                            int D, int H, int W, int pool, void* stream) {
+  DRSA_REQUIRE(H % 8 == 0 && W % 8 == 0, "projection_fwd: H, W must be multiples of 8");
+  DRSA_REQUIRE(!pool || (pooled && amax), "projection_fwd: pool needs outputs");
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((H / 8) * (W / 8), B);
+  switch (D) {
+#define PF(DD)                                                                                        \
+  case DD: {                                                                                          \
+    static bool set = false;                                                                          \
+    if (!set) { int rc = with_lds(projection_fwd_kernel<DD>, proj_fwd_lds<DD>()); if (rc) return rc; set = true; } \
+    hipLaunchKernelGGL(projection_fwd_kernel<DD>, grid, dim3(256), proj_fwd_lds<DD>(), s, a, U, h, ap, pooled, amax, \
+                       H, W, pool);                                                                   \
+    break;                                                                                            \
+  }
+    PF(16) PF(32) PF(64) PF(128)
+#undef PF
+    default:
+      drsa::set_error("projection_fwd: unsupported d=%d", D);
+      return DRSA_EUNSUPPORTED;
+  }
+  DRSA_LAUNCH_CHECK();
+  return DRSA_OK;
+}
+
+int drsa_amd_projection_bwd(const float* gp, const uint8_t* amax, const float* ap, const float* h, const float* a,
+                            const float* den, const float* U, float* G, int B, int D, int H, int W, int K,
+                            float eps_proj, float eps_den, int fanout, void* stream) {
+  DRSA_REQUIRE(H % 8 == 0 && W % 8 == 0, "projection_bwd: H, W must be multiples of 8");
+  DRSA_REQUIRE(K > 0 && D % K == 0, "projection_bwd: K must divide d");
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((H / 8) * (W / 8), B);
+  const int sparse = amax != nullptr, has_den = den != nullptr;
+  switch (D) {
+#define PB(DD)                                                                                        \
+  case DD: {                                                                                          \
+    static bool set = false;                                                                          \
+    if (!set) { int rc = with_lds(projection_bwd_kernel<DD>, proj_bwd_lds<DD>()); if (rc) return rc; set = true; } \
+    hipLaunchKernelGGL(projection_bwd_kernel<DD>, grid, dim3(256), proj_bwd_lds<DD>(), s, gp, amax, ap, h, a, den, U, \
+                       G, H, W, K, eps_proj, eps_den, sparse, has_den, fanout);                               \
+    break;                                                                                            \
+  }
+    PB(16) PB(32) PB(64) PB(128)
+#undef PB
+    default:
+      drsa::set_error("projection_bwd: unsupported d=%d", D);
+      return DRSA_EUNSUPPORTED;
+  }
+  DRSA_LAUNCH_CHECK();
+  return DRSA_OK;
+}
+
+int drsa_amd_first_layer_bwd(const float* g, const uint8_t* amax, const float* w2f, float* out, int Bq, int clones,
+                             int C, int H, int W, void* stream) {
+  DRSA_REQUIRE(Bq > 0 && clones > 0 && Bq % clones == 0, "first_layer_bwd: bad batch");
+  const dim3 grid(((H + FL_TH - 1) / FL_TH) * ((W + FL_TW - 1) / FL_TW), Bq);
+  hipLaunchKernelGGL(first_layer_bwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, g, amax, w2f, out, C, H, W,
+                     clones);
+  DRSA_LAUNCH_CHECK();
+  return DRSA_OK;
+}
+
+int drsa_amd_first_layer_den(const float* w2, const float* b2, float* den, int C, int CI, int H, int W, void* stream) {
+  const size_t n = (size_t)C * H * W;
+  hipLaunchKernelGGL(first_layer_den_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, w2,
+                     b2, den, C, CI, H, W);
+  DRSA_LAUNCH_CHECK();
+  return DRSA_OK;
+}
+
+int drsa_amd_heatmap_sort(const float* hm, int B, int K, int HW, float* std_out, float* std_rel, float* sub_out,
+                          float* rel, int64_t* mask, void* stream) {
+  DRSA_REQUIRE(K >= 1 && K <= 64, "heatmap_sort: K must be in [1, 64]");
+  DRSA_REQUIRE(HW % 4 == 0, "heatmap_sort: H*W must be a multiple of 4");
+  hipLaunchKernelGGL(heatmap_sort_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, hm, K, HW, std_out, std_rel,
+                     sub_out, rel, mask);
+  DRSA_LAUNCH_CHECK();
+  return DRSA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,525 @@
+"""LRP kernel plan: compile (model, composite) once, then run batches through HIP kernels.
+
+The reference attaches zennit hooks and lets autograd re-run 1-5 modified forwards per
+layer (attribute.py:98-107).  Here the sequential VGG structure (create_model.py:8-97,
+optionally with the ProjectionModel virtual layers, modify_model.py:19-60) is compiled
+into *stages*:
+
+  ConvStage   Conv2d [+BN folded by SequentialMergeBatchNorm] -> ReLU
+              [-> Projection/SubspaceFilter/InvProjection] [-> MaxPool2d(2)]
+  DenseStage  Linear [+BN folded] [-> ReLU] [-> Dropout]
+
+Forward: one ``drsa_amd_conv_fwd`` per conv stage computes y = pool(relu(conv)), the pool
+argmax and the rule's denominator at the argmax (the only place relevance arrives).
+Backward: one ``drsa_amd_conv_bwd`` per conv stage, the max-pool/ReLU backward folded
+into its input, the next lower layer's division folded into its output.  The subspace
+path fans one forward out into K+1 relevance clones at the projection
+(``drsa_amd_projection_bwd``), instead of replicating the batch K+1 times
+(explainer.py:92).
+
+Weights are prepared on the device once per plan (rule-modified, flipped/transposed for
+the backward, padded to the kernels' channel tiles).  Activation buffers are cached per
+batch size.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from .. import _capi
+from .._capi import POST_DIV, POST_MASK, POST_NONE, XM_MUL, XM_NONE, XM_SPLIT
+from ..zennit import rules as R
+from ..zennit.canonizers import SequentialMergeBatchNorm
+
+
+def _pad32(c: int) -> int:
+    return (c + 31) // 32 * 32
+
+
+def _cin_pad(c: int) -> int:
+    return 1 if c == 1 else _pad32(c)
+
+
+def _kind(rule) -> Optional[str]:
+    return None if rule is None else getattr(rule, "kind", type(rule).__name__)
+
+
+@dataclass
+class ProjGroup:
+    U: torch.Tensor
+    K: int
+    eps_inv: float
+    eps_proj: float
+    mask: bool          # SubspaceHook on the filter
+    pool_after: bool
+
+
+@dataclass
+class ConvStage:
+    name: str
+    cin: int
+    cout: int
+    rule_kind: Optional[str]
+    eps: float
+    pool: bool
+    proj: Optional[ProjGroup]
+    input_nonneg: bool
+    W: torch.Tensor = None
+    b: torch.Tensor = None
+    rule: object = None
+    # prepared
+    ng_fwd: int = 1
+    wts_fwd: torch.Tensor = None
+    bias3: torch.Tensor = None
+    den_kind: Optional[str] = None       # "gamma" | "eps" | "map" | None
+    ng_bwd: int = 1
+    wts_bwd: torch.Tensor = None
+    xmode_bwd: int = XM_NONE
+    w2_first: Optional[torch.Tensor] = None
+    den_maps: Dict[Tuple[int, int], torch.Tensor] = field(default_factory=dict)
+
+
+@dataclass
+class DenseStage:
+    name: str
+    W: torch.Tensor
+    b: Optional[torch.Tensor]
+    rule_kind: Optional[str]
+    eps: float
+    relu_after: bool
+
+
+class EngineError(NotImplementedError):
+    pass
+
+
+class LRPEngine:
+    def __init__(self, model: nn.Module, composite, device: Optional[torch.device] = None):
+        _capi.load()
+        self.model = model
+        self.composite = composite
+        p0 = next(model.parameters())
+        self.device = device or p0.device
+        if self.device.type != "cuda":
+            raise _capi.DrsaAmdError("the LRP engine runs on the GPU only; move the model to a HIP device")
+        rules = composite.rules(model) if composite is not None else {}
+        self.rules = rules
+        merge_bn = any(isinstance(c, SequentialMergeBatchNorm) for c in getattr(composite, "canonizers", []))
+        self.stages: List[ConvStage] = []
+        self.dense: List[DenseStage] = []
+        self._parse(model, rules, merge_bn)
+        for st in self.stages:
+            self._prepare_conv(st)
+        self._buffers: Dict[tuple, dict] = {}
+        self.last: Optional[dict] = None
+
+    # ------------------------------------------------------------------ parse
+    def _parse(self, model, rules, merge_bn):
+        feats = list(model.features.named_children())
+        i, n = 0, len(feats)
+        prev_nonneg = False          # raw network input may be negative
+        while i < n:
+            name, m = feats[i]
+            if isinstance(m, (nn.Dropout, nn.Identity)):
+                i += 1
+                continue
+            if not isinstance(m, nn.Conv2d):
+                raise EngineError(f"engine: unexpected feature layer features.{name} ({type(m).__name__})")
+            self._check_conv(m, name)
+            W = m.weight.detach().to(self.device, torch.float32)
+            b = (m.bias.detach().to(self.device, torch.float32) if m.bias is not None
+                 else torch.zeros(m.out_channels, device=self.device))
+            j = i + 1
+            if j < n and isinstance(feats[j][1], nn.BatchNorm2d):
+                if not merge_bn:
+                    raise EngineError("BatchNorm2d in the trunk needs the SequentialMergeBatchNorm canonizer")
+                W, b = SequentialMergeBatchNorm.fold(W, b, _bn_to(feats[j][1], self.device))
+                j += 1
+            if j >= n or not isinstance(feats[j][1], nn.ReLU):
+                raise EngineError(f"engine: conv features.{name} must be followed by ReLU")
+            self._rule_ok_on_activation(rules.get(f"features.{feats[j][0]}"))
+            j += 1
+            proj = None
+            if j < n and type(feats[j][1]).__name__ == "Projection":
+                if not (j + 2 < n and type(feats[j + 1][1]).__name__ == "SubspaceFilter"
+                        and type(feats[j + 2][1]).__name__ == "InvProjection"):
+                    raise EngineError("engine: Projection must be followed by SubspaceFilter, InvProjection")
+                pm, fm, im = feats[j][1], feats[j + 1][1], feats[j + 2][1]
+                r_p = rules.get(f"features.{feats[j][0]}")
+                r_f = rules.get(f"features.{feats[j + 1][0]}")
+                r_i = rules.get(f"features.{feats[j + 2][0]}")
+                if _kind(r_p) != "epsilon" or _kind(r_i) != "epsilon":
+                    raise EngineError("engine: projection layers need Epsilon rules (get_class_composite)")
+                if r_f is not None and type(r_f).__name__ != "SubspaceHook":
+                    raise EngineError("engine: only SubspaceHook is supported on the subspace filter")
+                U = pm.U.detach().to(self.device, torch.float32).contiguous()
+                proj = ProjGroup(U=U, K=int(pm.num_concepts), eps_inv=r_i.epsilon, eps_proj=r_p.epsilon,
+                                 mask=r_f is not None, pool_after=False)
+                if r_f is not None and int(r_f.num_concepts) != proj.K:
+                    raise EngineError("engine: SubspaceHook num_concepts differs from the projection")
+                j += 3
+            pool = False
+            if j < n and isinstance(feats[j][1], nn.MaxPool2d):
+                self._check_pool(feats[j][1])
+                self._rule_ok_on_activation(rules.get(f"features.{feats[j][0]}"))
+                pool = True
+                j += 1
+            if proj is not None:
+                proj.pool_after = pool
+            rule = rules.get(f"features.{name}")
+            kind = _kind(rule)
+            if kind not in (None, "epsilon", "gamma", "wsquare", "flat"):
+                raise EngineError(f"engine: rule {type(rule).__name__} on conv features.{name} is not supported yet")
+            eps = {None: 0.0, "epsilon": getattr(rule, "epsilon", 0.0), "gamma": getattr(rule, "stabilizer", 0.0),
+                   "wsquare": getattr(rule, "stabilizer", 0.0), "flat": getattr(rule, "stabilizer", 0.0)}[kind]
+            st = ConvStage(name=f"features.{name}", cin=m.in_channels, cout=m.out_channels, rule_kind=kind,
+                           eps=float(eps), pool=pool, proj=proj, input_nonneg=prev_nonneg, W=W, b=b, rule=rule)
+            self.stages.append(st)
+            prev_nonneg = proj is None      # outputs are post-ReLU (pooled) unless a' follows
+            i = j
+        # classifier
+        cl = list(model.classifier.named_children())
+        i, n = 0, len(cl)
+        while i < n:
+            name, m = cl[i]
+            if isinstance(m, (nn.Dropout, nn.Identity)):
+                i += 1
+                continue
+            if not isinstance(m, nn.Linear):
+                raise EngineError(f"engine: unexpected classifier layer classifier.{name} ({type(m).__name__})")
+            W = m.weight.detach().to(self.device, torch.float32)
+            b = m.bias.detach().to(self.device, torch.float32) if m.bias is not None else None
+            j = i + 1
+            if j < n and isinstance(cl[j][1], nn.BatchNorm1d):
+                if not merge_bn:
+                    raise EngineError("BatchNorm1d in the head needs the SequentialMergeBatchNorm canonizer")
+                W, b = SequentialMergeBatchNorm.fold(W, b, _bn_to(cl[j][1], self.device))
+                j += 1
+            relu = False
+            while j < n and isinstance(cl[j][1], (nn.ReLU, nn.Dropout)):
+                if isinstance(cl[j][1], nn.ReLU):
+                    relu = True
+                    self._rule_ok_on_activation(rules.get(f"classifier.{cl[j][0]}"))
+                j += 1
+            rule = rules.get(f"classifier.{name}")
+            kind = _kind(rule)
+            if kind not in (None, "epsilon"):
+                raise EngineError(f"engine: rule {type(rule).__name__} on classifier.{name} is not supported yet")
+            if rule is not None and "bias" in getattr(rule, "zero_params", ()):
+                raise EngineError("engine: zero_params on dense layers is not supported yet")
+            self.dense.append(DenseStage(name=f"classifier.{name}", W=W.contiguous(),
+                                         b=None if b is None else b.contiguous(), rule_kind=kind,
+                                         eps=float(getattr(rule, "epsilon", 0.0)), relu_after=relu))
+            i = j
+        if not self.stages or not self.dense:
+            raise EngineError("engine: model must have a conv trunk and a dense head")
+
+    @staticmethod
+    def _check_conv(m: nn.Conv2d, name):
+        pad = m.padding
+        ok = (tuple(m.kernel_size) == (3, 3) and tuple(m.stride) == (1, 1) and tuple(m.dilation) == (1, 1)
+              and m.groups == 1 and (pad == "same" or tuple(pad) == (1, 1)) and m.padding_mode == "zeros")
+        if not ok:
+            raise EngineError(f"engine: features.{name} must be a 3x3 stride-1 'same' zero-padded conv")
+
+    @staticmethod
+    def _check_pool(m: nn.MaxPool2d):
+        ks = m.kernel_size if isinstance(m.kernel_size, tuple) else (m.kernel_size, m.kernel_size)
+        st = m.stride if isinstance(m.stride, tuple) else (m.stride, m.stride)
+        pd = m.padding if isinstance(m.padding, tuple) else (m.padding, m.padding)
+        dl = m.dilation if isinstance(m.dilation, tuple) else (m.dilation, m.dilation)
+        if tuple(ks) != (2, 2) or tuple(st) != (2, 2) or tuple(pd) != (0, 0) or tuple(dl) != (1, 1) or m.ceil_mode:
+            raise EngineError(f"engine: only MaxPool2d(2) is supported yet (got kernel {ks})")
+
+    @staticmethod
+    def _rule_ok_on_activation(rule):
+        if rule is not None and _kind(rule) != "pass":
+            raise EngineError(f"engine: rule {type(rule).__name__} on an activation/pool layer is not supported")
+
+    # ---------------------------------------------------------------- prepare
+    @torch.no_grad()
+    def _prepare_conv(self, st: ConvStage):
+        dev = self.device
+        W, b = st.W, st.b
+        cin_p, cout_p = _cin_pad(st.cin), _pad32(st.cout)
+        zero_bias = "bias" in getattr(st.rule, "zero_params", ())
+        bd = torch.zeros_like(b) if zero_bias else b
+
+        def fwd_layout(Wx):   # [cout][cin][3][3] -> [9*cin_p][cout_p]
+            t = torch.zeros(3, 3, cin_p, cout_p, device=dev)
+            t[:, :, :st.cin, :st.cout] = Wx.permute(2, 3, 1, 0)
+            return t.reshape(9 * cin_p, cout_p)
+
+        def bwd_layout(Wx):   # transposed conv: [9*cout_p][pad32(cin)], flipped taps
+            cin_o = _pad32(st.cin)
+            t = torch.zeros(3, 3, cout_p, cin_o, device=dev)
+            t[:, :, :st.cout, :st.cin] = Wx.flip(2, 3).permute(2, 3, 0, 1)
+            return t.reshape(9 * cout_p, cin_o)
+
+        bias3 = torch.zeros(3, cout_p, device=dev)
+        bias3[0, :st.cout] = b
+        k = st.rule_kind
+        if k == "gamma":
+            g = st.rule.gamma
+            Wp, Wn = W + g * W.clamp(min=0), W + g * W.clamp(max=0)
+            bp, bn = bd + g * bd.clamp(min=0), bd + g * bd.clamp(max=0)
+            bias3[1, :st.cout], bias3[2, :st.cout] = bp, bn
+            sets = [W, Wp] + ([Wn] if not st.input_nonneg else [])
+            st.ng_fwd = len(sets)
+            st.den_kind = "gamma"
+            if st.input_nonneg:
+                st.ng_bwd, st.xmode_bwd, bsets = 1, XM_MUL, [Wp]
+            else:
+                st.ng_bwd, st.xmode_bwd, bsets = 2, XM_SPLIT, [Wp, Wn]
+        elif k == "epsilon":
+            bias3[1, :st.cout] = bd
+            sets, st.ng_fwd, st.den_kind = [W], 1, "eps"
+            st.ng_bwd, st.xmode_bwd, bsets = 1, XM_MUL, [W]
+        elif k in ("wsquare", "flat"):
+            if k == "wsquare":
+                W2, b2 = W * W, bd * bd
+            else:
+                W2, b2 = torch.ones_like(W), torch.zeros_like(b)
+            st.W2, st.b2 = W2.contiguous(), b2.contiguous()
+            sets, st.ng_fwd, st.den_kind = [W], 1, "map"
+            st.ng_bwd, st.xmode_bwd, bsets = 1, XM_NONE, [W2]
+            if st.cin == 1:
+                st.w2_first = W2.reshape(st.cout, 9).contiguous()
+        else:   # no rule: plain gradient
+            sets, st.ng_fwd, st.den_kind = [W], 1, None
+            st.ng_bwd, st.xmode_bwd, bsets = 1, XM_NONE, [W]
+        st.wts_fwd = torch.stack([fwd_layout(s) for s in sets]).contiguous()
+        st.bias3 = bias3.contiguous()
+        st.wts_bwd = torch.stack([bwd_layout(s) for s in bsets]).contiguous()
+        if st.proj is not None and st.proj.U.size(0) != st.cout:
+            raise EngineError("engine: projection width differs from the conv channels")
+
+    def _den_map(self, st: ConvStage, H: int, W: int) -> torch.Tensor:
+        key = (H, W)
+        if key not in st.den_maps:
+            den = torch.empty(st.cout, H, W, device=self.device)
+            _capi.call("drsa_amd_first_layer_den", st.W2.data_ptr(), st.b2.data_ptr(), den.data_ptr(), st.cout,
+                       st.cin, H, W, _capi.stream_ptr(self.device))
+            st.den_maps[key] = den
+        return st.den_maps[key]
+
+    # ---------------------------------------------------------------- buffers
+    def _buf(self, key, shape, dtype=torch.float32):
+        t = self._cur_bufs.get(key)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+            t = torch.empty(shape, dtype=dtype, device=self.device)
+            self._cur_bufs[key] = t
+        return t
+
+    # ---------------------------------------------------------------- forward
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """Model forward with all LRP state (argmax, denominators) kept on device."""
+        _capi.require_gpu(x, "input", dtype=None)
+        x = x.detach().to(torch.float32).contiguous()
+        if x.dim() != 4 or x.size(1) != self.stages[0].cin:
+            raise ValueError(f"input must be [B, {self.stages[0].cin}, H, W]")
+        B, _, H, W = x.shape
+        self._cur_bufs = self._buffers.setdefault(("fwd", B, H, W), {})
+        s = _capi.stream_ptr(self.device)
+        state = {"B": B, "input": x, "stages": []}
+        cur, h, w = x, H, W
+        for li, st in enumerate(self.stages):
+            if h % 2 or w % 2:
+                raise ValueError(f"{st.name}: feature map {h}x{w} must have even sides")
+            rec = {"in": cur, "H": h, "W": w}
+            den_map = self._den_map(st, h, w) if st.den_kind == "map" else None
+            need_den = st.den_kind is not None
+            if st.proj is None and st.pool:
+                out = self._buf((li, "y"), (B, st.cout, h // 2, w // 2))
+                amax = self._buf((li, "amax"), (B, st.cout, h // 2, w // 2), torch.uint8)
+                den = self._buf((li, "den"), (B, st.cout, h // 2, w // 2)) if need_den else None
+                _capi.call("drsa_amd_conv_fwd", cur.data_ptr(), st.wts_fwd.data_ptr(), st.bias3.data_ptr(),
+                           _capi.ptr(den_map), out.data_ptr(), amax.data_ptr(), _capi.ptr(den), B, st.cin, st.cout,
+                           h, w, st.ng_fwd, 1, s)
+                rec.update(y=out, amax=amax, den=den, Hout=h // 2, Wout=w // 2)
+                cur, h, w = out, h // 2, w // 2
+            else:
+                a = self._buf((li, "a"), (B, st.cout, h, w))
+                den = self._buf((li, "den"), (B, st.cout, h, w)) if need_den else None
+                _capi.call("drsa_amd_conv_fwd", cur.data_ptr(), st.wts_fwd.data_ptr(), st.bias3.data_ptr(),
+                           _capi.ptr(den_map), a.data_ptr(), None, _capi.ptr(den), B, st.cin, st.cout, h, w,
+                           st.ng_fwd, 0, s)
+                rec.update(a=a, den=den)
+                if st.proj is not None:
+                    P = st.proj
+                    hb = self._buf((li, "h"), (B, h * w, st.cout))
+                    ap = self._buf((li, "ap"), (B, st.cout, h, w))
+                    if P.pool_after:
+                        pooled = self._buf((li, "y"), (B, st.cout, h // 2, w // 2))
+                        amax = self._buf((li, "amax"), (B, st.cout, h // 2, w // 2), torch.uint8)
+                    else:
+                        pooled = amax = None
+                    _capi.call("drsa_amd_projection_fwd", a.data_ptr(), P.U.data_ptr(), hb.data_ptr(), ap.data_ptr(),
+                               _capi.ptr(pooled), _capi.ptr(amax), B, st.cout, h, w, 1 if P.pool_after else 0, s)
+                    rec.update(h=hb, ap=ap, amax=amax)
+                    if P.pool_after:
+                        rec.update(y=pooled, Hout=h // 2, Wout=w // 2)
+                        cur, h, w = pooled, h // 2, w // 2
+                    else:
+                        rec.update(y=ap, Hout=h, Wout=w)
+                        cur = ap
+                else:
+                    rec.update(y=a, Hout=h, Wout=w)
+                    cur = a
+            state["stages"].append(rec)
+        flat = cur.reshape(B, -1)
+        if flat.size(1) != self.dense[0].W.size(1):
+            raise ValueError(f"flattened trunk output {flat.size(1)} != classifier input {self.dense[0].W.size(1)}")
+        state["flat"] = flat
+        dense_recs = []
+        inp = flat
+        for di, ds in enumerate(self.dense):
+            N, Kd = ds.W.shape
+            z = self._buf(("d", di, "z"), (B, N))
+            act = self._buf(("d", di, "a"), (B, N)) if ds.relu_after else None
+            _capi.call("drsa_amd_linear_fwd", inp.data_ptr(), ds.W.data_ptr(), _capi.ptr(ds.b), z.data_ptr(),
+                       _capi.ptr(act), B, N, Kd, s)
+            dense_recs.append({"x": inp, "z": z, "a": act})
+            inp = act if act is not None else z
+        state["dense"] = dense_recs
+        self.last = state
+        return dense_recs[-1]["z"]
+
+    # --------------------------------------------------------------- backward
+    def _post_for(self, li: int):
+        """(post, den, eps) for relevance arriving at the OUTPUT of conv stage li."""
+        st = self.stages[li]
+        rec = self.last["stages"][li]
+        if st.proj is not None:
+            return POST_NONE, None, 0.0
+        if st.den_kind is None:
+            return POST_MASK, None, 0.0
+        return POST_DIV, rec["den"], st.eps
+
+    @torch.no_grad()
+    def backward(self, seed: Optional[torch.Tensor] = None, cls: Optional[torch.Tensor] = None,
+                 one_hot: bool = False, fanout: bool = False) -> torch.Tensor:
+        """Relevance at the input.  ``seed`` [B, n_out] (output relevance) or ``cls`` [B] int32
+        (lrp_output_modifier semantics).  ``fanout``: the projection stage emits K+1 clones per
+        sample (HeatmapGenerator path); otherwise rows are treated as the reference's
+        replicated batch."""
+        st0 = self.last
+        if st0 is None:
+            raise RuntimeError("backward() before forward()")
+        B = st0["B"]
+        s = _capi.stream_ptr(self.device)
+        self._cur_bufs = self._buffers.setdefault(("bwd", B, fanout), {})
+        # ---- dense head, top-down ----
+        L = len(self.stages)
+        R = seed
+        for di in range(len(self.dense) - 1, -1, -1):
+            ds, rec = self.dense[di], st0["dense"][di]
+            N, Kd = ds.W.shape
+            out = self._buf(("d", di), (B, Kd))
+            post, den, eps_post = POST_NONE, None, 0.0
+            if di == 0:
+                post, den, eps_post = self._post_for(L - 1)
+                x_mask = rec["x"]
+            else:
+                x_mask = rec["x"]
+            relu_mask = 1 if ds.relu_after else 0
+            xmode = XM_MUL if ds.rule_kind == "epsilon" else XM_NONE
+            den_flat = None if den is None else den.reshape(B, -1)
+            if di == len(self.dense) - 1 and cls is not None:
+                _capi.call("drsa_amd_linear_bwd", None, cls.data_ptr(), 1 if one_hot else 0, rec["z"].data_ptr(),
+                           relu_mask, 1 if ds.rule_kind == "epsilon" else 0, ds.eps, ds.W.data_ptr(),
+                           x_mask.data_ptr(), xmode, _capi.ptr(den_flat), post, eps_post, out.data_ptr(), B, N, Kd, s)
+            else:
+                if R is None:
+                    raise ValueError("backward needs a seed or class indices")
+                R = R.to(self.device, torch.float32).contiguous()
+                _capi.call("drsa_amd_linear_bwd", R.data_ptr(), None, 0, rec["z"].data_ptr(), relu_mask,
+                           1 if ds.rule_kind == "epsilon" else 0, ds.eps, ds.W.data_ptr(), x_mask.data_ptr(), xmode,
+                           _capi.ptr(den_flat), post, eps_post, out.data_ptr(), B, N, Kd, s)
+            R = out
+        # ---- conv trunk, top-down ----
+        g = R.reshape(B, self.stages[-1].cout, st0["stages"][-1]["Hout"], st0["stages"][-1]["Wout"])
+        clones, Bq = 1, B
+        for li in range(L - 1, -1, -1):
+            st, rec = self.stages[li], st0["stages"][li]
+            h, w = rec["H"], rec["W"]
+            amax_in = None
+            if st.proj is not None:
+                P = st.proj
+                K = P.K if P.mask else P.K
+                fan = fanout and P.mask
+                nq = (K + 1) if fan else 1
+                G = self._buf((li, "G"), (B * nq, st.cout, h, w))
+                post, den, eps = (POST_DIV, rec["den"], st.eps) if st.den_kind is not None else (POST_MASK, None, 0.0)
+                if not P.mask:
+                    raise EngineError("engine: projection without SubspaceHook is not supported yet")
+                _capi.call("drsa_amd_projection_bwd", g.data_ptr(), _capi.ptr(rec["amax"] if P.pool_after else None),
+                           rec["ap"].data_ptr(), rec["h"].data_ptr(), rec["a"].data_ptr(),
+                           _capi.ptr(den if post == POST_DIV else None), P.U.data_ptr(), G.data_ptr(), B, st.cout,
+                           h, w, K, P.eps_inv, eps, 1 if fan else 0, s)
+                g, clones, Bq = G, nq, B * nq
+            elif st.pool:
+                amax_in = rec["amax"]
+            # rule backward of conv li
+            x_in = rec["in"]
+            if li > 0:
+                post, den, eps = self._post_for(li - 1)
+            else:
+                post, den, eps = POST_NONE, None, 0.0
+            if li == 0 and st.w2_first is not None:
+                out = self._buf((li, "R"), (Bq, 1, h, w))
+                _capi.call("drsa_amd_first_layer_bwd", g.data_ptr(), _capi.ptr(amax_in), st.w2_first.data_ptr(),
+                           out.data_ptr(), Bq, clones, st.cout, h, w, s)
+            else:
+                out = self._buf((li, "R"), (Bq, st.cin, h, w))
+                _capi.call("drsa_amd_conv_bwd", g.data_ptr(), _capi.ptr(amax_in), st.wts_bwd.data_ptr(),
+                           x_in.data_ptr() if (st.xmode_bwd != XM_NONE or post != POST_NONE) else None,
+                           _capi.ptr(den), out.data_ptr(), Bq, clones, st.cout, st.cin, h, w, st.ng_bwd,
+                           st.xmode_bwd, post, float(eps), s)
+            g = out
+        return g
+
+    # -------------------------------------------------------------- heatmaps
+    @torch.no_grad()
+    def subspace_heatmaps(self, x: torch.Tensor, class_idx=None, cls: Optional[torch.Tensor] = None,
+                          one_hot: bool = False) -> dict:
+        """HeatmapGenerator.generate_subspace_heatmaps on device: one shared forward, the top
+        backward once, K+1 relevance clones below the projection, then split/sum/sort."""
+        proj = [st.proj for st in self.stages if st.proj is not None]
+        if len(proj) != 1 or not proj[0].mask:
+            raise EngineError("subspace heatmaps need exactly one projection group with a SubspaceHook")
+        K = proj[0].K
+        self.forward(x)
+        B = x.size(0)
+        if cls is None:
+            cls = torch.full((B,), int(class_idx), dtype=torch.int32, device=self.device)
+        hm = self.backward(cls=cls, one_hot=one_hot, fanout=True)     # [B*(K+1), 1, H, W]
+        H, W = hm.shape[-2:]
+        HW = H * W
+        out = {
+            "standard_heatmaps": torch.empty(B, 1, H, W, device=self.device),
+            "standard_relevance": torch.empty(B, device=self.device),
+            "subspace_heatmaps": torch.empty(B, K, H, W, device=self.device),
+            "subspace_relevances": torch.empty(B, K, device=self.device),
+            "mask": torch.empty(B, K, dtype=torch.int64, device=self.device),
+        }
+        _capi.call("drsa_amd_heatmap_sort", hm.data_ptr(), B, K, HW, out["standard_heatmaps"].data_ptr(),
+                   out["standard_relevance"].data_ptr(), out["subspace_heatmaps"].data_ptr(),
+                   out["subspace_relevances"].data_ptr(), out["mask"].data_ptr(), _capi.stream_ptr(self.device))
+        return out
+
+
+def _bn_to(bn, device):
+    class _B:   # detached fp32 copies of the BN statistics
+        pass
+    o = _B()
+    o.running_var = bn.running_var.detach().to(device, torch.float32)
+    o.running_mean = bn.running_mean.detach().to(device, torch.float32)
+    o.weight = (bn.weight.detach() if bn.weight is not None else torch.ones_like(bn.running_var)).to(device, torch.float32)
+    o.bias = (bn.bias.detach() if bn.bias is not None else torch.zeros_like(bn.running_var)).to(device, torch.float32)
+    o.eps = bn.eps
+    return o

@@ -1,0 +1,79 @@
+"""LRP rule descriptors with zennit 0.5.1 names and constructor signatures.
+
+Semantics (reference name maps ``constants.py:27-51``):
+  Epsilon(ε)   R_in = x ⊙ Jᵀ_W(R / stab_ε(z))
+  Gamma(γ, ε)  W± = W + γ·W.clamp(min/max=0) (bias likewise); positive/negative output split
+  WSquare(ε)   R_in = Jᵀ_{W²}(R / stab_ε(conv(1; W², b²)))
+  Flat(ε)      as WSquare with W -> 1, b -> 0
+  Pass()       R_in = R_out (activation layers only)
+``ZPlus``, ``AlphaBeta``, ``Norm`` are accepted as descriptors but not executed by the HIP
+engine yet (compiling a composite that maps them raises ``NotImplementedError``).
+"""
+from __future__ import annotations
+
+from .core import BasicHook, Stabilizer
+
+
+class Epsilon(BasicHook):
+    kind = "epsilon"
+
+    def __init__(self, epsilon=1e-6, zero_params=None):
+        super().__init__(zero_params)
+        self.epsilon = Stabilizer.ensure(epsilon).epsilon
+
+
+class Gamma(BasicHook):
+    kind = "gamma"
+
+    def __init__(self, gamma=0.25, stabilizer=1e-6, zero_params=None):
+        super().__init__(zero_params)
+        self.gamma = float(gamma)
+        self.stabilizer = Stabilizer.ensure(stabilizer).epsilon
+
+
+class WSquare(BasicHook):
+    kind = "wsquare"
+
+    def __init__(self, stabilizer=1e-6, zero_params=None):
+        super().__init__(zero_params)
+        self.stabilizer = Stabilizer.ensure(stabilizer).epsilon
+
+
+class Flat(BasicHook):
+    kind = "flat"
+
+    def __init__(self, stabilizer=1e-6, zero_params=None):
+        super().__init__(zero_params)
+        self.stabilizer = Stabilizer.ensure(stabilizer).epsilon
+
+
+class Pass(BasicHook):
+    kind = "pass"
+
+    def __init__(self):
+        super().__init__()
+
+
+class ZPlus(BasicHook):
+    kind = "zplus"
+
+    def __init__(self, stabilizer=1e-6, zero_params=None):
+        super().__init__(zero_params)
+        self.stabilizer = Stabilizer.ensure(stabilizer).epsilon
+
+
+class AlphaBeta(BasicHook):
+    kind = "alphabeta"
+
+    def __init__(self, alpha=2.0, beta=1.0, stabilizer=1e-6, zero_params=None):
+        super().__init__(zero_params)
+        self.alpha, self.beta = float(alpha), float(beta)
+        self.stabilizer = Stabilizer.ensure(stabilizer).epsilon
+
+
+class Norm(BasicHook):
+    kind = "norm"
+
+    def __init__(self, stabilizer=1e-6):
+        super().__init__()
+        self.stabilizer = Stabilizer.ensure(stabilizer).epsilon

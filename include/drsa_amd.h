@@ -73,6 +73,76 @@ int drsa_amd_drsa_run(const float* A, const float* C, int64_t N, int d, int K, f
 /* orthogonalize (drsa.py:201-221): U_out = V (V^T V)^{-1/2}, Newton-Schulz on device. */
 int drsa_amd_polar(const float* V, int d, float* U_out, int* iters_out, void* stream);
 
+/* compute_subspace_relevances (explainer.py:206-242): out[b][k] = sum_n sum_{j in block k}
+ * (act[b][n] U)_j (ctx[b][n] U)_j for act, ctx [B][N][d]. */
+int drsa_amd_subspace_relevances(const float* act, const float* ctx, int64_t B, int64_t N, int d, int K,
+                                 const float* U, float* out, void* stream);
+
+
+/* ------------------------------------------------------------------------- *
+ * LRP engine (zennit 0.5.1 rules over the VGG-type CNN; cxai/xai/explain).
+ * Enumerations shared by the calls below:
+ *   xmode: 0 = R = acc, 1 = R = x * acc, 2 = R = max(x,0)*acc0 + min(x,0)*acc1
+ *   post : 0 = none, 1 = g = [x > 0] R / stab(den, eps), 2 = g = [x > 0] R
+ * stab(t, eps) = t + eps * (sign(t) + [t == 0])   (zennit Stabilizer)
+ * ------------------------------------------------------------------------- */
+
+/* Floats of a prepared conv weight tensor [ng][9 * cin_p][cout_p]. */
+size_t drsa_amd_conv_weight_floats(int cin, int cout, int ng);
+
+/* Forward conv3x3 'same' + bias + ReLU [+ 2x2 max-pool with argmax] and the layer's LRP
+ * denominator (Gamma: ng = 2 (x >= 0) or 3; Epsilon: ng = 1; WSquare/Flat: den_map).
+ * Replaces the model forward (create_model.py:91-97) plus the modified forwards zennit's
+ * BasicHook re-runs in backward (attribute.py:98-107 via zennit.core.BasicHook). */
+int drsa_amd_conv_fwd(const float* in, const float* wts, const float* bias, const float* den_map, float* out,
+                      uint8_t* out_amax, float* out_den, int B, int cin, int cout, int H, int W, int ng,
+                      int pool, void* stream);
+
+/* Rule backward of one conv as a transposed conv (flipped/transposed weights), with the
+ * max-pool/ReLU backward folded into the input (g_amax != NULL: g at pool resolution) and
+ * the next layer's division folded into the output (post).  Bq rows = samples * clones.
+ * Replaces zennit's Gamma / Epsilon / WSquare / Flat gradient_mapper + reducer
+ * (constants.py:27-51 rule maps). */
+int drsa_amd_conv_bwd(const float* g, const uint8_t* g_amax, const float* wts, const float* x, const float* den,
+                      float* out, int Bq, int clones, int cin, int cout, int H, int W, int ng, int xmode,
+                      int post, float eps, void* stream);
+
+/* Dense layer forward: z = x W^T + b [, relu(z)]  (classifier Linear layers). */
+int drsa_amd_linear_fwd(const float* x, const float* W, const float* bias, float* z_out, float* relu_out, int M,
+                        int N, int K, void* stream);
+
+/* Dense layer rule backward: g = [z>0?] (R | seed) / stab(z, eps)  ->  out = epi(g W).
+ * seed_cls (device int per row) replaces lrp_output_modifier (attribute.py:111-160):
+ * R = one_hot ? onehot(cls) : z * onehot(cls). */
+int drsa_amd_linear_bwd(const float* R, const int* seed_cls, int one_hot, const float* z, int relu_mask, int rule_eps,
+                        float eps, const float* W, const float* x, int xmode, const float* den, int post,
+                        float eps_post, float* out, int M, int Nout, int Kin, void* stream);
+
+/* ProjectionModel forward (modify_model.py:75-123): h = a_vec U, a' = h U^T [, 2x2 pool]. */
+int drsa_amd_projection_fwd(const float* a, const float* U, float* h, float* ap, float* pooled, uint8_t* amax, int B,
+                            int D, int H, int W, int pool, void* stream);
+
+/* Epsilon(invprojection) -> SubspaceHook mask -> Epsilon(projection) -> ReLU backward ->
+ * division of the conv rule below (explainer.py:198-203, attribute.py:42-60).
+ * fanout != 0: each sample yields K+1 clones (standard + K subspaces); fanout == 0: row b is
+ * clone (b mod (K+1)) of a replicated batch (explainer.py:92 semantics). */
+int drsa_amd_projection_bwd(const float* gp, const uint8_t* amax, const float* ap, const float* h, const float* a,
+                            const float* den, const float* U, float* G, int B, int D, int H, int W, int K,
+                            float eps_proj, float eps_den, int fanout, void* stream);
+
+/* First-layer (one input channel) WSquare / Flat backward: R = J^T_{W2} g. */
+int drsa_amd_first_layer_bwd(const float* g, const uint8_t* amax, const float* w2, float* out, int Bq, int clones,
+                             int C, int H, int W, void* stream);
+
+/* Input-independent WSquare / Flat denominator map conv(1; W2, b2): [C][H][W]. */
+int drsa_amd_first_layer_den(const float* w2, const float* b2, float* den, int C, int CI, int H, int W, void* stream);
+
+/* HeatmapGenerator post-processing (explainer.py:99-123, sort_subspaces 151-176): standard
+ * heatmap + relevance, subspace heatmaps sorted by descending relevance, relevances, mask
+ * (int64, numpy argsort(...)[..., ::-1] order). */
+int drsa_amd_heatmap_sort(const float* hm, int B, int K, int HW, float* std_out, float* std_rel, float* sub_out,
+                          float* rel, int64_t* mask, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

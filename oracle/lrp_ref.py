@@ -114,12 +114,18 @@ def _layer_fwd(L: Layer, x: torch.Tensor) -> torch.Tensor:
 # ----------------------------------------------------------------------------
 # Jacobian-transpose products for the parametrised layers
 # ----------------------------------------------------------------------------
+def _pad(m: nn.Conv2d):
+    if isinstance(m.padding, str):   # 'same' (odd kernels, stride 1)
+        return tuple((k - 1) // 2 for k in m.kernel_size)
+    return m.padding
+
+
 def _conv(m: nn.Conv2d, x, w, b):
-    return F.conv2d(x, w, b, stride=m.stride, padding=m.padding, dilation=m.dilation, groups=m.groups)
+    return F.conv2d(x, w, b, stride=m.stride, padding=_pad(m), dilation=m.dilation, groups=m.groups)
 
 
 def _conv_jt(m: nn.Conv2d, x_shape, w, g):
-    return torch.nn.grad.conv2d_input(x_shape, w, g, stride=m.stride, padding=m.padding,
+    return torch.nn.grad.conv2d_input(x_shape, w, g, stride=m.stride, padding=_pad(m),
                                       dilation=m.dilation, groups=m.groups)
 
 
