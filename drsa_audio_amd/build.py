@@ -22,7 +22,7 @@ LIB = os.path.join(LIBDIR, "libdrsa_amd.so")
 ROOT = os.path.dirname(HERE)
 ARCH = os.environ.get("DRSA_AMD_ARCH", "gfx950")
 
-CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
+CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off", "-Wall",
             "-Wno-unused-result", "-Wno-unused-variable", "-Wno-unused-function",
             "-I", CSRC, "-I", os.path.join(ROOT, "include")]
 

@@ -8,7 +8,7 @@ enum PostMode { POST_NONE = 0, POST_DIV = 1, POST_MASK = 2 };
 struct ConvArgs {
   const float* in;          // A source: NCHW input (dense) or g at pool resolution (sparse)
   const uint8_t* in_amax;   // pool argmax (0..3) of the sparse source, per sample
-  const float* wts;         // [NG][9 * cin_p][cout_p], k = (ky*3 + kx) * cin_p + ci
+  const float* wts;         // [NG][9 * cin_p][cout_p], k = ci * 9 + ky * 3 + kx
   const float* bias;        // forward: [3][cout_p] = (b, b+, b-)
   const float* den_map;     // forward, WSquare/Flat: [cout][H][W] input-independent denominator
   const float* x;           // backward: activation at output resolution (per sample)

@@ -18,8 +18,10 @@
 //
 // GEMM view: M = output pixels of a TH x TW tile (window-major order so that every 2x2 pool
 // window lands in 4 consecutive accumulator registers of one lane), N = output channels
-// (32-wide MFMA tiles), K = 9 * Cin (chunks of CIC input channels staged in LDS with the
-// halo; weights [k][co] staged next to them).
+// (32-wide MFMA tiles), K = 9 * Cin in the order k = ci*9 + (ky*3 + kx) (chunks of CIC input
+// channels staged in LDS with the halo; weights [k][co] staged next to them).  Every output
+// is one k-ordered fp32 fma chain (MFMA f32 semantics), independent of the chunking, which
+// is what oracle/lrp_exact.c reproduces bit for bit.
 #include "common.h"
 #include "lrp_conv.h"
 
@@ -136,16 +138,13 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(ConvArgs a) {
       }
       halo[ci * PLANE + hy * RS + hx] = v;
     }
-    // ---- stage the weight chunk: rows k = tap*CIC + ci  <- global k = tap*CIN + c0 + ci ----
+    // ---- stage the weight chunk: rows k = ci*9 + tap (channel-major) <- global row c0*9 + k ----
     for (int idx = tid; idx < NG * KCP * (COUT / 4); idx += kThreads) {
       const int g = idx / (KCP * (COUT / 4));
       const int rem = idx - g * (KCP * (COUT / 4));
       const int k = rem / (COUT / 4), c4 = (rem - k * (COUT / 4)) * 4;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (k < KC) {
-        const int tap = k / CIC, ci = k - tap * CIC;
-        v = *reinterpret_cast<const float4*>(a.wts + ((size_t)g * 9 * CIN + tap * CIN + c0 + ci) * COUT + c4);
-      }
+      if (k < KC) v = *reinterpret_cast<const float4*>(a.wts + ((size_t)g * 9 * CIN + c0 * 9 + k) * COUT + c4);
       *reinterpret_cast<float4*>(wl + ((size_t)g * KCP + k) * COUT + c4) = v;
     }
     __syncthreads();
@@ -155,7 +154,7 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(ConvArgs a) {
 #pragma unroll 2
     for (int k0 = 0; k0 < KCP; k0 += 2) {
       const int k = k0 + h;
-      const int tap = k / CIC, ci = k - tap * CIC;
+      const int ci = k / 9, tap = k - ci * 9;     // accumulation order: channel-major, tap-minor
       const int ky = tap / 3, kx = tap - ky * 3;
       const bool kvalid = k < KC;
       const int off = ci * PLANE + ky * RS + kx;

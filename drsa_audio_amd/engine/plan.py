@@ -248,15 +248,15 @@ class LRPEngine:
         zero_bias = "bias" in getattr(st.rule, "zero_params", ())
         bd = torch.zeros_like(b) if zero_bias else b
 
-        def fwd_layout(Wx):   # [cout][cin][3][3] -> [9*cin_p][cout_p]
-            t = torch.zeros(3, 3, cin_p, cout_p, device=dev)
-            t[:, :, :st.cin, :st.cout] = Wx.permute(2, 3, 1, 0)
+        def fwd_layout(Wx):   # [cout][cin][3][3] -> [9*cin_p][cout_p], row k = ci*9 + ky*3 + kx
+            t = torch.zeros(cin_p, 3, 3, cout_p, device=dev)
+            t[:st.cin, :, :, :st.cout] = Wx.permute(1, 2, 3, 0)
             return t.reshape(9 * cin_p, cout_p)
 
-        def bwd_layout(Wx):   # transposed conv: [9*cout_p][pad32(cin)], flipped taps
+        def bwd_layout(Wx):   # transposed conv as 'same' conv: [9*cout_p][pad32(cin)], flipped taps
             cin_o = _pad32(st.cin)
-            t = torch.zeros(3, 3, cout_p, cin_o, device=dev)
-            t[:, :, :st.cout, :st.cin] = Wx.flip(2, 3).permute(2, 3, 0, 1)
+            t = torch.zeros(cout_p, 3, 3, cin_o, device=dev)
+            t[:st.cout, :, :, :st.cin] = Wx.flip(2, 3).permute(0, 2, 3, 1)
             return t.reshape(9 * cout_p, cin_o)
 
         bias3 = torch.zeros(3, cout_p, device=dev)

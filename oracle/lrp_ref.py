@@ -29,12 +29,20 @@ Rule arithmetic (z = f(x; W, b), Jᵀ_W g = input-gradient of f with weights W):
 Layers without a rule use their plain gradient (ReLU, MaxPool [first max], Dropout
 (eval), BatchNorm (eval), flatten), exactly like zennit's Gradient attributor.
 
-Two execution modes share that arithmetic:
+Three execution modes share that arithmetic:
 * ``mode="analytic"`` — each rule evaluated with explicit conv/conv-transpose calls.
 * ``mode="zennit"``   — each rule evaluated the way zennit's BasicHook does it
   (modified forwards + ``torch.autograd.grad``), and the heatmap generator replicates
   the batch K+1 times like ``explainer.py:92``.  This is the representative CPU
   baseline that ``bench.py`` times; tests check both modes agree.
+* ``mode="exact"``    — the analytic structure with every dot product computed as one
+  sequential fp32 fma chain in a pinned order (``oracle/lrp_exact.c``): channel-major /
+  tap-minor for convolutions, bias added last.  This is the order the HIP kernels
+  accumulate in (f32 MFMA is an exact k-ordered fma chain), so this mode is the
+  bit-exact parity oracle.  The reference path is ill-conditioned with respect to
+  rounding (the ProjectionModel's a' = (aU)Uᵀ differs from a at rounding level and the
+  ε = 1e-6 stabilisers amplify that at dead ReLU channels: correctly rounded projections
+  move subspace relevances by up to ~6 %), so only a pinned order can pin it.
 """
 from __future__ import annotations
 
@@ -102,17 +110,23 @@ def sequential_layers(model: nn.Module) -> List[Layer]:
     return out
 
 
-def _layer_fwd(L: Layer, x: torch.Tensor) -> torch.Tensor:
+def _layer_fwd(L: Layer, x: torch.Tensor, ops=None) -> torch.Tensor:
     m = L.module
     if L.kind == "flatten":
         return x.reshape(x.size(0), -1)
     if L.kind == "dropout":
         return x
+    if ops is not None and L.kind == "conv":
+        return ops.conv(m, x, m.weight.detach(), None if m.bias is None else m.bias.detach())
+    if ops is not None and L.kind == "linear":
+        return ops.linear(x, m.weight.detach(), None if m.bias is None else m.bias.detach())
+    if ops is not None and L.kind in ("proj", "invproj"):
+        return _proj_fwd(L, x, ops)
     return m(x)
 
 
 # ----------------------------------------------------------------------------
-# Jacobian-transpose products for the parametrised layers
+# primitive ops: torch (oneDNN order) or exact (pinned fma order, oracle/lrp_exact.c)
 # ----------------------------------------------------------------------------
 def _pad(m: nn.Conv2d):
     if isinstance(m.padding, str):   # 'same' (odd kernels, stride 1)
@@ -120,25 +134,128 @@ def _pad(m: nn.Conv2d):
     return m.padding
 
 
-def _conv(m: nn.Conv2d, x, w, b):
-    return F.conv2d(x, w, b, stride=m.stride, padding=_pad(m), dilation=m.dilation, groups=m.groups)
+class TorchOps:
+    name = "torch"
+
+    @staticmethod
+    def conv(m, x, w, b):
+        return F.conv2d(x, w, b, stride=m.stride, padding=_pad(m), dilation=m.dilation, groups=m.groups)
+
+    @staticmethod
+    def conv_t(m, x_shape, w, g):
+        return torch.nn.grad.conv2d_input(x_shape, w, g, stride=m.stride, padding=_pad(m),
+                                          dilation=m.dilation, groups=m.groups)
+
+    @staticmethod
+    def linear(x, w, b):
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def linear_t(g, w):
+        return g @ w
+
+    @staticmethod
+    def matmul(a, b):
+        return a @ b
+
+    @staticmethod
+    def plane_sum(hm: np.ndarray) -> np.ndarray:
+        return hm.sum(axis=(-2, -1))
 
 
-def _conv_jt(m: nn.Conv2d, x_shape, w, g):
-    return torch.nn.grad.conv2d_input(x_shape, w, g, stride=m.stride, padding=_pad(m),
-                                      dilation=m.dilation, groups=m.groups)
+class ExactOps:
+    """Pinned-order primitives (each output one k-ordered fp32 fma chain; oracle/lrp_exact.c)."""
+    name = "exact"
+    _lib = None
+
+    @classmethod
+    def lib(cls):
+        if cls._lib is None:
+            import ctypes, os
+            path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "liblrp_exact.so")
+            if not os.path.exists(path):
+                import subprocess
+                subprocess.run(["make", "-C", os.path.dirname(path).rsplit("/lib", 1)[0]], check=True,
+                               capture_output=True)
+            L = ctypes.CDLL(path)
+            P, I = ctypes.c_void_p, ctypes.c_int
+            L.conv2d_exact.argtypes = [P, P, P, P, I, I, I, I, I]
+            L.conv_transpose_exact.argtypes = [P, P, P, I, I, I, I, I]
+            L.linear_exact.argtypes = [P, P, P, P, I, I, I]
+            L.matmul_exact.argtypes = [P, P, P, I, I, I]
+            L.tree_sum_hw.argtypes = [P, I]
+            L.tree_sum_hw.restype = ctypes.c_float
+            cls._lib = L
+        return cls._lib
+
+    @staticmethod
+    def _c(t):
+        return t.detach().to(torch.float32).contiguous()
+
+    @classmethod
+    def conv(cls, m, x, w, b):
+        if tuple(m.kernel_size) != (3, 3) or tuple(m.stride) != (1, 1) or tuple(_pad(m)) != (1, 1):
+            raise NotImplementedError("exact ops: 3x3 same convs only")
+        x, w = cls._c(x), cls._c(w)
+        b = None if b is None else cls._c(b)
+        B, Cin, H, W = x.shape
+        out = torch.empty(B, w.size(0), H, W)
+        cls.lib().conv2d_exact(x.data_ptr(), w.data_ptr(), None if b is None else b.data_ptr(), out.data_ptr(),
+                               B, Cin, w.size(0), H, W)
+        return out
+
+    @classmethod
+    def conv_t(cls, m, x_shape, w, g):
+        g, w = cls._c(g), cls._c(w)
+        B, Cout, H, W = g.shape
+        out = torch.empty(B, w.size(1), H, W)
+        cls.lib().conv_transpose_exact(g.data_ptr(), w.data_ptr(), out.data_ptr(), B, Cout, w.size(1), H, W)
+        return out
+
+    @classmethod
+    def linear(cls, x, w, b):
+        x, w = cls._c(x), cls._c(w)
+        b = None if b is None else cls._c(b)
+        out = torch.empty(x.size(0), w.size(0))
+        cls.lib().linear_exact(x.data_ptr(), w.data_ptr(), None if b is None else b.data_ptr(), out.data_ptr(),
+                               x.size(0), w.size(0), x.size(1))
+        return out
+
+    @classmethod
+    def linear_t(cls, g, w):
+        return cls.matmul(g, w)
+
+    @classmethod
+    def matmul(cls, a, b):
+        shp = a.shape
+        a2 = cls._c(a.reshape(-1, shp[-1]))
+        b = cls._c(b)
+        out = torch.empty(a2.size(0), b.size(1))
+        cls.lib().matmul_exact(a2.data_ptr(), b.data_ptr(), out.data_ptr(), a2.size(0), b.size(1), a2.size(1))
+        return out.reshape(*shp[:-1], b.size(1))
+
+    @classmethod
+    def plane_sum(cls, hm: np.ndarray) -> np.ndarray:
+        hm = np.ascontiguousarray(hm, dtype=np.float32)
+        lead = hm.shape[:-2]
+        flat = hm.reshape(-1, hm.shape[-2] * hm.shape[-1])
+        out = np.array([cls.lib().tree_sum_hw(r.ctypes.data, r.size) for r in flat], dtype=np.float32)
+        return out.reshape(lead)
 
 
-def _aff(L: Layer, x, w, b):
+OPS = {"analytic": TorchOps, "zennit": TorchOps, "exact": ExactOps}
+
+
+def _aff(L: Layer, x, w, b, ops=TorchOps):
     if L.kind == "conv":
-        return _conv(L.module, x, w, b)
-    return F.linear(x, w, b)
+        return ops.conv(L.module, x, w, b)
+    return ops.linear(x, w, b)
 
 
-def _aff_jt(L: Layer, x_shape, w, g):
+def _aff_jt(L: Layer, x_shape, w, g, ops=TorchOps):
     if L.kind == "conv":
-        return _conv_jt(L.module, x_shape, w, g)
-    return g @ w
+        return ops.conv_t(L.module, x_shape, w, g)
+    return ops.linear_t(g, w)
 
 
 def _params(m):
@@ -149,27 +266,49 @@ def _mod(p, fn):
     return None if p is None else fn(p)
 
 
+def _proj_fwd(L: Layer, x, ops):
+    """Projection / InvProjection forward through the given matmul (modify_model.py:89-123)."""
+    m = L.module
+    if L.kind == "proj":
+        b, d = x.size(0), x.size(1)
+        vecs = x.reshape(b, d, -1).transpose(1, 2)
+        h = ops.matmul(vecs, m.U.to(torch.float32))
+        return h.reshape(b, vecs.size(1), m.num_concepts, m.d_k)
+    b, n = x.size(0), x.size(1)
+    side = int(round(n ** 0.5))
+    a = ops.matmul(x.reshape(b, n, m.d), m.U_inv.to(torch.float32).contiguous())
+    return a.transpose(1, 2).reshape(b, m.d, side, side).contiguous()
+
+
+def _proj_jt(L: Layer, x, g, ops):
+    """Input-gradient of (inv)projection applied to g (linear maps, explicit)."""
+    m = L.module
+    if L.kind == "proj":        # h = a_vec U  ->  J^T g = g_vec U^T (back to [b, d, H, W])
+        b, n = g.size(0), g.size(1)
+        t = ops.matmul(g.reshape(b, n, -1), m.U.to(torch.float32).t().contiguous())
+        return t.transpose(1, 2).reshape(x.shape)
+    b, d = g.size(0), g.size(1)     # a' = h U^T  ->  J^T g = g_vec U
+    gv = g.reshape(b, d, -1).transpose(1, 2)
+    return ops.matmul(gv, m.U_inv.to(torch.float32).t().contiguous()).reshape(x.shape)
+
+
 # ----------------------------------------------------------------------------
 # analytic rules
 # ----------------------------------------------------------------------------
 def rule_backward_analytic(L: Layer, rule: RuleSpec, x: torch.Tensor, z: torch.Tensor,
-                           R: torch.Tensor) -> torch.Tensor:
+                           R: torch.Tensor, ops=TorchOps) -> torch.Tensor:
     kind = rule[0]
     if kind == "pass":
         return R
     if L.kind in ("proj", "invproj"):
-        # only Epsilon is meaningful here (explainer.py:200,202); generic via autograd
+        # only Epsilon is meaningful here (explainer.py:200,202)
         if kind != "epsilon":
             raise ValueError("oracle: only Epsilon on (inv)projection")
-        xx = x.detach().requires_grad_(True)
-        with torch.enable_grad():
-            zz = L.module(xx)
-            g, = torch.autograd.grad(zz, xx, R / stabilize(zz.detach(), rule[1]))
-        return x * g
+        return x * _proj_jt(L, x, R / stabilize(z, rule[1]), ops)
     w, b = _params(L.module)
     if kind == "epsilon":
         g = R / stabilize(z, rule[1])
-        return x * _aff_jt(L, x.shape, w, g)
+        return x * _aff_jt(L, x.shape, w, g, ops)
     if kind == "gamma":
         gam, eps = rule[1], rule[2]
         wp = w + gam * w.clamp(min=0)
@@ -177,22 +316,22 @@ def rule_backward_analytic(L: Layer, rule: RuleSpec, x: torch.Tensor, z: torch.T
         bp = _mod(b, lambda t: t + gam * t.clamp(min=0))
         bn = _mod(b, lambda t: t + gam * t.clamp(max=0))
         xp, xn = x.clamp(min=0), x.clamp(max=0)
-        z0 = _aff(L, xp, wp, bp)
-        z1 = _aff(L, xn, wn, bn)
-        z2 = _aff(L, xp, wn, bn)
-        z3 = _aff(L, xn, wp, bp)
+        z0 = _aff(L, xp, wp, bp, ops)
+        z1 = _aff(L, xn, wn, bn, ops)
+        z2 = _aff(L, xp, wn, bn, ops)
+        z3 = _aff(L, xn, wp, bp, ops)
         gpos = R * (z > 0) / stabilize(z0 + z1, eps)
         gneg = R * (z < 0) / stabilize(z2 + z3, eps)
-        return (xp * _aff_jt(L, x.shape, wp, gpos) + xn * _aff_jt(L, x.shape, wn, gpos)
-                + xp * _aff_jt(L, x.shape, wn, gneg) + xn * _aff_jt(L, x.shape, wp, gneg))
+        return (xp * _aff_jt(L, x.shape, wp, gpos, ops) + xn * _aff_jt(L, x.shape, wn, gpos, ops)
+                + xp * _aff_jt(L, x.shape, wn, gneg, ops) + xn * _aff_jt(L, x.shape, wp, gneg, ops))
     if kind in ("wsquare", "flat"):
         eps = rule[1]
         if kind == "wsquare":
             w2, b2 = w * w, _mod(b, lambda t: t * t)
         else:
             w2, b2 = torch.ones_like(w), _mod(b, torch.zeros_like)
-        den = _aff(L, torch.ones_like(x), w2, b2)
-        return _aff_jt(L, x.shape, w2, R / stabilize(den, eps))
+        den = _aff(L, torch.ones_like(x), w2, b2, ops)
+        return _aff_jt(L, x.shape, w2, R / stabilize(den, eps), ops)
     raise ValueError(f"oracle: unknown rule {rule}")
 
 
@@ -200,10 +339,10 @@ def rule_backward_analytic(L: Layer, rule: RuleSpec, x: torch.Tensor, z: torch.T
 # zennit-structured rules (modified forwards + autograd.grad), for the CPU baseline
 # ----------------------------------------------------------------------------
 def rule_backward_zennit(L: Layer, rule: RuleSpec, x: torch.Tensor, z: torch.Tensor,
-                         R: torch.Tensor) -> torch.Tensor:
+                         R: torch.Tensor, ops=TorchOps) -> torch.Tensor:
     kind = rule[0]
     if kind == "pass" or L.kind in ("proj", "invproj"):
-        return rule_backward_analytic(L, rule, x, z, R)
+        return rule_backward_analytic(L, rule, x, z, R, ops)
     w, b = _params(L.module)
 
     def run(inputs, params):
@@ -245,7 +384,7 @@ def rule_backward_zennit(L: Layer, rule: RuleSpec, x: torch.Tensor, z: torch.Ten
 # ----------------------------------------------------------------------------
 # plain-gradient layers
 # ----------------------------------------------------------------------------
-def _plain_backward(L: Layer, x: torch.Tensor, z: torch.Tensor, R: torch.Tensor, aux) -> torch.Tensor:
+def _plain_backward(L: Layer, x: torch.Tensor, z: torch.Tensor, R: torch.Tensor, aux, ops=TorchOps) -> torch.Tensor:
     if L.kind == "relu":
         return torch.where(z > 0, R, torch.zeros_like(R))
     if L.kind == "maxpool":
@@ -255,7 +394,13 @@ def _plain_backward(L: Layer, x: torch.Tensor, z: torch.Tensor, R: torch.Tensor,
         return R
     if L.kind == "flatten":
         return R.reshape(x.shape)
-    if L.kind in ("bn2d", "bn1d", "conv", "linear", "proj", "invproj"):
+    if L.kind == "conv":
+        return ops.conv_t(L.module, x.shape, L.module.weight.detach(), R)
+    if L.kind == "linear":
+        return ops.linear_t(R, L.module.weight.detach())
+    if L.kind in ("proj", "invproj"):
+        return _proj_jt(L, x, R, ops)
+    if L.kind in ("bn2d", "bn1d"):
         xx = x.detach().requires_grad_(True)
         with torch.enable_grad():
             zz = _layer_fwd(L, xx)
@@ -297,6 +442,7 @@ def lrp(model: nn.Module, rules: Dict[str, RuleSpec], x: torch.Tensor, class_idx
         capture: Optional[str] = None):
     """Returns (logits, R_input[, (act, rel) at layer ``capture``])."""
     layers = sequential_layers(model)
+    ops = OPS[mode]
     acts: List[Tuple[torch.Tensor, torch.Tensor, object]] = []
     h = x.detach().to(torch.float32)
     for L in layers:
@@ -306,7 +452,7 @@ def lrp(model: nn.Module, rules: Dict[str, RuleSpec], x: torch.Tensor, class_idx
             out, aux = F.max_pool2d(h, m.kernel_size, m.stride, m.padding, m.dilation,
                                     m.ceil_mode, return_indices=True)
         else:
-            out = _layer_fwd(L, h)
+            out = _layer_fwd(L, h, ops)
         acts.append((h, out, aux))
         h = out
     logits = h
@@ -320,9 +466,9 @@ def lrp(model: nn.Module, rules: Dict[str, RuleSpec], x: torch.Tensor, class_idx
         if rule is not None and rule[0] == "subspace":
             R = subspace_mask(R, rule[1])
         elif rule is not None:
-            R = rb(L, rule, xin, zout, R)
+            R = rb(L, rule, xin, zout, R, ops)
         else:
-            R = _plain_backward(L, xin, zout, R, aux)
+            R = _plain_backward(L, xin, zout, R, aux, ops)
     if capture is not None:
         return logits, R, captured
     return logits, R
@@ -337,9 +483,9 @@ def class_composite_rules(name_map: Dict[str, RuleSpec], K: int) -> Dict[str, Ru
     return r
 
 
-def sort_subspaces(sub: np.ndarray):
+def sort_subspaces(sub: np.ndarray, ops=TorchOps):
     """explainer.py:151-176 with batch dims kept (defect D7: B=1 must not squeeze)."""
-    rel = sub.sum(axis=(-2, -1)).reshape(sub.shape[0], sub.shape[1])
+    rel = ops.plane_sum(sub).reshape(sub.shape[0], sub.shape[1])
     mask = np.argsort(rel, axis=-1)[..., ::-1]
     ar = np.arange(sub.shape[0])[:, None]
     return sub[ar, mask], rel[ar, mask], mask
@@ -356,10 +502,11 @@ def subspace_heatmaps(proj_model: nn.Module, name_map: Dict[str, RuleSpec], K: i
     H, W = R.shape[-2:]
     hm = R.reshape(-1, K + 1, H, W).numpy()
     std, sub = hm[:, 0:1], hm[:, 1:]
-    sub_s, rel_s, mask = sort_subspaces(sub)
+    ops = OPS[mode]
+    sub_s, rel_s, mask = sort_subspaces(sub, ops)
     return {
         "standard_heatmaps": std,
-        "standard_relevance": std.sum(axis=(-2, -1)).flatten(),
+        "standard_relevance": ops.plane_sum(std).flatten(),
         "subspace_heatmaps": sub_s,
         "subspace_relevances": rel_s,
         "mask": mask,
