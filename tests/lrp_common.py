@@ -1,0 +1,62 @@
+"""Shared builders for the LRP tests (models, synthetic log-mels, rule specs for the oracle)."""
+import numpy as np
+import torch
+
+from drsa_audio_amd.model.create_model import VGGType
+
+
+def gtzan128(seed=0):
+    torch.manual_seed(seed)
+    return VGGType(n_filters=(32, 32, 64, 64, 128), n_dense=128, pool_kernels=((2, 2),) * 5, dropout=0.4,
+                   input_size=(128, 128), conv_bn=False, dense_bn=False, block_depth=1).eval()
+
+
+def toy(seed=0):
+    torch.manual_seed(seed)
+    return VGGType(n_filters=(8, 8, 16, 16, 16), n_dense=32, n_classes=2, pool_kernels=((2, 2),) * 5,
+                   dropout=0.0, input_size=(64, 64), conv_bn=False, dense_bn=False, block_depth=1).eval()
+
+
+def logmel(B, H=128, W=128, seed=1):
+    """Synthetic log-mel: clamp(log10(e * tilt + 1e-7), -4), e ~ Exp(1)."""
+    g = torch.Generator().manual_seed(seed)
+    e = torch.empty(B, 1, H, W).exponential_(generator=g)
+    tilt = 10 ** (-3 * torch.arange(H).float() / max(H - 1, 1))
+    return torch.clamp(torch.log10(e * tilt[None, None, :, None] + 1e-7), min=-4)
+
+
+def spec(name_map):
+    """Product rule descriptors -> oracle rule specs."""
+    out = {}
+    for names, r in name_map:
+        k = r.kind
+        if k == "epsilon":
+            t = ("epsilon", r.epsilon)
+        elif k == "gamma":
+            t = ("gamma", r.gamma, r.stabilizer)
+        elif k in ("wsquare", "flat"):
+            t = (k, r.stabilizer)
+        elif k == "pass":
+            t = ("pass",)
+        else:
+            raise ValueError(k)
+        for n in names:
+            out[n] = t
+    return out
+
+
+def u64():
+    import os
+    from conftest import GOLDEN
+    return torch.from_numpy(np.load(os.path.join(GOLDEN, "u64_seed42.npy")))
+
+
+def ortho(d, seed):
+    q, _ = np.linalg.qr(np.random.default_rng(seed).standard_normal((d, d)))
+    return torch.from_numpy(q.astype(np.float32))
+
+
+def maxnorm_err(a, b):
+    a = torch.as_tensor(a).reshape(a.shape[0], -1).double()
+    b = torch.as_tensor(b).reshape(b.shape[0], -1).double()
+    return float(((a - b).abs().amax(1) / b.abs().amax(1).clamp_min(1e-30)).max())

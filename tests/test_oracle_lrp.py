@@ -1,0 +1,193 @@
+"""The LRP oracle (oracle/lrp_ref.py) on CPU.
+
+zennit is not installed and the reference has no tests, so the rule arithmetic is
+*parity-unpinned vs zennit*; it is pinned here by theory known-answer tests:
+(i) sum of subspace heatmaps = standard heatmap, (ii) epsilon conservation, (iii) WSquare /
+Flat input independence, (iv) U = I, K = 1 reproduces plain LRP, (v) a hand-computed
+network in float64, plus agreement of the three oracle modes.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+import lrp_ref
+from lrp_common import gtzan128, logmel, maxnorm_err, ortho, spec, toy, u64
+from drsa_audio_amd.model.modify_model import ProjectionModel
+from drsa_audio_amd.utils.constants import LRP_NAME_MAP_GTZAN, LRP_NAME_MAP_TOY
+
+NM = spec(LRP_NAME_MAP_GTZAN)
+
+
+@pytest.fixture(scope="module")
+def model():
+    return gtzan128()
+
+
+def test_zennit_structured_mode_equals_analytic(model):
+    x = logmel(2)
+    _, Ra = lrp_ref.lrp(model, NM, x, class_idx=3, mode="analytic")
+    _, Rz = lrp_ref.lrp(model, NM, x, class_idx=3, mode="zennit")
+    assert torch.equal(Ra, Rz)
+
+
+def test_exact_mode_within_rounding_envelope_of_analytic(model):
+    x = logmel(2, seed=7)
+    la, Ra = lrp_ref.lrp(model, NM, x, class_idx=5, mode="analytic")
+    le, Re = lrp_ref.lrp(model, NM, x, class_idx=5, mode="exact")
+    assert (la - le).abs().max() <= 1e-6 * la.abs().max()
+    # the reference path's own sensitivity to accumulation order (parity)
+    assert maxnorm_err(Re, Ra) < 2e-3
+
+
+@pytest.mark.parametrize("mode", ["analytic", "exact"])
+def test_subspace_heatmaps_sum_to_standard(model, mode):
+    pm = ProjectionModel(model, 7, u64(), 4).eval()
+    out = lrp_ref.subspace_heatmaps(pm, NM, 4, logmel(1, seed=3), class_idx=2, mode=mode)
+    s = out["subspace_heatmaps"].sum(1)
+    std = out["standard_heatmaps"][:, 0]
+    assert np.abs(s - std).max() <= 1e-5 * np.abs(std).max()
+    assert np.allclose(out["subspace_relevances"].sum(1), out["standard_relevance"], rtol=1e-4, atol=1e-9)
+
+
+def test_epsilon_conservation_bias_free_linear():
+    torch.manual_seed(0)
+    lin = nn.Linear(7, 5, bias=False)
+    L = lrp_ref.Layer("l", lin, "linear")
+    x = torch.randn(3, 7)
+    z = lin(x).detach()
+    R = torch.randn(3, 5)
+    eps = 1e-3
+    Rin = lrp_ref.rule_backward_analytic(L, ("epsilon", eps), x, z, R)
+    expect = (R * z / lrp_ref.stabilize(z, eps)).sum(1)
+    assert torch.allclose(Rin.sum(1), expect, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("kind", ["wsquare", "flat"])
+def test_first_layer_rules_ignore_input_values(kind):
+    torch.manual_seed(1)
+    conv = nn.Conv2d(1, 4, 3, padding=1)
+    L = lrp_ref.Layer("c", conv, "conv")
+    R = torch.randn(2, 4, 8, 8)
+    x1, x2 = torch.randn(2, 1, 8, 8), torch.randn(2, 1, 8, 8) * 10
+    r1 = lrp_ref.rule_backward_analytic(L, (kind, 1e-7), x1, None, R)
+    r2 = lrp_ref.rule_backward_analytic(L, (kind, 1e-7), x2, None, R)
+    assert torch.equal(r1, r2)
+
+
+def test_identity_projection_reproduces_plain_lrp(model):
+    x = logmel(1, seed=11)
+    _, R = lrp_ref.lrp(model, NM, x, class_idx=1)
+    pm = ProjectionModel(model, 7, torch.eye(64), 1).eval()
+    out = lrp_ref.subspace_heatmaps(pm, NM, 1, x, class_idx=1)
+    assert maxnorm_err(out["standard_heatmaps"], R.numpy()) < 1e-4
+    assert np.allclose(out["subspace_heatmaps"], out["standard_heatmaps"])
+
+
+def _hand_lrp(W1, b1, W2, b2, x, c, gam, eps):
+    """float64 loops: conv3x3(1->2)+ReLU+maxpool2 -> Linear(8->3); Gamma on conv, Epsilon on linear."""
+    H = x.shape[0]
+    z = np.zeros((2, H, H)); zp = np.zeros((2, H, H))
+    Wp = W1 + gam * np.maximum(W1, 0); bp = b1 + gam * np.maximum(b1, 0); bn = b1 + gam * np.minimum(b1, 0)
+    xp = np.pad(x, 1)
+    for o in range(2):
+        for i in range(H):
+            for j in range(H):
+                patch = xp[i:i + 3, j:j + 3]
+                z[o, i, j] = (patch * W1[o]).sum() + b1[o]
+                zp[o, i, j] = (np.maximum(patch, 0) * Wp[o]).sum() + bp[o] + (np.minimum(patch, 0) * (W1[o] + gam * np.minimum(W1[o], 0))).sum() + bn[o]
+    a = np.maximum(z, 0)
+    P = np.zeros((2, H // 2, H // 2)); arg = {}
+    for o in range(2):
+        for i in range(H // 2):
+            for j in range(H // 2):
+                win = a[o, 2 * i:2 * i + 2, 2 * j:2 * j + 2]
+                k = int(np.argmax(win.reshape(-1)))
+                P[o, i, j] = win.reshape(-1)[k]; arg[(o, i, j)] = (2 * i + k // 2, 2 * j + k % 2)
+    f = P.reshape(-1)
+    y = W2 @ f + b2
+    Rout = np.zeros_like(y); Rout[c] = y[c]
+    st = lambda t: t + eps * (np.sign(t) + (t == 0))
+    Rf = f * (W2.T @ (Rout / st(y)))
+    Ra = np.zeros_like(a)
+    for (o, i, j), (p, q) in arg.items():
+        Ra[o, p, q] = Rf.reshape(P.shape)[o, i, j] * (a[o, p, q] > 0)
+    g = Ra * (z > 0) / st(zp)
+    Rin = np.zeros((H, H))
+    gp = np.pad(g, ((0, 0), (1, 1), (1, 1)))
+    for i in range(H):
+        for j in range(H):
+            acc_p = 0.0; acc_n = 0.0
+            for o in range(2):
+                for ky in range(3):
+                    for kx in range(3):
+                        gv = gp[o, i + 2 - ky, j + 2 - kx]
+                        acc_p += gv * Wp[o, ky, kx]
+                        acc_n += gv * (W1[o, ky, kx] + gam * min(W1[o, ky, kx], 0))
+            Rin[i, j] = max(x[i, j], 0) * acc_p + min(x[i, j], 0) * acc_n
+    return y, Rin
+
+
+def test_hand_computed_network_float64():
+    rng = np.random.default_rng(5)
+    W1 = rng.standard_normal((2, 3, 3)); b1 = rng.standard_normal(2) * 0.1
+    W2 = rng.standard_normal((3, 8)); b2 = rng.standard_normal(3) * 0.1
+    x = rng.standard_normal((4, 4))
+    y, Rin = _hand_lrp(W1, b1, W2, b2, x, 1, 0.25, 1e-6)
+
+    class Net(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.features = nn.Sequential(nn.Conv2d(1, 2, 3, padding=1), nn.ReLU(), nn.MaxPool2d(2))
+            self.classifier = nn.Sequential(nn.Linear(8, 3))
+    net = Net()
+    with torch.no_grad():
+        net.features[0].weight.copy_(torch.from_numpy(W1[:, None]))
+        net.features[0].bias.copy_(torch.from_numpy(b1))
+        net.classifier[0].weight.copy_(torch.from_numpy(W2))
+        net.classifier[0].bias.copy_(torch.from_numpy(b2))
+    rules = {"features.0": ("gamma", 0.25, 1e-6), "classifier.0": ("epsilon", 1e-6)}
+    lg, R = lrp_ref.lrp(net, rules, torch.from_numpy(x[None, None]).float(), class_idx=1)
+    assert np.allclose(lg.numpy()[0], y, rtol=1e-5, atol=1e-5)
+    assert np.abs(R.numpy()[0, 0] - Rin).max() <= 1e-4 * np.abs(Rin).max()
+
+
+def test_sort_ties_and_batch_one():
+    sub = np.zeros((1, 3, 2, 2), dtype=np.float32)
+    sub[0, 0] = 1.0; sub[0, 2] = 1.0; sub[0, 1] = 2.0
+    s, r, m = lrp_ref.sort_subspaces(sub)
+    assert m.tolist() == [[1, 2, 0]]            # descending, ties -> larger index first
+    assert s.shape == (1, 3, 2, 2) and r.shape == (1, 3)
+
+
+def test_toy_runs_through_oracle():
+    x = logmel(1, 64, 64, seed=2)
+    lg, R = lrp_ref.lrp(toy(), spec(LRP_NAME_MAP_TOY), x, class_idx=0)
+    assert R.shape == x.shape and torch.isfinite(R).all()
+
+
+def test_model_fixture_pins_vggtype(golden_dir):
+    fx = np.load(f"{golden_dir}/model_fixture.npz")
+    m = gtzan128()
+    assert [n for n, _ in m.named_modules() if n.count(".") == 1] == list(fx["gtzan_names"])
+    assert np.array_equal(np.array([float(p.double().sum()) for p in m.parameters()]), fx["gtzan_param_sums"])
+    with torch.no_grad():
+        assert np.array_equal(m(torch.from_numpy(fx["gtzan_x"])).numpy(), fx["gtzan_logits"])
+        pm = ProjectionModel(m, 7, u64(), 4).eval()
+        assert np.array_equal(pm(torch.from_numpy(fx["gtzan_x"])).numpy(), fx["proj_logits"])
+        assert [n for n, _ in pm.named_modules() if n.count(".") == 1] == list(fx["proj_names"])
+        h = pm.features[:9](torch.from_numpy(fx["gtzan_x"]))
+        assert np.array_equal(h[:, :64].numpy(), fx["proj_h"])
+    t = toy()
+    assert np.array_equal(np.array([float(p.double().sum()) for p in t.parameters()]), fx["toy_param_sums"])
+
+
+def test_preprocessing_helpers_match_reference_fixture(golden_dir):
+    import drsa_ref
+    fx = np.load(f"{golden_dir}/preprocessing_fixture.npz")
+    va = drsa_ref.get_vectors_from_maps(torch.from_numpy(fx["maps_a"]), fx["idx"])
+    vr = drsa_ref.get_vectors_from_maps(torch.from_numpy(fx["maps_r"]), fx["idx"])
+    assert np.array_equal(va.numpy(), fx["vec_a"]) and np.array_equal(vr.numpy(), fx["vec_r"])
+    ctx = drsa_ref.compute_context_vectors(va, vr)
+    assert np.array_equal(ctx.numpy(), fx["ctx"])
+    assert np.array_equal(drsa_ref.normalize_vectors(va).numpy(), fx["norm_a"])
