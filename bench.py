@@ -1,0 +1,302 @@
+"""Benchmark: explained samples/sec (LRP + DRSA subspace heatmaps, K=4) on MI355X.
+
+Workload (BASELINE.json metric): GTZAN-128 VGG (random init, torch.manual_seed(0)),
+HeatmapGenerator at layer j=7 (conv3 block, d=64) with K=4 subspaces, U = ortho_group.rvs(64)
+(seed 42, committed fixture), synthetic 128x128 log-mel batches.  One step = one batch through
+the whole hot path: forward, LRP backward with the K+1 relevance clones, split/sum/sort
+(HeatmapGenerator.info semantics), inputs resident in HBM, outputs left in HBM.
+
+  python bench.py [--gpus N --steps K --warmup W --batch B]
+  (N>1: torchrun --nproc-per-node N; each rank explains its own batch, no collective on the
+   data path -> weak scaling; time = max over ranks.)
+
+Also reported: per-kernel HIP-event timings of the dominant kernel (roofline), the standard
+LRP rate at bs=64 (C2), the DRSA step rate at C3 (N=20000, d=64, K=4) with its objective
+checked against the CPU oracle, and the CPU baseline (oracle's zennit-structured restatement,
+K+1 batch replication like explainer.py:92) on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np
+import torch
+
+FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: dense fp32 MFMA (= vector) peak
+HBM_PEAK_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def synthetic_logmel(B, H=128, W=128, seed=1, device="cpu"):
+    g = torch.Generator().manual_seed(seed)
+    e = torch.empty(B, 1, H, W).exponential_(generator=g)
+    tilt = 10 ** (-3 * torch.arange(H).float() / (H - 1))
+    return torch.clamp(torch.log10(e * tilt[None, None, :, None] + 1e-7), min=-4).to(device)
+
+
+def gtzan128():
+    from drsa_audio_amd.model.create_model import VGGType
+    torch.manual_seed(0)
+    return VGGType(n_filters=(32, 32, 64, 64, 128), n_dense=128, pool_kernels=((2, 2),) * 5, dropout=0.4,
+                   input_size=(128, 128), conv_bn=False, dense_bn=False, block_depth=1).eval()
+
+
+def load_u():
+    return torch.from_numpy(np.load(os.path.join(ROOT, "tests", "golden", "u64_seed42.npy")))
+
+
+# --------------------------------------------------------------------------- FLOP model
+def kernel_macs(eng, B, K):
+    """Algorithmic multiply-accumulates per launch of each kernel tag for one batch of B
+    explained samples ('Algorithmic work')."""
+    macs = {}
+    rec = eng.last["stages"]
+    clones_below = False
+    for li in range(len(eng.stages) - 1, -1, -1):
+        st = eng.stages[li]
+        h, w = rec[li]["H"], rec[li]["W"]
+        if st.proj is not None:
+            d = st.cout
+            macs["projection_fwd"] = B * h * w * d * d * 2
+            macs["projection_bwd"] = B * h * w * (d * d + d * d + d * d)   # g1 U, clone 0, K blocks
+            clones_below = True
+        nq = (K + 1) if clones_below else 1
+        macs[f"conv_fwd:{st.name}"] = B * h * w * st.cout * st.cin * 9 * st.ng_fwd
+        tag = f"first_layer_bwd:{st.name}" if (li == 0 and st.w2_first is not None) else f"conv_bwd:{st.name}"
+        macs[tag] = B * nq * h * w * st.cout * st.cin * 9 * st.ng_bwd
+    for ds in eng.dense:
+        N, Kd = ds.W.shape
+        macs[f"linear_fwd:{ds.name}"] = B * N * Kd
+        macs[f"linear_bwd:{ds.name}"] = B * N * Kd
+    return macs
+
+
+# --------------------------------------------------------------------------- CPU baseline
+def cpu_baseline(budget_s=15.0):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import lrp_ref
+    from drsa_audio_amd.model.modify_model import ProjectionModel
+    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "64")), 16)
+    torch.set_num_threads(threads)
+    nm = {"features.0": ("wsquare", 1e-7), "features.3": ("gamma", 0.4, 1e-7), "features.6": ("gamma", 0.4, 1e-7),
+          "features.9": ("gamma", 0.2, 1e-7), "features.12": ("gamma", 0.1, 1e-7),
+          "classifier.0": ("epsilon", 1e-7), "classifier.3": ("epsilon", 1e-7), "classifier.6": ("epsilon", 1e-7)}
+    pm = ProjectionModel(gtzan128(), 7, load_u(), 4).eval()
+    chunk = 16
+    lrp_ref.subspace_heatmaps(pm, nm, 4, synthetic_logmel(1, seed=98), class_idx=3, mode="zennit")  # warm-up
+    n, dt, i = 0, 0.0, 0
+    while dt < budget_s and n < 1024:
+        x = synthetic_logmel(chunk, seed=100 + i)
+        t0 = time.perf_counter()
+        lrp_ref.subspace_heatmaps(pm, nm, 4, x, class_idx=3, mode="zennit")
+        dt += time.perf_counter() - t0
+        n += chunk
+        i += 1
+    cpu = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": n / dt, "unit": "explained samples/s", "cores": threads, "kind": "port",
+            "sample": f"{n} samples x (K+1=5 replicated rows), GTZAN-128 j=7 K=4, oracle zennit-structured "
+                      f"mode (5-pass Gamma + autograd like zennit.BasicHook), torch {torch.__version__} CPU, "
+                      f"{threads} threads, {cpu}, {dt:.1f} s"}
+
+
+# --------------------------------------------------------------------------- DRSA
+def drsa_bench(device, steps=200):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import drsa_ref
+    from gen_fixtures import drsa_inputs
+    from drsa_audio_amd.xai.drsa.drsa import DrsaWorkspace, drsa_run
+    N, d, K = 20000, 64, 4
+    A, C = drsa_inputs(N, d, 3)
+    U0 = np.load(os.path.join(ROOT, "tests", "golden", "u64_seed42.npy"))
+    Ag, Cg, Ug = (torch.from_numpy(v).to(device) for v in (A, C, U0))
+    ws = DrsaWorkspace(N, d, K, device)
+    s = torch.cuda.Stream(device)
+    with torch.cuda.stream(s):
+        drsa_run(Ag, Cg, Ug, K, 4, ws)                       # warm-up (graph instantiate)
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        U, traj = drsa_run(Ag, Cg, Ug, K, steps, ws)
+        torch.cuda.synchronize(device)
+        dt = time.perf_counter() - t0
+    traj = traj.cpu().numpy()
+    # objective vs the CPU restatement of drsa.py for the first 10 steps
+    Ur, ref = torch.from_numpy(U0), []
+    At, Ct = torch.from_numpy(A), torch.from_numpy(C)
+    for _ in range(10):
+        Ur, f, _ = drsa_ref.step(At, Ct, Ur, K)
+        ref.append(f)
+    rel = float(np.max(np.abs(traj[:10] - np.array(ref)) / np.abs(np.array(ref))))
+    flop = 8.0 * N * d * d
+    return {"config": "C3: N=20000, d=64, K=4 (synthetic normalised A=|N(0,1)|, C~N(0,1))",
+            "ms_per_step": dt / steps * 1e3, "vector_steps_per_s": N * steps / dt,
+            "tflops_algorithmic": flop * steps / dt / 1e12, "steps": steps,
+            "objective_max_rel_err_vs_oracle_10_steps": rel, "objective_final": float(traj[-1])}
+
+
+# --------------------------------------------------------------------------- main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=512, help="explained samples per GPU per step")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-drsa", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    from drsa_audio_amd.utils.constants import LRP_NAME_MAP_GTZAN
+    from drsa_audio_amd.xai.explain.explainer import HeatmapGenerator
+    from drsa_audio_amd.engine import get_engine
+
+    B, K = args.batch, 4
+    model = gtzan128().to(device)
+    hg = HeatmapGenerator(model, load_u(), LRP_NAME_MAP_GTZAN, "blues", num_concepts=K, layer_idx=7, device=device)
+    x = synthetic_logmel(B, seed=1 + rank, device=device)
+
+    for _ in range(args.warmup):
+        hg.generate_subspace_heatmaps(x, to_host=False)
+    torch.cuda.synchronize(device)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        hg.generate_subspace_heatmaps(x, to_host=False)
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t)
+    ms = dt / args.steps * 1e3
+    value = world * B * args.steps / dt
+
+    # ---- per-kernel timing (HIP events on the launch stream), separate traced steps ----
+    eng = get_engine(hg.projectionmodel, hg.composite)
+    eng.trace = []
+    for _ in range(3):
+        hg.generate_subspace_heatmaps(x, to_host=False)
+    torch.cuda.synchronize(device)
+    per = {}
+    for tag, e0, e1 in eng.trace:
+        per.setdefault(tag, []).append(e0.elapsed_time(e1))
+    eng.trace = None
+    macs = kernel_macs(eng, B, K)
+    kernels = {}
+    for tag, ts in per.items():
+        avg = float(np.mean(ts))
+        m = macs.get(tag)
+        kernels[tag] = {"avg_ms": avg, "launches": len(ts)}
+        if m:
+            kernels[tag]["tflops"] = 2.0 * m / (avg * 1e-3) / 1e12
+    dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
+    dom_ach = kernels[dom].get("tflops", 0.0)
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            with open(pmc_path) as fh:
+                pm = json.load(fh)
+            traffic = pm.get("per_launch_bytes", {}).get(dom)
+        except Exception:
+            traffic = None
+    total_macs = sum(macs.values())
+
+    # ---- secondary: standard LRP (C2, bs=64) ----
+    from drsa_audio_amd.zennit.composites import NameMapComposite
+    from drsa_audio_amd.xai.explain.attribute import compute_relevances
+    comp = NameMapComposite(LRP_NAME_MAP_GTZAN)
+    x64 = synthetic_logmel(64, seed=7 + rank, device=device)
+    for _ in range(3):
+        compute_relevances(model, x64, comp, class_idx=3)
+    torch.cuda.synchronize(device)
+    t1 = time.perf_counter()
+    for _ in range(10):
+        compute_relevances(model, x64, comp, class_idx=3)
+    torch.cuda.synchronize(device)
+    c2 = 64 * 10 / (time.perf_counter() - t1)
+    # bs=64 explained samples (same path, C2 batch size)
+    x64b = x64
+    for _ in range(3):
+        hg.generate_subspace_heatmaps(x64b, to_host=False)
+    torch.cuda.synchronize(device)
+    t1 = time.perf_counter()
+    for _ in range(10):
+        hg.generate_subspace_heatmaps(x64b, to_host=False)
+    torch.cuda.synchronize(device)
+    bs64 = 64 * 10 / (time.perf_counter() - t1)
+
+    drsa = None
+    if not args.no_drsa and rank == 0:
+        drsa = drsa_bench(device)
+    cpu = None
+    if not args.no_cpu_baseline and rank == 0 and world == 1:
+        cpu = cpu_baseline()
+
+    if rank == 0:
+        out = {
+            "metric": "explained samples/sec (LRP+DRSA k=4)",
+            "value": value,
+            "unit": "explained samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (seeded log-mel-like 128x128 batches; random-init GTZAN-128 weights, "
+                    "torch.manual_seed(0); U = ortho_group.rvs(64) seed 42)",
+            "config": {"workload": "GTZAN-128 HeatmapGenerator: LRP (WSquare/Gamma/Epsilon name map) + DRSA "
+                                   "subspace heatmaps, K=4 at layer j=7 (conv3 block, d=64), sorted info dict",
+                       "global_batch": B * world, "per_gpu_batch": B, "input": "128x128 log-mel",
+                       "parallelism": f"data-parallel x{world} (no collective on the data path)"},
+            "roofline": {"bound": "mfma", "kernel": dom, "achieved": dom_ach, "peak": FP32_MFMA_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": dom_ach / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic},
+            "whole_path": {"algorithmic_gflop_per_sample": 2.0 * total_macs / B / 1e9,
+                           "achieved_tflops": 2.0 * total_macs * value / B / world / 1e12},
+            "kernels": kernels,
+            "secondary": {"standard_lrp_c2_bs64_samples_per_s": c2 * world,
+                          "explained_samples_per_s_bs64": bs64 * world, "drsa": drsa},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -115,6 +115,17 @@ class LRPEngine:
             self._prepare_conv(st)
         self._buffers: Dict[tuple, dict] = {}
         self.last: Optional[dict] = None
+        self.trace: Optional[list] = None      # set to [] to record (tag, start_event, end_event)
+
+    def _call(self, tag: str, name: str, *args) -> None:
+        if self.trace is None:
+            _capi.call(name, *args)
+            return
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        _capi.call(name, *args)
+        e1.record()
+        self.trace.append((tag, e0, e1))
 
     # ------------------------------------------------------------------ parse
     def _parse(self, model, rules, merge_bn):
@@ -337,16 +348,16 @@ class LRPEngine:
                 out = self._buf((li, "y"), (B, st.cout, h // 2, w // 2))
                 amax = self._buf((li, "amax"), (B, st.cout, h // 2, w // 2), torch.uint8)
                 den = self._buf((li, "den"), (B, st.cout, h // 2, w // 2)) if need_den else None
-                _capi.call("drsa_amd_conv_fwd", cur.data_ptr(), st.wts_fwd.data_ptr(), st.bias3.data_ptr(),
-                           _capi.ptr(den_map), out.data_ptr(), amax.data_ptr(), _capi.ptr(den), B, st.cin, st.cout,
+                self._call(f"conv_fwd:{st.name}", "drsa_amd_conv_fwd", cur.data_ptr(), st.wts_fwd.data_ptr(),
+                           st.bias3.data_ptr(), _capi.ptr(den_map), out.data_ptr(), amax.data_ptr(), _capi.ptr(den), B, st.cin, st.cout,
                            h, w, st.ng_fwd, 1, s)
                 rec.update(y=out, amax=amax, den=den, Hout=h // 2, Wout=w // 2)
                 cur, h, w = out, h // 2, w // 2
             else:
                 a = self._buf((li, "a"), (B, st.cout, h, w))
                 den = self._buf((li, "den"), (B, st.cout, h, w)) if need_den else None
-                _capi.call("drsa_amd_conv_fwd", cur.data_ptr(), st.wts_fwd.data_ptr(), st.bias3.data_ptr(),
-                           _capi.ptr(den_map), a.data_ptr(), None, _capi.ptr(den), B, st.cin, st.cout, h, w,
+                self._call(f"conv_fwd:{st.name}", "drsa_amd_conv_fwd", cur.data_ptr(), st.wts_fwd.data_ptr(),
+                           st.bias3.data_ptr(), _capi.ptr(den_map), a.data_ptr(), None, _capi.ptr(den), B, st.cin, st.cout, h, w,
                            st.ng_fwd, 0, s)
                 rec.update(a=a, den=den)
                 if st.proj is not None:
@@ -358,7 +369,7 @@ class LRPEngine:
                         amax = self._buf((li, "amax"), (B, st.cout, h // 2, w // 2), torch.uint8)
                     else:
                         pooled = amax = None
-                    _capi.call("drsa_amd_projection_fwd", a.data_ptr(), P.U.data_ptr(), hb.data_ptr(), ap.data_ptr(),
+                    self._call("projection_fwd", "drsa_amd_projection_fwd", a.data_ptr(), P.U.data_ptr(), hb.data_ptr(), ap.data_ptr(),
                                _capi.ptr(pooled), _capi.ptr(amax), B, st.cout, h, w, 1 if P.pool_after else 0, s)
                     rec.update(h=hb, ap=ap, amax=amax)
                     if P.pool_after:
@@ -381,7 +392,7 @@ class LRPEngine:
             N, Kd = ds.W.shape
             z = self._buf(("d", di, "z"), (B, N))
             act = self._buf(("d", di, "a"), (B, N)) if ds.relu_after else None
-            _capi.call("drsa_amd_linear_fwd", inp.data_ptr(), ds.W.data_ptr(), _capi.ptr(ds.b), z.data_ptr(),
+            self._call(f"linear_fwd:{ds.name}", "drsa_amd_linear_fwd", inp.data_ptr(), ds.W.data_ptr(), _capi.ptr(ds.b), z.data_ptr(),
                        _capi.ptr(act), B, N, Kd, s)
             dense_recs.append({"x": inp, "z": z, "a": act})
             inp = act if act is not None else z
@@ -430,14 +441,14 @@ class LRPEngine:
             xmode = XM_MUL if ds.rule_kind == "epsilon" else XM_NONE
             den_flat = None if den is None else den.reshape(B, -1)
             if di == len(self.dense) - 1 and cls is not None:
-                _capi.call("drsa_amd_linear_bwd", None, cls.data_ptr(), 1 if one_hot else 0, rec["z"].data_ptr(),
+                self._call(f"linear_bwd:{ds.name}", "drsa_amd_linear_bwd", None, cls.data_ptr(), 1 if one_hot else 0, rec["z"].data_ptr(),
                            relu_mask, 1 if ds.rule_kind == "epsilon" else 0, ds.eps, ds.W.data_ptr(),
                            x_mask.data_ptr(), xmode, _capi.ptr(den_flat), post, eps_post, out.data_ptr(), B, N, Kd, s)
             else:
                 if R is None:
                     raise ValueError("backward needs a seed or class indices")
                 R = R.to(self.device, torch.float32).contiguous()
-                _capi.call("drsa_amd_linear_bwd", R.data_ptr(), None, 0, rec["z"].data_ptr(), relu_mask,
+                self._call(f"linear_bwd:{ds.name}", "drsa_amd_linear_bwd", R.data_ptr(), None, 0, rec["z"].data_ptr(), relu_mask,
                            1 if ds.rule_kind == "epsilon" else 0, ds.eps, ds.W.data_ptr(), x_mask.data_ptr(), xmode,
                            _capi.ptr(den_flat), post, eps_post, out.data_ptr(), B, N, Kd, s)
             R = out
@@ -457,7 +468,7 @@ class LRPEngine:
                 post, den, eps = (POST_DIV, rec["den"], st.eps) if st.den_kind is not None else (POST_MASK, None, 0.0)
                 if not P.mask:
                     raise EngineError("engine: projection without SubspaceHook is not supported yet")
-                _capi.call("drsa_amd_projection_bwd", g.data_ptr(), _capi.ptr(rec["amax"] if P.pool_after else None),
+                self._call("projection_bwd", "drsa_amd_projection_bwd", g.data_ptr(), _capi.ptr(rec["amax"] if P.pool_after else None),
                            rec["ap"].data_ptr(), rec["h"].data_ptr(), rec["a"].data_ptr(),
                            _capi.ptr(den if post == POST_DIV else None), P.U.data_ptr(), G.data_ptr(), B, st.cout,
                            h, w, K, P.eps_inv, eps, 1 if fan else 0, s)
@@ -472,11 +483,11 @@ class LRPEngine:
                 post, den, eps = POST_NONE, None, 0.0
             if li == 0 and st.w2_first is not None:
                 out = self._buf((li, "R"), (Bq, 1, h, w))
-                _capi.call("drsa_amd_first_layer_bwd", g.data_ptr(), _capi.ptr(amax_in), st.w2_first.data_ptr(),
+                self._call(f"first_layer_bwd:{st.name}", "drsa_amd_first_layer_bwd", g.data_ptr(), _capi.ptr(amax_in), st.w2_first.data_ptr(),
                            out.data_ptr(), Bq, clones, st.cout, h, w, s)
             else:
                 out = self._buf((li, "R"), (Bq, st.cin, h, w))
-                _capi.call("drsa_amd_conv_bwd", g.data_ptr(), _capi.ptr(amax_in), st.wts_bwd.data_ptr(),
+                self._call(f"conv_bwd:{st.name}", "drsa_amd_conv_bwd", g.data_ptr(), _capi.ptr(amax_in), st.wts_bwd.data_ptr(),
                            x_in.data_ptr() if (st.xmode_bwd != XM_NONE or post != POST_NONE) else None,
                            _capi.ptr(den), out.data_ptr(), Bq, clones, st.cout, st.cin, h, w, st.ng_bwd,
                            st.xmode_bwd, post, float(eps), s)
@@ -507,7 +518,7 @@ class LRPEngine:
             "subspace_relevances": torch.empty(B, K, device=self.device),
             "mask": torch.empty(B, K, dtype=torch.int64, device=self.device),
         }
-        _capi.call("drsa_amd_heatmap_sort", hm.data_ptr(), B, K, HW, out["standard_heatmaps"].data_ptr(),
+        self._call("heatmap_sort", "drsa_amd_heatmap_sort", hm.data_ptr(), B, K, HW, out["standard_heatmaps"].data_ptr(),
                    out["standard_relevance"].data_ptr(), out["subspace_heatmaps"].data_ptr(),
                    out["subspace_relevances"].data_ptr(), out["mask"].data_ptr(), _capi.stream_ptr(self.device))
         return out
