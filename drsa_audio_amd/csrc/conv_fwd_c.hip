@@ -1,0 +1,11 @@
+// Instantiations of the 3x3 conv kernel (lrp_conv_kernel.h), split across files so the
+// build compiles them in parallel.
+#include "lrp_conv_kernel.h"
+
+namespace drsa_conv {
+static const Entry kTableFwdC_e[] = {
+    FWD_SET(64, 64, 8),
+    FWD_SET(64, 128, 8),
+};
+extern const Table kTableFwdC = {kTableFwdC_e, (int)(sizeof(kTableFwdC_e) / sizeof(kTableFwdC_e[0]))};
+}  // namespace drsa_conv

@@ -1,0 +1,359 @@
+// 3x3 'same' convolution on fp32 MFMA (v_mfma_f32_32x32x2_f32) for the LRP engine.
+//
+// One templated implicit-GEMM kernel serves the whole conv trunk of the VGG-type CNN
+// (reference cxai/model/create_model.py:100-137) in both directions:
+//
+//   forward  (FWD_POOL / FWD_RELU):  z = conv(x; W) + b  ->  y = relu(z)  [-> 2x2 max-pool + argmax]
+//            plus, in the same pass over the input tile, the LRP denominator of the layer's rule:
+//            Gamma  (zennit 0.5.1):  den = (conv(x+; W+) + b+) + (conv(x-; W-) + b-)
+//            Epsilon:                               den = z
+//            WSquare / Flat:                        den = precomputed input-independent map
+//            den is stored only where the relevance can arrive: at the pool argmax.
+//   backward (BWD): the transposed conv as a 'same' conv with flipped/transposed weights,
+//            R_in = x+ (.) J^T_{W+} g  [+ x- (.) J^T_{W-} g]   (Gamma; g_- vanishes because every
+//            conv is followed by ReLU), or x (.) J^T_W g (Epsilon) or J^T g (WSquare/Flat/plain),
+//            with the pool-backward + ReLU-backward folded into the A-operand prologue (AMODE 1:
+//            g lives at pool resolution plus an argmax byte) and the NEXT layer's division folded
+//            into the epilogue (POST_DIV: g_next = [x > 0] R / stab(den_next)).
+//
+// GEMM view: M = output pixels of a TH x TW tile (window-major order so that every 2x2 pool
+// window lands in 4 consecutive accumulator registers of one lane), N = output channels
+// (32-wide MFMA tiles), K = 9 * Cin in the order k = ci*9 + (ky*3 + kx) (chunks of CIC input
+// channels staged in LDS with the halo; weights [k][co] staged next to them).  Every output
+// is one k-ordered fp32 fma chain (MFMA f32 semantics), independent of the chunking, which
+// is what oracle/lrp_exact.c reproduces bit for bit.
+#pragma once
+#include "common.h"
+#include "lrp_conv.h"
+
+namespace drsa_conv {
+
+constexpr int kThreads = 256;
+
+template <int V, int M>
+constexpr int round_up() { return (V + M - 1) / M * M; }
+
+// halo row stride: the 32 lanes of one ds_read_b32 group read a (16/MW x 2) grid of
+// MW*2-pixel runs; RS = 16 (mod 32) for 2 rows x 16, RS = 8 (mod 32) for 4 rows x 8 puts the
+// runs on disjoint banks.
+constexpr int halo_stride(int hx, int mw) {
+  int r = hx;
+  const int want = (mw == 8) ? 16 : 8;
+  while (r % 32 != want) ++r;
+  return r;
+}
+
+enum AMode { A_DENSE = 0, A_POOLSPARSE = 1 };
+enum Epi { EPI_FWD_POOL = 0, EPI_FWD_RELU = 1, EPI_BWD = 2 };
+
+template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI>
+struct ConvCfg {
+  static constexpr int HY = TH + 2, HX = TW + 2;
+  static constexpr int RS = halo_stride(HX, MW);
+  static constexpr int PLANE_RAW = HY * RS;
+  static constexpr int PLANE = PLANE_RAW + ((PLANE_RAW % 32) == 0 ? 4 : 0);
+  static constexpr int MTH = 16 / MW;      // M-tile height (pixels)
+  static constexpr int MTW = 2 * MW;       // M-tile width (pixels)
+  static constexpr int MTX = TW / MTW;     // M-tiles per tile row
+  static constexpr int MT = (TH / MTH) * MTX;
+  static constexpr int NT = COUT / 32;
+  static constexpr int WM = MT >= 4 ? 4 : MT;
+  static constexpr int WN = (4 / WM) < NT ? (4 / WM) : NT;   // waves >= WM*WN idle (tiny layers)
+  static constexpr int MPW = MT / WM;      // m-tiles per wave
+  static constexpr int NPW = NT / WN;      // n-tiles per wave
+  static constexpr int KC = 9 * CIC;
+  static constexpr int KCP = round_up<KC, 2>();
+  static constexpr int NCHUNK = CIN / CIC;
+  static constexpr size_t lds_floats = (size_t)CIC * PLANE + (size_t)NG * KCP * COUT;
+  static_assert(TH % MTH == 0 && TW % MTW == 0, "tile must be a multiple of the M-tile");
+  static_assert(COUT % 32 == 0, "COUT must be padded to 32");
+  static_assert(CIN % CIC == 0, "CIN must be a multiple of the chunk");
+  static_assert(MT % WM == 0 && NT % WN == 0 && WM * WN <= 4, "wave split");
+};
+
+template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI>
+__global__ __launch_bounds__(kThreads) void conv3x3_kernel(ConvArgs a) {
+  using Cfg = ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AMODE, EPI>;
+  constexpr int HY = Cfg::HY, HX = Cfg::HX, RS = Cfg::RS, PLANE = Cfg::PLANE;
+  constexpr int MTH = Cfg::MTH, MTW = Cfg::MTW, MTX = Cfg::MTX;
+  constexpr int WM = Cfg::WM, MPW = Cfg::MPW, NPW = Cfg::NPW;
+  constexpr int KC = Cfg::KC, KCP = Cfg::KCP;
+
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* halo = smem;                          // [CIC][PLANE]
+  float* wl = smem + CIC * PLANE;              // [NG][KCP][COUT]
+
+  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int H = a.H, W = a.W;
+  const int tiles_x = (W + TW - 1) / TW;
+  const int ty0 = (blockIdx.x / tiles_x) * TH;
+  const int tx0 = (blockIdx.x % tiles_x) * TW;
+  const int bq = blockIdx.y;                  // batch index (incl. clones)
+  const int bs = bq / a.clones;               // sample index (shared forward state)
+  const int wm = w % WM, wn = w / WM;
+  const bool active = w < WM * Cfg::WN;
+  const int h = lane >> 5;
+
+  // MFMA orientation: D[channel][pixel] = W^T[channel][k] * X[k][pixel]
+  //   A operand (lane l): W[k = k0 + (l>>5)][co = n0 + (l&31)]
+  //   B operand (lane l): X[k = k0 + (l>>5)][pixel p = l&31 of the m-tile]
+  //   D: lane l holds pixel p = l&31, registers r hold channels n0 + (r&3) + 8(r>>2) + 4(l>>5)
+  // pixel p of an m-tile -> pool window win = p>>2, sub = p&3 (window-major order)
+  int pix_off[MPW], pix_y[MPW], pix_x[MPW];
+#pragma unroll
+  for (int u = 0; u < MPW; ++u) {
+    const int mt = wm * MPW + u;
+    const int p = lane & 31, win = p >> 2, sub = p & 3;
+    pix_y[u] = (mt / MTX) * MTH + 2 * (win / MW) + (sub >> 1);
+    pix_x[u] = (mt % MTX) * MTW + 2 * (win % MW) + (sub & 1);
+    pix_off[u] = pix_y[u] * RS + pix_x[u];
+  }
+
+  f32x16 acc[NG][MPW][NPW];
+#pragma unroll
+  for (int g = 0; g < NG; ++g)
+#pragma unroll
+    for (int u = 0; u < MPW; ++u)
+#pragma unroll
+      for (int v = 0; v < NPW; ++v)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[g][u][v][r] = 0.f;
+
+  for (int chunk = 0; chunk < Cfg::NCHUNK; ++chunk) {
+    const int c0 = chunk * CIC;
+    __syncthreads();
+    if constexpr (AMODE == A_DENSE) {
+      // ---- halo [CIC][HY][HX] straight from the NCHW input (loads issued before stores) ----
+      constexpr int NE = CIC * HY * HX, IT = (NE + kThreads - 1) / kThreads;
+      float v[IT];
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int idx = tid + it * kThreads;
+        const int ci = idx / (HY * HX), rem = idx % (HY * HX);
+        const int hy = rem / HX, hx = rem % HX;
+        const int gy = ty0 - 1 + hy, gx = tx0 - 1 + hx, c = c0 + ci;
+        v[it] = (idx < NE && gy >= 0 && gy < H && gx >= 0 && gx < W && c < a.cin)
+                    ? a.in[(((size_t)bq * a.cin + c) * H + gy) * W + gx] : 0.f;
+      }
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int idx = tid + it * kThreads;
+        if (idx < NE) {
+          const int ci = idx / (HY * HX), rem = idx % (HY * HX);
+          halo[ci * PLANE + (rem / HX) * RS + rem % HX] = v[it];
+        }
+      }
+    } else {
+      // ---- pool-sparse source: cells (g at pool resolution + argmax) cover the halo; each
+      //      cell writes its 2x2 pixels (value at the argmax position, zeros elsewhere) ----
+      constexpr int CY = TH / 2 + 2, CX = TW / 2 + 2, NE = CIC * CY * CX;
+      constexpr int IT = (NE + kThreads - 1) / kThreads;
+      const int H2 = H >> 1, W2 = W >> 1;
+      const int qy0 = (ty0 >> 1) - 1, qx0 = (tx0 >> 1) - 1;
+      float v[IT];
+      int sb[IT];
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int idx = tid + it * kThreads;
+        const int ci = idx / (CY * CX), rem = idx % (CY * CX);
+        const int cy = qy0 + rem / CX, cx = qx0 + rem % CX, c = c0 + ci;
+        const bool ok = idx < NE && cy >= 0 && cy < H2 && cx >= 0 && cx < W2 && c < a.cin;
+        v[it] = ok ? a.in[(((size_t)bq * a.cin + c) * H2 + cy) * W2 + cx] : 0.f;
+        sb[it] = ok ? (int)a.in_amax[(((size_t)bs * a.cin + c) * H2 + cy) * W2 + cx] : 0;
+      }
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int idx = tid + it * kThreads;
+        if (idx < NE) {
+          const int ci = idx / (CY * CX), rem = idx % (CY * CX);
+          const int ry = rem / CX, rx = rem % CX;
+          // cell (ry, rx) covers halo rows 2ry-1, 2ry and cols 2rx-1, 2rx (halo origin = pixel ty0-1)
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) {
+            const int hy = 2 * ry - 1 + (s4 >> 1), hx = 2 * rx - 1 + (s4 & 1);
+            if (hy >= 0 && hy < HY && hx >= 0 && hx < HX)
+              halo[ci * PLANE + hy * RS + hx] = (sb[it] == s4) ? v[it] : 0.f;
+          }
+        }
+      }
+    }
+    {
+      // ---- weights: rows [c0*9, c0*9 + KC) of every set, contiguous (k = ci*9 + tap) ----
+      constexpr int NV = NG * KCP * (COUT / 4), IT = (NV + kThreads - 1) / kThreads;
+      float4 wv[IT];
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int idx = tid + it * kThreads;
+        const int g = idx / (KCP * (COUT / 4)), rem = idx % (KCP * (COUT / 4));
+        const int k = rem / (COUT / 4), c4 = (rem % (COUT / 4)) * 4;
+        wv[it] = (idx < NV && k < KC)
+                     ? *reinterpret_cast<const float4*>(a.wts + ((size_t)g * 9 * CIN + c0 * 9 + k) * COUT + c4)
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int idx = tid + it * kThreads;
+        if (idx < NV) *reinterpret_cast<float4*>(wl + (size_t)idx * 4) = wv[it];
+      }
+    }
+    __syncthreads();
+    if (!active) continue;
+    // ---- MFMA over the chunk (unrolled by 9 k-steps = two channels: offsets repeat) ----
+#pragma unroll 9
+    for (int k0 = 0; k0 < KCP; k0 += 2) {
+      const int k = k0 + h;
+      const int ci = k / 9, tap = k - ci * 9;
+      const int off = (k < KC) ? ci * PLANE + (tap / 3) * RS + (tap % 3) : 0;
+      float xv[MPW];
+#pragma unroll
+      for (int u = 0; u < MPW; ++u) xv[u] = (KC % 2 == 0 || k < KC) ? halo[off + pix_off[u]] : 0.f;
+#pragma unroll
+      for (int v = 0; v < NPW; ++v) {
+        const int co = (wn * NPW + v) * 32 + (lane & 31);
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          const float wvv = wl[((size_t)g * KCP + k) * COUT + co];
+#pragma unroll
+          for (int u = 0; u < MPW; ++u) {
+            float x = xv[u];
+            if constexpr (EPI != EPI_BWD && NG == 3) {
+              x = (g == 0) ? x : (g == 1 ? fmaxf(x, 0.f) : fminf(x, 0.f));
+            } else if constexpr (EPI != EPI_BWD && NG == 2) {
+              x = (g == 0) ? x : fmaxf(x, 0.f);
+            }
+            acc[g][u][v] = mfma32(wvv, x, acc[g][u][v]);
+          }
+        }
+      }
+    }
+  }
+
+  // ---- epilogue: lane = pixel, registers = channels ----
+  if (!active) return;
+  const int sub = lane & 3;
+#pragma unroll
+  for (int u = 0; u < MPW; ++u) {
+    const int py = ty0 + pix_y[u], px = tx0 + pix_x[u];
+    const bool inside = py < H && px < W;   // partial tiles of small maps (windows are whole)
+#pragma unroll
+    for (int v = 0; v < NPW; ++v) {
+      const int n0 = (wn * NPW + v) * 32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = n0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const bool live = inside && co < a.cout;
+        if constexpr (EPI == EPI_FWD_POOL || EPI == EPI_FWD_RELU) {
+          const float b0 = (a.bias && co < a.cout) ? a.bias[co] : 0.f;
+          const float z = acc[0][u][v][r] + b0;
+          float y = z > 0.f ? z : 0.f;
+          if (z != z) y = z;   // relu(NaN) = NaN (torch semantics)
+          float den = 0.f;
+          if (a.out_den) {
+            if (a.den_map) {
+              den = live ? a.den_map[((size_t)co * H + py) * W + px] : 0.f;
+            } else if constexpr (NG >= 2) {
+              const float bp = (a.bias && co < a.cout) ? a.bias[COUT + co] : 0.f;
+              const float bn = (a.bias && co < a.cout) ? a.bias[2 * COUT + co] : 0.f;
+              const float z0 = acc[1][u][v][r] + bp;
+              float z1 = bn;
+              if constexpr (NG == 3) z1 = acc[2][u][v][r] + bn;
+              den = z0 + z1;
+            } else {
+              // Epsilon: den = conv(x; W) + b_den (b_den = b, or 0 under zero_params=['bias'])
+              den = acc[0][u][v][r] + ((a.bias && co < a.cout) ? a.bias[COUT + co] : 0.f);
+            }
+          }
+          if constexpr (EPI == EPI_FWD_POOL) {
+            // torch max_pool2d: first maximum in row-major window order; NaN wins
+            const int base = lane & ~3;
+            float yy[4], dd[4];
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+              yy[s4] = __shfl(y, base + s4, 64);
+              dd[s4] = __shfl(den, base + s4, 64);
+            }
+            int am = 0;
+            float m = yy[0];
+#pragma unroll
+            for (int s4 = 1; s4 < 4; ++s4)
+              if (yy[s4] > m || (yy[s4] != yy[s4] && m == m)) { m = yy[s4]; am = s4; }
+            if (sub == 0 && live) {
+              const int H2 = H >> 1, W2 = W >> 1;
+              const size_t o = (((size_t)bq * a.cout + co) * H2 + (py >> 1)) * W2 + (px >> 1);
+              a.out[o] = m;
+              a.out_amax[o] = (uint8_t)am;
+              if (a.out_den) a.out_den[o] = dd[am];
+            }
+          } else if (live) {
+            const size_t o = (((size_t)bq * a.cout + co) * H + py) * W + px;
+            a.out[o] = y;
+            if (a.out_den) a.out_den[o] = den;
+          }
+        } else {   // EPI_BWD
+          if (!live) continue;
+          const size_t os = (((size_t)bs * a.cout + co) * H + py) * W + px;
+          const size_t oq = (((size_t)bq * a.cout + co) * H + py) * W + px;
+          float R;
+          if (a.xmode == XM_NONE) {
+            R = acc[0][u][v][r];
+          } else {
+            const float x = a.x[os];
+            if (a.xmode == XM_MUL) {
+              R = x * acc[0][u][v][r];
+            } else {   // XM_SPLIT: x+ * acc0 + x- * acc1
+              R = fmaxf(x, 0.f) * acc[0][u][v][r];
+              if constexpr (NG >= 2) R += fminf(x, 0.f) * acc[1][u][v][r];
+            }
+          }
+          if (a.post == POST_DIV) {
+            const float x = a.x[os];
+            R = (x > 0.f) ? R / stab(a.den[os], a.eps) : 0.f;
+          } else if (a.post == POST_MASK) {
+            R = (a.x[os] > 0.f) ? R : 0.f;
+          }
+          a.out[oq] = R;
+        }
+      }
+    }
+  }
+}
+
+typedef void (*KernFn)(ConvArgs);
+
+struct Entry {
+  int cin_p, cout_p, th, tw, mw, cic, ng, amode, epi;
+  KernFn fn;
+  size_t lds;
+};
+
+#define CONV_ENTRY(CIN, COUT, TH, TW, MW, CIC, NG, AM, EP)                                                 \
+  drsa_conv::Entry{CIN, COUT, TH, TW, MW, CIC, NG, AM, EP,                                                 \
+                   drsa_conv::conv3x3_kernel<CIN, COUT, TH, TW, MW, CIC, NG, AM, EP>,                      \
+                   drsa_conv::ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AM, EP>::lds_floats * sizeof(float)}
+
+// tile by output width: W >= 32 -> 8x32 (MW 8); 8 < W < 32 -> 8x16 (MW 8); W <= 8 -> 8x8 (MW 4)
+#define CONV_FAMILY(CIN, COUT, CIC, NG, AM, EP)                      \
+  CONV_ENTRY(CIN, COUT, 8, 32, 8, CIC, NG, AM, EP),                  \
+  CONV_ENTRY(CIN, COUT, 8, 16, 8, CIC, NG, AM, EP),                  \
+  CONV_ENTRY(CIN, COUT, 8, 8, 4, CIC, NG, AM, EP)
+
+#define FWD_SET(CIN, COUT, CIC)                                                        \
+  CONV_FAMILY(CIN, COUT, CIC, 1, drsa_conv::A_DENSE, drsa_conv::EPI_FWD_POOL),          \
+  CONV_FAMILY(CIN, COUT, CIC, 2, drsa_conv::A_DENSE, drsa_conv::EPI_FWD_POOL),          \
+  CONV_FAMILY(CIN, COUT, CIC, 3, drsa_conv::A_DENSE, drsa_conv::EPI_FWD_POOL),          \
+  CONV_FAMILY(CIN, COUT, CIC, 1, drsa_conv::A_DENSE, drsa_conv::EPI_FWD_RELU),          \
+  CONV_FAMILY(CIN, COUT, CIC, 2, drsa_conv::A_DENSE, drsa_conv::EPI_FWD_RELU),          \
+  CONV_FAMILY(CIN, COUT, CIC, 3, drsa_conv::A_DENSE, drsa_conv::EPI_FWD_RELU)
+
+#define BWD_SET(CIN, COUT, CIC)                                                        \
+  CONV_FAMILY(CIN, COUT, CIC, 1, drsa_conv::A_DENSE, drsa_conv::EPI_BWD),               \
+  CONV_FAMILY(CIN, COUT, CIC, 2, drsa_conv::A_DENSE, drsa_conv::EPI_BWD),               \
+  CONV_FAMILY(CIN, COUT, CIC, 1, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD),          \
+  CONV_FAMILY(CIN, COUT, CIC, 2, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD)
+
+struct Table {
+  const Entry* entries;
+  int n;
+};
+
+}  // namespace drsa_conv

@@ -345,6 +345,89 @@ __global__ __launch_bounds__(256) void first_layer_bwd_kernel(const float* __res
   }
 }
 
+// Pool-sparse variant (the VGG case: conv0 -> ReLU -> MaxPool2d(2)).  One thread per pool
+// cell = 2x2 output pixels; the 3x3 cell neighbourhood (gp + argmax) is staged in LDS per
+// channel chunk; the 4x4 pixel patch those pixels read is rebuilt in registers (each patch
+// slot maps to exactly one cell and one sub-position, so it is a compile-time select), then
+// 9 fmas per pixel and channel in the dense chain order (channel, dy, dx) — the same chain
+// as the dense kernel above and oracle/lrp_exact.c, zeros included.
+constexpr int FQ_Y = 8, FQ_X = 32, FQ_C = 8;
+
+__global__ __launch_bounds__(256) void first_layer_bwd_pooled_kernel(const float* __restrict__ g,
+                                                                     const uint8_t* __restrict__ amax,
+                                                                     const float* __restrict__ w2,
+                                                                     float* __restrict__ out, int C, int H, int W,
+                                                                     int clones) {
+  constexpr int RY = FQ_Y + 2, RX = FQ_X + 2;
+  __shared__ float sg[FQ_C][RY][RX + 1];
+  __shared__ uint8_t sa[FQ_C][RY][RX + 4];
+  const int tid = threadIdx.x;
+  const int H2 = H / 2, W2 = W / 2;
+  const int tiles_x = (W2 + FQ_X - 1) / FQ_X;
+  const int qy0 = (blockIdx.x / tiles_x) * FQ_Y, qx0 = (blockIdx.x % tiles_x) * FQ_X;
+  const int bq = blockIdx.y, bs = bq / clones;
+  const int ty = tid / FQ_X, tx = tid % FQ_X;
+  const int qy = qy0 + ty, qx = qx0 + tx;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < C; c0 += FQ_C) {
+    __syncthreads();
+    constexpr int NE = FQ_C * RY * RX;
+#pragma unroll
+    for (int it = 0; it < (NE + 255) / 256; ++it) {
+      const int idx = tid + it * 256;
+      if (idx < NE) {
+        const int ci = idx / (RY * RX), rem = idx % (RY * RX);
+        const int ry = rem / RX, rx = rem % RX;
+        const int cy = qy0 - 1 + ry, cx = qx0 - 1 + rx, c = c0 + ci;
+        float v = 0.f;
+        uint8_t s = 255;
+        if (c < C && cy >= 0 && cy < H2 && cx >= 0 && cx < W2) {
+          v = g[(((size_t)bq * C + c) * H2 + cy) * W2 + cx];
+          s = amax[(((size_t)bs * C + c) * H2 + cy) * W2 + cx];
+        }
+        sg[ci][ry][rx] = v;
+        sa[ci][ry][rx] = s;
+      }
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int ci = 0; ci < FQ_C; ++ci) {
+      const int c = c0 + ci;
+      float wv[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) wv[t] = (c < C) ? w2[c * 9 + t] : 0.f;
+      // patch P[i][j]: pixel (2qy - 1 + i, 2qx - 1 + j); its cell row offset and sub-row:
+      //   i = 0 -> cell qy-1, sub-row 1;  i = 1 -> qy, 0;  i = 2 -> qy, 1;  i = 3 -> qy+1, 0
+      float P[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int dcy = (i == 0) ? -1 : ((i == 3) ? 1 : 0), sr = (i == 1 || i == 3) ? 0 : 1;
+          const int dcx = (j == 0) ? -1 : ((j == 3) ? 1 : 0), sc = (j == 1 || j == 3) ? 0 : 1;
+          const uint8_t s = sa[ci][ty + 1 + dcy][tx + 1 + dcx];
+          P[i][j] = (s == (uint8_t)(sr * 2 + sc)) ? sg[ci][ty + 1 + dcy][tx + 1 + dcx] : 0.f;
+        }
+#pragma unroll
+      for (int py = 0; py < 2; ++py)
+#pragma unroll
+        for (int px = 0; px < 2; ++px)
+#pragma unroll
+          for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+            for (int dx = -1; dx <= 1; ++dx)
+              acc[py * 2 + px] = fmaf(P[py + 1 + dy][px + 1 + dx], wv[(1 - dy) * 3 + (1 - dx)], acc[py * 2 + px]);
+    }
+  }
+  if (qy < H2 && qx < W2) {
+#pragma unroll
+    for (int py = 0; py < 2; ++py) {
+      float2 v = make_float2(acc[py * 2], acc[py * 2 + 1]);
+      *reinterpret_cast<float2*>(out + ((size_t)bq * H + 2 * qy + py) * W + 2 * qx) = v;
+    }
+  }
+}
+
 // den[co][y][x] = sum_ci sum_{in-bounds taps} w2[co][ci][ky][kx] * 1 + b2[co]
 __global__ void first_layer_den_kernel(const float* __restrict__ w2, const float* __restrict__ b2, float* __restrict__ den,
                                        int C, int CI, int H, int W) {
@@ -520,9 +603,17 @@ int drsa_amd_projection_bwd(const float* gp, const uint8_t* amax, const float* a
 int drsa_amd_first_layer_bwd(const float* g, const uint8_t* amax, const float* w2f, float* out, int Bq, int clones,
                              int C, int H, int W, void* stream) {
   DRSA_REQUIRE(Bq > 0 && clones > 0 && Bq % clones == 0, "first_layer_bwd: bad batch");
-  const dim3 grid(((H + FL_TH - 1) / FL_TH) * ((W + FL_TW - 1) / FL_TW), Bq);
-  hipLaunchKernelGGL(first_layer_bwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, g, amax, w2f, out, C, H, W,
-                     clones);
+  if (amax) {
+    DRSA_REQUIRE(H % 2 == 0 && W % 4 == 0, "first_layer_bwd: pooled path needs even H and W % 4 == 0");
+    const int H2 = H / 2, W2 = W / 2;
+    const dim3 grid(((H2 + FQ_Y - 1) / FQ_Y) * ((W2 + FQ_X - 1) / FQ_X), Bq);
+    hipLaunchKernelGGL(first_layer_bwd_pooled_kernel, grid, dim3(256), 0, (hipStream_t)stream, g, amax, w2f, out, C,
+                       H, W, clones);
+  } else {
+    const dim3 grid(((H + FL_TH - 1) / FL_TH) * ((W + FL_TW - 1) / FL_TW), Bq);
+    hipLaunchKernelGGL(first_layer_bwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, g, amax, w2f, out, C, H, W,
+                       clones);
+  }
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;
 }
