@@ -21,4 +21,5 @@ struct ConvArgs {
   int clones;               // batch index / clones = sample index
   int xmode, post;
   float eps;
+  int dbg;                  // ablation only (DRSA_AMD_CONV_DBG): 1 no staging loads, 2 no epilogue I/O, 4 no MFMA
 };

@@ -3,6 +3,8 @@
 #include "lrp_conv.h"
 #include "lrp_conv_kernel.h"
 
+#include <stdlib.h>
+
 // ---------------------------------------------------------------------------
 // dispatch table
 // ---------------------------------------------------------------------------
@@ -19,9 +21,15 @@ const drsa_conv::Table* kTables[] = {&drsa_conv::kTableFwdA, &drsa_conv::kTableF
 
 int pad32(int c) { return (c + 31) / 32 * 32; }
 
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+
 const Entry* find(int cin_p, int cout_p, int W, int ng, int amode, int epi) {
   int th = 8, tw, mw;
-  if (W >= 32) { tw = 32; mw = 8; }
+  static const int th16 = env_int("DRSA_AMD_CONV_TH16", 0);
+  if (W >= 32) { tw = 32; mw = 8; th = (th16 && cout_p == 32 && ng <= 2) ? 16 : 8; }
   else if (W > 8) { tw = 16; mw = 8; }
   else { tw = 8; mw = 4; }
   for (const drsa_conv::Table* t : kTables)
@@ -50,6 +58,7 @@ int launch(const Entry* e, const ConvArgs& args, int batch, hipStream_t s) {
 }
 
 int cin_pad(int cin) { return cin == 1 ? 1 : pad32(cin); }
+
 
 }  // namespace
 
@@ -95,6 +104,8 @@ int drsa_amd_conv_bwd(const float* g, const uint8_t* g_amax, const float* wts, c
   ConvArgs a{};
   a.in = g; a.in_amax = g_amax; a.wts = wts; a.x = x; a.den = den; a.out = out; a.H = H; a.W = W;
   a.cin = cin; a.cout = cout; a.clones = clones; a.xmode = xmode; a.post = post; a.eps = eps;
+  static const int dbg = env_int("DRSA_AMD_CONV_DBG", 0);
+  a.dbg = dbg;
   return launch(e, a, Bq, (hipStream_t)stream);
 }
 

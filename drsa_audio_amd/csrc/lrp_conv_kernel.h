@@ -64,7 +64,11 @@ struct ConvCfg {
   static constexpr int KC = 9 * CIC;
   static constexpr int KCP = round_up<KC, 2>();
   static constexpr int NCHUNK = CIN / CIC;
-  static constexpr size_t lds_floats = (size_t)CIC * PLANE + (size_t)NG * KCP * COUT;
+  static constexpr int TWP = (TW == 32) ? 48 : TW;          // epilogue tile row stride (conflict-free writes)
+  static constexpr int TCH = WN * 32;                          // channels staged per epilogue pass
+  static constexpr size_t staging_floats = (size_t)CIC * PLANE + (size_t)NG * KCP * COUT;
+  static constexpr size_t epi_floats = (size_t)TCH * TH * TWP;
+  static constexpr size_t lds_floats = staging_floats > epi_floats ? staging_floats : epi_floats;
   static_assert(TH % MTH == 0 && TW % MTW == 0, "tile must be a multiple of the M-tile");
   static_assert(COUT % 32 == 0, "COUT must be padded to 32");
   static_assert(CIN % CIC == 0, "CIN must be a multiple of the chunk");
@@ -132,7 +136,7 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(ConvArgs a) {
         const int ci = idx / (HY * HX), rem = idx % (HY * HX);
         const int hy = rem / HX, hx = rem % HX;
         const int gy = ty0 - 1 + hy, gx = tx0 - 1 + hx, c = c0 + ci;
-        v[it] = (idx < NE && gy >= 0 && gy < H && gx >= 0 && gx < W && c < a.cin)
+        v[it] = (idx < NE && gy >= 0 && gy < H && gx >= 0 && gx < W && c < a.cin && !(a.dbg & 1))
                     ? a.in[(((size_t)bq * a.cin + c) * H + gy) * W + gx] : 0.f;
       }
 #pragma unroll
@@ -157,7 +161,7 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(ConvArgs a) {
         const int idx = tid + it * kThreads;
         const int ci = idx / (CY * CX), rem = idx % (CY * CX);
         const int cy = qy0 + rem / CX, cx = qx0 + rem % CX, c = c0 + ci;
-        const bool ok = idx < NE && cy >= 0 && cy < H2 && cx >= 0 && cx < W2 && c < a.cin;
+        const bool ok = idx < NE && cy >= 0 && cy < H2 && cx >= 0 && cx < W2 && c < a.cin && !(a.dbg & 1);
         v[it] = ok ? a.in[(((size_t)bq * a.cin + c) * H2 + cy) * W2 + cx] : 0.f;
         sb[it] = ok ? (int)a.in_amax[(((size_t)bs * a.cin + c) * H2 + cy) * W2 + cx] : 0;
       }
@@ -197,121 +201,275 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(ConvArgs a) {
       }
     }
     __syncthreads();
-    if (!active) continue;
-    // ---- MFMA over the chunk (unrolled by 9 k-steps = two channels: offsets repeat) ----
-#pragma unroll 9
+    if (!active || (a.dbg & 4)) continue;
+    // ---- MFMA over the chunk.  k = k0 + h (h = lane half) with k = ci*9 + tap: the halo
+    //      offset pattern repeats every 9 k-steps (two channels), so the 9 per-lane bases
+    //      (one per step of the period, per m-tile) are computed once and every LDS read in
+    //      the fully unrolled loop is base register + immediate. ----
+    constexpr int NSTEP = KCP / 2;
+    // operands of step k0 are read one step ahead (explicit software pipeline)
+    auto read_x = [&](int k0, float (&xv)[MPW]) {
+      const int jj = (k0 / 2) % 9, mm = (k0 / 2) / 9;
+      const int kk = 2 * jj + h;
+      const int off = (kk / 9) * PLANE + ((kk % 9) / 3) * RS + (kk % 3) + mm * 2 * PLANE;
+#pragma unroll
+      for (int u = 0; u < MPW; ++u) {
+        if constexpr (KC % 2 == 0) xv[u] = halo[off + pix_off[u]];
+        else xv[u] = (k0 + h < KC) ? halo[off + pix_off[u]] : 0.f;
+      }
+    };
+    auto read_w = [&](int k0, float (&wv)[NG][NPW]) {
+#pragma unroll
+      for (int v = 0; v < NPW; ++v)
+#pragma unroll
+        for (int g = 0; g < NG; ++g) wv[g][v] = wl[((size_t)g * KCP + k0 + h) * COUT + (wn * NPW + v) * 32 + (lane & 31)];
+    };
+    float xa[MPW], wa[NG][NPW];
+    read_x(0, xa);
+    read_w(0, wa);
+#pragma unroll
     for (int k0 = 0; k0 < KCP; k0 += 2) {
-      const int k = k0 + h;
-      const int ci = k / 9, tap = k - ci * 9;
-      const int off = (k < KC) ? ci * PLANE + (tap / 3) * RS + (tap % 3) : 0;
-      float xv[MPW];
+      float xb[MPW], wb[NG][NPW];
+      if (k0 + 2 < KCP) {
+        read_x(k0 + 2, xb);
+        read_w(k0 + 2, wb);
+      }
 #pragma unroll
-      for (int u = 0; u < MPW; ++u) xv[u] = (KC % 2 == 0 || k < KC) ? halo[off + pix_off[u]] : 0.f;
+      for (int v = 0; v < NPW; ++v)
 #pragma unroll
-      for (int v = 0; v < NPW; ++v) {
-        const int co = (wn * NPW + v) * 32 + (lane & 31);
-#pragma unroll
-        for (int g = 0; g < NG; ++g) {
-          const float wvv = wl[((size_t)g * KCP + k) * COUT + co];
+        for (int g = 0; g < NG; ++g)
 #pragma unroll
           for (int u = 0; u < MPW; ++u) {
-            float x = xv[u];
+            float x = xa[u];
             if constexpr (EPI != EPI_BWD && NG == 3) {
               x = (g == 0) ? x : (g == 1 ? fmaxf(x, 0.f) : fminf(x, 0.f));
             } else if constexpr (EPI != EPI_BWD && NG == 2) {
               x = (g == 0) ? x : fmaxf(x, 0.f);
             }
-            acc[g][u][v] = mfma32(wvv, x, acc[g][u][v]);
+            acc[g][u][v] = mfma32(wa[g][v], x, acc[g][u][v]);
           }
-        }
+      if (k0 + 2 < KCP) {
+#pragma unroll
+        for (int u = 0; u < MPW; ++u) xa[u] = xb[u];
+#pragma unroll
+        for (int v = 0; v < NPW; ++v)
+#pragma unroll
+          for (int g = 0; g < NG; ++g) wa[g][v] = wb[g][v];
       }
     }
+    (void)NSTEP;
   }
 
-  // ---- epilogue: lane = pixel, registers = channels ----
-  if (!active) return;
-  const int sub = lane & 3;
+  // ---- epilogue, staged through LDS so global I/O is coalesced float4 rows ----
+  // pass (v, kind): every active wave writes its 32-channel slice (n-tile wn*NPW + v) of its
+  // m-tiles into T[TCH][TH][TWP] (lane = pixel, register = channel: conflict-free rows),
+  // then all threads walk T in row order.
+  constexpr int TWP = Cfg::TWP, TCH = Cfg::TCH;
+  constexpr int NV4 = TCH * TH * TW / 4;                 // float4 groups per pass
+  constexpr int V4T = (NV4 + kThreads - 1) / kThreads;   // per thread
+  constexpr int NCELL = TCH * (TH / 2) * (TW / 2);
+  constexpr int CT = (NCELL + kThreads - 1) / kThreads;
+  float* T = smem;
+  auto stage = [&](int v, auto valfn) {
+    __syncthreads();
+    if (active) {
 #pragma unroll
-  for (int u = 0; u < MPW; ++u) {
-    const int py = ty0 + pix_y[u], px = tx0 + pix_x[u];
-    const bool inside = py < H && px < W;   // partial tiles of small maps (windows are whole)
+      for (int u = 0; u < MPW; ++u)
 #pragma unroll
-    for (int v = 0; v < NPW; ++v) {
-      const int n0 = (wn * NPW + v) * 32;
+        for (int r = 0; r < 16; ++r) {
+          const int cl = wn * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          T[(cl * TH + pix_y[u]) * TWP + pix_x[u]] = valfn(u, r);
+        }
+    }
+    __syncthreads();
+  };
+  auto gch = [&](int cl, int v) { return ((cl >> 5) * NPW + v) * 32 + (cl & 31); };   // global channel
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int co = n0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const bool live = inside && co < a.cout;
-        if constexpr (EPI == EPI_FWD_POOL || EPI == EPI_FWD_RELU) {
-          const float b0 = (a.bias && co < a.cout) ? a.bias[co] : 0.f;
-          const float z = acc[0][u][v][r] + b0;
-          float y = z > 0.f ? z : 0.f;
-          if (z != z) y = z;   // relu(NaN) = NaN (torch semantics)
-          float den = 0.f;
-          if (a.out_den) {
-            if (a.den_map) {
-              den = live ? a.den_map[((size_t)co * H + py) * W + px] : 0.f;
-            } else if constexpr (NG >= 2) {
-              const float bp = (a.bias && co < a.cout) ? a.bias[COUT + co] : 0.f;
-              const float bn = (a.bias && co < a.cout) ? a.bias[2 * COUT + co] : 0.f;
-              const float z0 = acc[1][u][v][r] + bp;
-              float z1 = bn;
-              if constexpr (NG == 3) z1 = acc[2][u][v][r] + bn;
-              den = z0 + z1;
-            } else {
-              // Epsilon: den = conv(x; W) + b_den (b_den = b, or 0 under zero_params=['bias'])
-              den = acc[0][u][v][r] + ((a.bias && co < a.cout) ? a.bias[COUT + co] : 0.f);
-            }
-          }
-          if constexpr (EPI == EPI_FWD_POOL) {
+  for (int v = 0; v < NPW; ++v) {
+    if constexpr (EPI == EPI_FWD_POOL || EPI == EPI_FWD_RELU) {
+      // pass 0: y = relu(z)
+      stage(v, [&](int u, int r) {
+        const int co = gch(wn * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, v);
+        const float z = acc[0][u][v][r] + ((a.bias && co < a.cout) ? a.bias[co] : 0.f);
+        float y = z > 0.f ? z : 0.f;
+        if (z != z) y = z;   // relu(NaN) = NaN (torch semantics)
+        return y;
+      });
+      int am_keep[CT];
+      if constexpr (EPI == EPI_FWD_POOL) {
+        const int H2 = H >> 1, W2 = W >> 1;
+#pragma unroll
+        for (int it = 0; it < CT; ++it) {
+          const int i = tid + it * kThreads;
+          am_keep[it] = 0;
+          if (i < NCELL) {
+            const int cl = i / ((TH / 2) * (TW / 2)), rem = i % ((TH / 2) * (TW / 2));
+            const int cy = rem / (TW / 2), cx = rem % (TW / 2);
+            const int co = gch(cl, v);
+            const int qy = (ty0 >> 1) + cy, qx = (tx0 >> 1) + cx;
+            const float* t = T + (cl * TH + 2 * cy) * TWP + 2 * cx;
+            const float yy[4] = {t[0], t[1], t[TWP], t[TWP + 1]};
             // torch max_pool2d: first maximum in row-major window order; NaN wins
-            const int base = lane & ~3;
-            float yy[4], dd[4];
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) {
-              yy[s4] = __shfl(y, base + s4, 64);
-              dd[s4] = __shfl(den, base + s4, 64);
-            }
             int am = 0;
             float m = yy[0];
 #pragma unroll
             for (int s4 = 1; s4 < 4; ++s4)
               if (yy[s4] > m || (yy[s4] != yy[s4] && m == m)) { m = yy[s4]; am = s4; }
-            if (sub == 0 && live) {
-              const int H2 = H >> 1, W2 = W >> 1;
-              const size_t o = (((size_t)bq * a.cout + co) * H2 + (py >> 1)) * W2 + (px >> 1);
+            am_keep[it] = am;
+            if (co < a.cout && qy < H2 && qx < W2) {
+              const size_t o = (((size_t)bq * a.cout + co) * H2 + qy) * W2 + qx;
               a.out[o] = m;
               a.out_amax[o] = (uint8_t)am;
-              if (a.out_den) a.out_den[o] = dd[am];
-            }
-          } else if (live) {
-            const size_t o = (((size_t)bq * a.cout + co) * H + py) * W + px;
-            a.out[o] = y;
-            if (a.out_den) a.out_den[o] = den;
-          }
-        } else {   // EPI_BWD
-          if (!live) continue;
-          const size_t os = (((size_t)bs * a.cout + co) * H + py) * W + px;
-          const size_t oq = (((size_t)bq * a.cout + co) * H + py) * W + px;
-          float R;
-          if (a.xmode == XM_NONE) {
-            R = acc[0][u][v][r];
-          } else {
-            const float x = a.x[os];
-            if (a.xmode == XM_MUL) {
-              R = x * acc[0][u][v][r];
-            } else {   // XM_SPLIT: x+ * acc0 + x- * acc1
-              R = fmaxf(x, 0.f) * acc[0][u][v][r];
-              if constexpr (NG >= 2) R += fminf(x, 0.f) * acc[1][u][v][r];
             }
           }
-          if (a.post == POST_DIV) {
-            const float x = a.x[os];
-            R = (x > 0.f) ? R / stab(a.den[os], a.eps) : 0.f;
-          } else if (a.post == POST_MASK) {
-            R = (a.x[os] > 0.f) ? R : 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int it = 0; it < V4T; ++it) {
+          const int i = tid + it * kThreads;
+          if (i < NV4) {
+            const int cl = i / (TH * TW / 4), rem = i % (TH * TW / 4);
+            const int py = rem / (TW / 4), px = (rem % (TW / 4)) * 4;
+            const int co = gch(cl, v);
+            if (co < a.cout && ty0 + py < H && tx0 + px < W) {
+              const float4 val = *reinterpret_cast<const float4*>(T + (cl * TH + py) * TWP + px);
+              *reinterpret_cast<float4*>(a.out + (((size_t)bq * a.cout + co) * H + ty0 + py) * W + tx0 + px) = val;
+            }
           }
-          a.out[oq] = R;
+        }
+      }
+      if (a.out_den) {
+        // pass 1: the rule's denominator
+        stage(v, [&](int u, int r) {
+          const int co = gch(wn * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, v);
+          const bool cok = co < a.cout;
+          if (a.den_map) {
+            const int py = ty0 + pix_y[u], px = tx0 + pix_x[u];
+            return (cok && py < H && px < W) ? a.den_map[((size_t)co * H + py) * W + px] : 0.f;
+          }
+          if constexpr (NG >= 2) {
+            const float bp = (a.bias && cok) ? a.bias[COUT + co] : 0.f;
+            const float bn = (a.bias && cok) ? a.bias[2 * COUT + co] : 0.f;
+            const float z0 = acc[1][u][v][r] + bp;
+            float z1 = bn;
+            if constexpr (NG == 3) z1 = acc[2][u][v][r] + bn;
+            return z0 + z1;
+          }
+          // Epsilon: den = conv(x; W) + b_den (b_den = b, or 0 under zero_params=['bias'])
+          return acc[0][u][v][r] + ((a.bias && cok) ? a.bias[COUT + co] : 0.f);
+        });
+        if constexpr (EPI == EPI_FWD_POOL) {
+          const int H2 = H >> 1, W2 = W >> 1;
+#pragma unroll
+          for (int it = 0; it < CT; ++it) {
+            const int i = tid + it * kThreads;
+            if (i < NCELL) {
+              const int cl = i / ((TH / 2) * (TW / 2)), rem = i % ((TH / 2) * (TW / 2));
+              const int cy = rem / (TW / 2), cx = rem % (TW / 2);
+              const int co = gch(cl, v);
+              const int qy = (ty0 >> 1) + cy, qx = (tx0 >> 1) + cx;
+              const int am = am_keep[it];
+              if (co < a.cout && qy < H2 && qx < W2)
+                a.out_den[(((size_t)bq * a.cout + co) * H2 + qy) * W2 + qx] =
+                    T[(cl * TH + 2 * cy + (am >> 1)) * TWP + 2 * cx + (am & 1)];
+            }
+          }
+        } else {
+#pragma unroll
+          for (int it = 0; it < V4T; ++it) {
+            const int i = tid + it * kThreads;
+            if (i < NV4) {
+              const int cl = i / (TH * TW / 4), rem = i % (TH * TW / 4);
+              const int py = rem / (TW / 4), px = (rem % (TW / 4)) * 4;
+              const int co = gch(cl, v);
+              if (co < a.cout && ty0 + py < H && tx0 + px < W) {
+                const float4 val = *reinterpret_cast<const float4*>(T + (cl * TH + py) * TWP + px);
+                *reinterpret_cast<float4*>(a.out_den + (((size_t)bq * a.cout + co) * H + ty0 + py) * W + tx0 + px) = val;
+              }
+            }
+          }
+        }
+      }
+    } else {   // EPI_BWD: R = xmode(acc, x) -> post -> out
+      float4 Rk[V4T];
+      stage(v, [&](int u, int r) { return acc[0][u][v][r]; });
+#pragma unroll
+      for (int it = 0; it < V4T; ++it) {
+        const int i = tid + it * kThreads;
+        Rk[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (i < NV4) {
+          const int cl = i / (TH * TW / 4), rem = i % (TH * TW / 4);
+          const int py = rem / (TW / 4), px = (rem % (TW / 4)) * 4;
+          const int co = gch(cl, v);
+          if (co < a.cout && ty0 + py < H && tx0 + px < W) {
+            const float4 t = *reinterpret_cast<const float4*>(T + (cl * TH + py) * TWP + px);
+            if (a.xmode == XM_NONE || (a.dbg & 2)) {
+              Rk[it] = t;
+            } else {
+              const float4 x = *reinterpret_cast<const float4*>(a.x + (((size_t)bs * a.cout + co) * H + ty0 + py) * W + tx0 + px);
+              if (a.xmode == XM_MUL) {
+                Rk[it] = make_float4(x.x * t.x, x.y * t.y, x.z * t.z, x.w * t.w);
+              } else {
+                Rk[it] = make_float4(fmaxf(x.x, 0.f) * t.x, fmaxf(x.y, 0.f) * t.y, fmaxf(x.z, 0.f) * t.z,
+                                     fmaxf(x.w, 0.f) * t.w);
+              }
+            }
+          }
+        }
+      }
+      if constexpr (NG >= 2) {
+        if (a.xmode == XM_SPLIT) {
+          stage(v, [&](int u, int r) { return acc[1][u][v][r]; });
+#pragma unroll
+          for (int it = 0; it < V4T; ++it) {
+            const int i = tid + it * kThreads;
+            if (i < NV4) {
+              const int cl = i / (TH * TW / 4), rem = i % (TH * TW / 4);
+              const int py = rem / (TW / 4), px = (rem % (TW / 4)) * 4;
+              const int co = gch(cl, v);
+              if (co < a.cout && ty0 + py < H && tx0 + px < W) {
+                const float4 t = *reinterpret_cast<const float4*>(T + (cl * TH + py) * TWP + px);
+                const float4 x = *reinterpret_cast<const float4*>(a.x + (((size_t)bs * a.cout + co) * H + ty0 + py) * W + tx0 + px);
+                Rk[it].x += fminf(x.x, 0.f) * t.x;
+                Rk[it].y += fminf(x.y, 0.f) * t.y;
+                Rk[it].z += fminf(x.z, 0.f) * t.z;
+                Rk[it].w += fminf(x.w, 0.f) * t.w;
+              }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < V4T; ++it) {
+        const int i = tid + it * kThreads;
+        if (i < NV4) {
+          const int cl = i / (TH * TW / 4), rem = i % (TH * TW / 4);
+          const int py = rem / (TW / 4), px = (rem % (TW / 4)) * 4;
+          const int co = gch(cl, v);
+          if (co < a.cout && ty0 + py < H && tx0 + px < W) {
+            const size_t os = (((size_t)bs * a.cout + co) * H + ty0 + py) * W + tx0 + px;
+            const size_t oq = (((size_t)bq * a.cout + co) * H + ty0 + py) * W + tx0 + px;
+            float4 R = Rk[it];
+            if (a.dbg & 2) {
+              if (R.x == 12345.f) a.out[oq] = 1.f;
+              continue;
+            }
+            if (a.post == POST_DIV) {
+              const float4 x = *reinterpret_cast<const float4*>(a.x + os);
+              const float4 d = *reinterpret_cast<const float4*>(a.den + os);
+              R.x = (x.x > 0.f) ? R.x / stab(d.x, a.eps) : 0.f;
+              R.y = (x.y > 0.f) ? R.y / stab(d.y, a.eps) : 0.f;
+              R.z = (x.z > 0.f) ? R.z / stab(d.z, a.eps) : 0.f;
+              R.w = (x.w > 0.f) ? R.w / stab(d.w, a.eps) : 0.f;
+            } else if (a.post == POST_MASK) {
+              const float4 x = *reinterpret_cast<const float4*>(a.x + os);
+              R.x = (x.x > 0.f) ? R.x : 0.f;
+              R.y = (x.y > 0.f) ? R.y : 0.f;
+              R.z = (x.z > 0.f) ? R.z : 0.f;
+              R.w = (x.w > 0.f) ? R.w : 0.f;
+            }
+            *reinterpret_cast<float4*>(a.out + oq) = R;
+          }
         }
       }
     }
@@ -331,8 +489,10 @@ struct Entry {
                    drsa_conv::conv3x3_kernel<CIN, COUT, TH, TW, MW, CIC, NG, AM, EP>,                      \
                    drsa_conv::ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AM, EP>::lds_floats * sizeof(float)}
 
-// tile by output width: W >= 32 -> 8x32 (MW 8); 8 < W < 32 -> 8x16 (MW 8); W <= 8 -> 8x8 (MW 4)
+// tile by output width: W >= 32 -> 16x32 (32 output channels) or 8x32 (MW 8); 8 < W < 32 -> 8x16
+// (MW 8); W <= 8 -> 8x8 (MW 4)
 #define CONV_FAMILY(CIN, COUT, CIC, NG, AM, EP)                      \
+  CONV_ENTRY(CIN, COUT, 16, 32, 8, CIC, NG, AM, EP),                 \
   CONV_ENTRY(CIN, COUT, 8, 32, 8, CIC, NG, AM, EP),                  \
   CONV_ENTRY(CIN, COUT, 8, 16, 8, CIC, NG, AM, EP),                  \
   CONV_ENTRY(CIN, COUT, 8, 8, 4, CIC, NG, AM, EP)

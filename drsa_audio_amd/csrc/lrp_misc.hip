@@ -107,82 +107,86 @@ __global__ __launch_bounds__(256) void linear_kernel(LinArgs a) {
 
 // ===========================================================================
 // projection forward: h = a_vec U, a' = h U^T, optional 2x2 max-pool of a'
-//   a [B][D][H][W] -> h [B][H*W][D], ap [B][D][H][W], pooled [B][D][H/2][W/2] + argmax
-//   workgroup = 8x8 pixel tile (64 pixels), 4 waves; D in {16,...,128} (multiple of 16)
+//   a [B][D][H][W] -> h [B][D][H*W] (channel-major), ap [B][D][H][W], pooled + argmax
+//   tile = 2 rows x 32 cols (64 pixels); a workgroup stages U once and walks PT tiles.
+//   MFMA orientation D[channel][pixel]: lanes = pixels (coalesced I/O).
 // ===========================================================================
+constexpr int PT = 4;   // row-pair tiles per workgroup
+
 template <int D>
 __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __restrict__ a, const float* __restrict__ U,
                                                             float* __restrict__ h, float* __restrict__ ap,
                                                             float* __restrict__ pooled, uint8_t* __restrict__ amax,
                                                             int H, int W, int pool) {
-  constexpr int P = 64, LD = D + 1;
+  constexpr int P = 64, LD = D + 1, PL = P + 4;
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* Us = sm;               // [D][LD]
-  float* as = Us + D * LD;      // [D][P]   (channel-major tile)
-  float* hs = as + D * P;       // [P][LD]
-  float* aps = as;              // [D][P]   (reuses the a tile after the first GEMM)
+  float* Us = sm;               // [D][LD]   U[c][j]
+  float* as = Us + D * LD;      // [D][PL]   a tile, then a' tile
+  float* hs = as + D * PL;      // [D][PL]   h tile
   const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
-  const int tiles_x = W / 8;
-  const int ty0 = (blockIdx.x / tiles_x) * 8, tx0 = (blockIdx.x % tiles_x) * 8;
   const int b = blockIdx.y;
-  const int HW = H * W;
+  const int TW = W < 32 ? W : 32, RPT = P / TW;      // tile = RPT rows x TW cols
+  const int HW = H * W, xt = W / TW;
   for (int i = tid; i < D * D; i += 256) Us[(i / D) * LD + i % D] = U[i];
-  for (int i = tid; i < D * P; i += 256) {
-    const int c = i / P, p = i % P;
-    const int y = ty0 + p / 8, x = tx0 + p % 8;
-    as[c * P + p] = a[((size_t)b * D + c) * HW + y * W + x];
-  }
-  __syncthreads();
-  constexpr int NB = D / 16, TILES = (P / 16) * NB;   // 16x16 output tiles of [P][D]
-  // h[p][j] = sum_c a[c][p] U[c][j]
-  for (int t = w; t < TILES; t += 4) {
-    const int pb = t / NB, jb = t % NB;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < D; k0 += 4) {
-      const int c = k0 + (lane >> 4);
-      acc = mfma16(as[c * P + pb * 16 + (lane & 15)], Us[c * LD + jb * 16 + (lane & 15)], acc);
+  constexpr int NB = D / 16, TILES = NB * (P / 16);
+  for (int t = 0; t < PT; ++t) {
+    const int tile = blockIdx.x * PT + t;
+    if (tile >= (H / RPT) * xt) break;
+    const int y0 = (tile / xt) * RPT, x0 = (tile % xt) * TW;
+    __syncthreads();
+    for (int i = tid; i < D * P; i += 256) {
+      const int c = i / P, p = i % P;
+      as[c * PL + p] = a[((size_t)b * D + c) * HW + (y0 + p / TW) * W + x0 + p % TW];
     }
-    for (int r = 0; r < 4; ++r) {
-      const int p = pb * 16 + (lane >> 4) * 4 + r, j = jb * 16 + (lane & 15);
-      hs[p * LD + j] = acc[r];
-      const int y = ty0 + p / 8, x = tx0 + p % 8;
-      h[((size_t)b * HW + y * W + x) * D + j] = acc[r];
+    __syncthreads();
+    // h[j][p] = sum_c U[c][j] a[c][p]
+    for (int q = w; q < TILES; q += 4) {
+      const int jb = q / (P / 16), pb = q % (P / 16);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int k0 = 0; k0 < D; k0 += 4) {
+        const int c = k0 + (lane >> 4);
+        acc = mfma16(Us[c * LD + jb * 16 + (lane & 15)], as[c * PL + pb * 16 + (lane & 15)], acc);
+      }
+      for (int r = 0; r < 4; ++r) {
+        const int j = jb * 16 + (lane >> 4) * 4 + r, p = pb * 16 + (lane & 15);
+        hs[j * PL + p] = acc[r];
+        h[((size_t)b * D + j) * HW + (y0 + p / TW) * W + x0 + p % TW] = acc[r];
+      }
     }
-  }
-  __syncthreads();
-  // a'[p][c] = sum_j h[p][j] U[c][j]
-  for (int t = w; t < TILES; t += 4) {
-    const int pb = t / NB, cb = t % NB;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < D; k0 += 4) {
-      const int j = k0 + (lane >> 4);
-      acc = mfma16(hs[(pb * 16 + (lane & 15)) * LD + j], Us[(cb * 16 + (lane & 15)) * LD + j], acc);
+    __syncthreads();
+    // a'[c][p] = sum_j U[c][j] h[j][p]
+    for (int q = w; q < TILES; q += 4) {
+      const int cb = q / (P / 16), pb = q % (P / 16);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int k0 = 0; k0 < D; k0 += 4) {
+        const int j = k0 + (lane >> 4);
+        acc = mfma16(Us[(cb * 16 + (lane & 15)) * LD + j], hs[j * PL + pb * 16 + (lane & 15)], acc);
+      }
+      for (int r = 0; r < 4; ++r) {
+        const int c = cb * 16 + (lane >> 4) * 4 + r, p = pb * 16 + (lane & 15);
+        as[c * PL + p] = acc[r];   // a tile no longer needed: holds a' now
+        ap[((size_t)b * D + c) * HW + (y0 + p / TW) * W + x0 + p % TW] = acc[r];
+      }
     }
-    for (int r = 0; r < 4; ++r) {
-      const int p = pb * 16 + (lane >> 4) * 4 + r, c = cb * 16 + (lane & 15);
-      aps[c * P + p] = acc[r];
-    }
-  }
-  __syncthreads();
-  for (int i = tid; i < D * P; i += 256) {
-    const int c = i / P, p = i % P;
-    const int y = ty0 + p / 8, x = tx0 + p % 8;
-    ap[((size_t)b * D + c) * HW + y * W + x] = aps[c * P + p];
-  }
-  if (pool) {
-    const int H2 = H / 2, W2 = W / 2;
-    for (int i = tid; i < D * 16; i += 256) {
-      const int c = i / 16, q = i % 16;
-      const int qy = q / 4, qx = q % 4;
-      const int p0 = (2 * qy) * 8 + 2 * qx;
-      float v[4] = {aps[c * P + p0], aps[c * P + p0 + 1], aps[c * P + p0 + 8], aps[c * P + p0 + 9]};
-      int am = 0;
-      float m = v[0];
-      for (int s = 1; s < 4; ++s)
-        if (v[s] > m || (v[s] != v[s] && m == m)) { m = v[s]; am = s; }
-      const size_t o = ((size_t)b * D + c) * H2 * W2 + (ty0 / 2 + qy) * W2 + tx0 / 2 + qx;
-      pooled[o] = m;
-      amax[o] = (uint8_t)am;
+    if (pool) {
+      __syncthreads();
+      const int H2 = H / 2, W2 = W / 2;
+      const int CXN = TW / 2;
+      for (int i = tid; i < D * 16; i += 256) {
+        const int c = i / 16, cell = i % 16, cy = cell / CXN, cx = cell % CXN;
+        const int p00 = (2 * cy) * TW + 2 * cx;
+        const float v[4] = {as[c * PL + p00], as[c * PL + p00 + 1], as[c * PL + p00 + TW],
+                            as[c * PL + p00 + TW + 1]};
+        int am = 0;
+        float m = v[0];
+        for (int s4 = 1; s4 < 4; ++s4)
+          if (v[s4] > m || (v[s4] != v[s4] && m == m)) { m = v[s4]; am = s4; }
+        const size_t o = ((size_t)b * D + c) * H2 * W2 + (y0 / 2 + cy) * W2 + x0 / 2 + cx;
+        pooled[o] = m;
+        amax[o] = (uint8_t)am;
+      }
     }
   }
 }
@@ -195,6 +199,7 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
 //   g2    = R_h / stab(h, eps_proj)                  Epsilon on projection (after the mask)
 //   clone 0: v = g2 U^T ; clone k: v = g2[block k-1] U[:, block k-1]^T   (SubspaceHook mask)
 //   G_q   = [a > 0] (a (.) v) / stab(den, eps_den)   ReLU-backward + the conv rule's division below
+// Tiles of 2 x 32 pixels, lanes = pixels; U staged once per workgroup (PT tiles).
 // ===========================================================================
 template <int D>
 __global__ __launch_bounds__(256) void projection_bwd_kernel(
@@ -202,76 +207,80 @@ __global__ __launch_bounds__(256) void projection_bwd_kernel(
     const float* __restrict__ h, const float* __restrict__ a, const float* __restrict__ den,
     const float* __restrict__ U, float* __restrict__ G, int H, int W, int K, float eps_proj, float eps_den,
     int sparse, int has_den, int fanout) {
-  constexpr int P = 64, LD = D + 1;
+  constexpr int P = 64, LD = D + 1, PL = P + 4;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* Us = sm;               // [D][LD]
-  float* g1 = Us + D * LD;      // [D][P]
-  float* g2 = g1 + D * P;       // [P][LD]
+  float* g1 = Us + D * LD;      // [D][PL]
+  float* g2 = g1 + D * PL;      // [D][PL]
   const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
-  const int tiles_x = W / 8;
-  const int ty0 = (blockIdx.x / tiles_x) * 8, tx0 = (blockIdx.x % tiles_x) * 8;
   const int b = blockIdx.y;
-  const int HW = H * W;
+  const int TW = W < 32 ? W : 32, RPT = P / TW;
+  const int HW = H * W, xt = W / TW;
   const int dk = D / K;
   for (int i = tid; i < D * D; i += 256) Us[(i / D) * LD + i % D] = U[i];
-  for (int i = tid; i < D * P; i += 256) {
-    const int c = i / P, p = i % P;
-    const int y = ty0 + p / 8, x = tx0 + p % 8;
-    float R;
-    if (sparse) {
-      const int H2 = H / 2, W2 = W / 2;
-      const size_t q = ((size_t)b * D + c) * H2 * W2 + (y >> 1) * W2 + (x >> 1);
-      R = (amax[q] == (((y & 1) << 1) | (x & 1))) ? gp[q] : 0.f;
-    } else {
-      R = gp[((size_t)b * D + c) * HW + y * W + x];
-    }
-    g1[c * P + p] = R / stab(ap[((size_t)b * D + c) * HW + y * W + x], eps_proj);
-  }
-  __syncthreads();
-  constexpr int NB = D / 16, TILES = (P / 16) * NB;
-  // t[p][j] = sum_c g1[c][p] U[c][j];  R_h = h (.) t;  g2 = R_h / stab(h)
-  for (int t = w; t < TILES; t += 4) {
-    const int pb = t / NB, jb = t % NB;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < D; k0 += 4) {
-      const int c = k0 + (lane >> 4);
-      acc = mfma16(g1[c * P + pb * 16 + (lane & 15)], Us[c * LD + jb * 16 + (lane & 15)], acc);
-    }
-    for (int r = 0; r < 4; ++r) {
-      const int p = pb * 16 + (lane >> 4) * 4 + r, j = jb * 16 + (lane & 15);
-      const int y = ty0 + p / 8, x = tx0 + p % 8;
-      const float hv = h[((size_t)b * HW + y * W + x) * D + j];
-      const float Rh = hv * acc[r];
-      g2[p * LD + j] = Rh / stab(hv, eps_proj);
-    }
-  }
-  __syncthreads();
-  // clones: q = 0 (all blocks), q = 1..K (block q-1).  fanout: write all K+1 clones of this
-  // sample; otherwise the row IS clone (b mod (K+1)) of a user-replicated batch (explainer.py:92).
+  constexpr int NB = D / 16, TILES = NB * (P / 16);
   const int nq = fanout ? (K + 1) : 1;
-  for (int t = w; t < nq * TILES; t += 4) {
-    const int q = fanout ? t / TILES : b % (K + 1), tt = t % TILES;
-    const int pb = tt / NB, cb = tt % NB;
-    const int j0 = q == 0 ? 0 : (q - 1) * dk, j1 = q == 0 ? D : q * dk;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int k0 = j0; k0 < j1; k0 += 4) {
-      const int j = k0 + (lane >> 4);
-      const bool ok = j < j1;
-      const float av = ok ? g2[(pb * 16 + (lane & 15)) * LD + j] : 0.f;
-      const float bv = ok ? Us[(cb * 16 + (lane & 15)) * LD + j] : 0.f;
-      acc = mfma16(av, bv, acc);
+  for (int t = 0; t < PT; ++t) {
+    const int tile = blockIdx.x * PT + t;
+    if (tile >= (H / RPT) * xt) break;
+    const int y0 = (tile / xt) * RPT, x0 = (tile % xt) * TW;
+    __syncthreads();
+    for (int i = tid; i < D * P; i += 256) {
+      const int c = i / P, p = i % P;
+      const int y = y0 + p / TW, x = x0 + p % TW;
+      float R;
+      if (sparse) {
+        const int H2 = H / 2, W2 = W / 2;
+        const size_t q = ((size_t)b * D + c) * H2 * W2 + (y >> 1) * W2 + (x >> 1);
+        R = (amax[q] == (((y & 1) << 1) | (x & 1))) ? gp[q] : 0.f;
+      } else {
+        R = gp[((size_t)b * D + c) * HW + y * W + x];
+      }
+      g1[c * PL + p] = R / stab(ap[((size_t)b * D + c) * HW + y * W + x], eps_proj);
     }
-    for (int r = 0; r < 4; ++r) {
-      const int p = pb * 16 + (lane >> 4) * 4 + r, c = cb * 16 + (lane & 15);
-      const int y = ty0 + p / 8, x = tx0 + p % 8;
-      const size_t os = ((size_t)b * D + c) * HW + y * W + x;
-      const float av = a[os];
-      float Rv = av * acc[r];
-      float g;
-      if (has_den) g = (av > 0.f) ? Rv / stab(den[os], eps_den) : 0.f;
-      else g = (av > 0.f) ? Rv : 0.f;
+    __syncthreads();
+    // t[j][p] = sum_c U[c][j] g1[c][p];  R_h = h (.) t;  g2 = R_h / stab(h)
+    for (int q = w; q < TILES; q += 4) {
+      const int jb = q / (P / 16), pb = q % (P / 16);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int k0 = 0; k0 < D; k0 += 4) {
+        const int c = k0 + (lane >> 4);
+        acc = mfma16(Us[c * LD + jb * 16 + (lane & 15)], g1[c * PL + pb * 16 + (lane & 15)], acc);
+      }
+      for (int r = 0; r < 4; ++r) {
+        const int j = jb * 16 + (lane >> 4) * 4 + r, p = pb * 16 + (lane & 15);
+        const float hv = h[((size_t)b * D + j) * HW + (y0 + p / TW) * W + x0 + p % TW];
+        const float Rh = hv * acc[r];
+        g2[j * PL + p] = Rh / stab(hv, eps_proj);
+      }
+    }
+    __syncthreads();
+    for (int q2 = w; q2 < nq * TILES; q2 += 4) {
+      const int qi = q2 / TILES, tt = q2 % TILES;
+      const int q = fanout ? qi : b % (K + 1);
+      const int cb = tt / (P / 16), pb = tt % (P / 16);
+      const int j0 = q == 0 ? 0 : (q - 1) * dk, j1 = q == 0 ? D : q * dk;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int k0 = j0; k0 < j1; k0 += 4) {
+        const int j = k0 + (lane >> 4);
+        const bool ok = j < j1;
+        const float av = ok ? Us[(cb * 16 + (lane & 15)) * LD + j] : 0.f;
+        const float bv = ok ? g2[j * PL + pb * 16 + (lane & 15)] : 0.f;
+        acc = mfma16(av, bv, acc);
+      }
       const size_t orow = fanout ? (size_t)b * (K + 1) + q : (size_t)b;
-      G[(orow * D + c) * HW + y * W + x] = g;
+      for (int r = 0; r < 4; ++r) {
+        const int c = cb * 16 + (lane >> 4) * 4 + r, p = pb * 16 + (lane & 15);
+        const size_t pix = (size_t)(y0 + p / TW) * W + x0 + p % TW;
+        const size_t os = ((size_t)b * D + c) * HW + pix;
+        const float av = a[os];
+        const float Rv = av * acc[r];
+        float g;
+        if (has_den) g = (av > 0.f) ? Rv / stab(den[os], eps_den) : 0.f;
+        else g = (av > 0.f) ? Rv : 0.f;
+        G[(orow * D + c) * HW + pix] = g;
+      }
     }
   }
 }
@@ -513,9 +522,9 @@ int with_lds(F* fn, size_t lds) {
 }
 
 template <int D>
-size_t proj_fwd_lds() { return ((size_t)D * (D + 1) + D * 64 + 64 * (D + 1)) * sizeof(float); }
+size_t proj_fwd_lds() { return ((size_t)D * (D + 1) + 2 * (size_t)D * 68) * sizeof(float); }
 template <int D>
-size_t proj_bwd_lds() { return ((size_t)D * (D + 1) + D * 64 + 64 * (D + 1)) * sizeof(float); }
+size_t proj_bwd_lds() { return ((size_t)D * (D + 1) + 2 * (size_t)D * 68) * sizeof(float); }
 
 }  // namespace
 
@@ -550,10 +559,13 @@ int drsa_amd_linear_bwd(const float* R, const int* seed_cls, int one_hot, const 
 
 int drsa_amd_projection_fwd(const float* a, const float* U, float* h, float* ap, float* pooled, uint8_t* amax, int B,
                             int D, int H, int W, int pool, void* stream) {
-  DRSA_REQUIRE(H % 8 == 0 && W % 8 == 0, "projection_fwd: H, W must be multiples of 8");
+  const int TW = W < 32 ? W : 32;
+  DRSA_REQUIRE((W == 8 || W == 16 || W % 32 == 0) && H % (64 / TW) == 0,
+               "projection_fwd: W must be 8, 16 or a multiple of 32 and H a multiple of 64/min(W,32) (got %dx%d)", H, W);
   DRSA_REQUIRE(!pool || (pooled && amax), "projection_fwd: pool needs outputs");
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((H / 8) * (W / 8), B);
+  const int tiles = (H / (64 / TW)) * (W / TW);
+  const dim3 grid((tiles + PT - 1) / PT, B);
   switch (D) {
 #define PF(DD)                                                                                        \
   case DD: {                                                                                          \
@@ -576,10 +588,13 @@ int drsa_amd_projection_fwd(const float* a, const float* U, float* h, float* ap,
 int drsa_amd_projection_bwd(const float* gp, const uint8_t* amax, const float* ap, const float* h, const float* a,
                             const float* den, const float* U, float* G, int B, int D, int H, int W, int K,
                             float eps_proj, float eps_den, int fanout, void* stream) {
-  DRSA_REQUIRE(H % 8 == 0 && W % 8 == 0, "projection_bwd: H, W must be multiples of 8");
+  const int TW = W < 32 ? W : 32;
+  DRSA_REQUIRE((W == 8 || W == 16 || W % 32 == 0) && H % (64 / TW) == 0,
+               "projection_bwd: W must be 8, 16 or a multiple of 32 and H a multiple of 64/min(W,32) (got %dx%d)", H, W);
   DRSA_REQUIRE(K > 0 && D % K == 0, "projection_bwd: K must divide d");
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((H / 8) * (W / 8), B);
+  const int tiles = (H / (64 / TW)) * (W / TW);
+  const dim3 grid((tiles + PT - 1) / PT, B);
   const int sparse = amax != nullptr, has_den = den != nullptr;
   switch (D) {
 #define PB(DD)                                                                                        \

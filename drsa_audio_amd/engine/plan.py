@@ -362,7 +362,7 @@ class LRPEngine:
                 rec.update(a=a, den=den)
                 if st.proj is not None:
                     P = st.proj
-                    hb = self._buf((li, "h"), (B, h * w, st.cout))
+                    hb = self._buf((li, "h"), (B, st.cout, h * w))        # channel-major
                     ap = self._buf((li, "ap"), (B, st.cout, h, w))
                     if P.pool_after:
                         pooled = self._buf((li, "y"), (B, st.cout, h // 2, w // 2))
