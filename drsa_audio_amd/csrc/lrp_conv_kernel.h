@@ -338,15 +338,43 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(ConvArgs a) {
           }
         }
       }
-      if (a.out_den) {
+      if (a.out_den && a.den_map) {
+        // WSquare / Flat: input-independent map, read directly (coalesced) where it is stored
+        if constexpr (EPI == EPI_FWD_POOL) {
+          const int H2 = H >> 1, W2 = W >> 1;
+#pragma unroll
+          for (int it = 0; it < CT; ++it) {
+            const int i = tid + it * kThreads;
+            if (i < NCELL) {
+              const int cl = i / ((TH / 2) * (TW / 2)), rem = i % ((TH / 2) * (TW / 2));
+              const int cy = rem / (TW / 2), cx = rem % (TW / 2);
+              const int co = gch(cl, v);
+              const int qy = (ty0 >> 1) + cy, qx = (tx0 >> 1) + cx;
+              const int am = am_keep[it];
+              if (co < a.cout && qy < H2 && qx < W2)
+                a.out_den[(((size_t)bq * a.cout + co) * H2 + qy) * W2 + qx] =
+                    a.den_map[((size_t)co * H + 2 * qy + (am >> 1)) * W + 2 * qx + (am & 1)];
+            }
+          }
+        } else {
+#pragma unroll
+          for (int it = 0; it < V4T; ++it) {
+            const int i = tid + it * kThreads;
+            if (i < NV4) {
+              const int cl = i / (TH * TW / 4), rem = i % (TH * TW / 4);
+              const int py = rem / (TW / 4), px = (rem % (TW / 4)) * 4;
+              const int co = gch(cl, v);
+              if (co < a.cout && ty0 + py < H && tx0 + px < W)
+                *reinterpret_cast<float4*>(a.out_den + (((size_t)bq * a.cout + co) * H + ty0 + py) * W + tx0 + px) =
+                    *reinterpret_cast<const float4*>(a.den_map + ((size_t)co * H + ty0 + py) * W + tx0 + px);
+            }
+          }
+        }
+      } else if (a.out_den) {
         // pass 1: the rule's denominator
         stage(v, [&](int u, int r) {
           const int co = gch(wn * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, v);
           const bool cok = co < a.cout;
-          if (a.den_map) {
-            const int py = ty0 + pix_y[u], px = tx0 + pix_x[u];
-            return (cok && py < H && px < W) ? a.den_map[((size_t)co * H + py) * W + px] : 0.f;
-          }
           if constexpr (NG >= 2) {
             const float bp = (a.bias && cok) ? a.bias[COUT + co] : 0.f;
             const float bn = (a.bias && cok) ? a.bias[2 * COUT + co] : 0.f;

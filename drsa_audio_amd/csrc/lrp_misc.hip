@@ -355,11 +355,12 @@ __global__ __launch_bounds__(256) void first_layer_bwd_kernel(const float* __res
 }
 
 // Pool-sparse variant (the VGG case: conv0 -> ReLU -> MaxPool2d(2)).  One thread per pool
-// cell = 2x2 output pixels; the 3x3 cell neighbourhood (gp + argmax) is staged in LDS per
-// channel chunk; the 4x4 pixel patch those pixels read is rebuilt in registers (each patch
-// slot maps to exactly one cell and one sub-position, so it is a compile-time select), then
-// 9 fmas per pixel and channel in the dense chain order (channel, dy, dx) — the same chain
-// as the dense kernel above and oracle/lrp_exact.c, zeros included.
+// cell = 2x2 output pixels.  The cells of the tile (+1 halo) are expanded to pixels while
+// staging (value at the argmax position, zeros elsewhere) into an LDS image whose origin is
+// pixel (2qy0-1, 2qx0-1), so every row of a thread's 4x4 input patch starts at an even column
+// and is two aligned 8-byte reads.  Then 9
+// fmas per pixel and channel in the dense chain order (channel, dy, dx) — the chain of the
+// dense kernel above and of oracle/lrp_exact.c, zeros included.
 constexpr int FQ_Y = 8, FQ_X = 32, FQ_C = 8;
 
 __global__ __launch_bounds__(256) void first_layer_bwd_pooled_kernel(const float* __restrict__ g,
@@ -367,9 +368,9 @@ __global__ __launch_bounds__(256) void first_layer_bwd_pooled_kernel(const float
                                                                      const float* __restrict__ w2,
                                                                      float* __restrict__ out, int C, int H, int W,
                                                                      int clones) {
-  constexpr int RY = FQ_Y + 2, RX = FQ_X + 2;
-  __shared__ float sg[FQ_C][RY][RX + 1];
-  __shared__ uint8_t sa[FQ_C][RY][RX + 4];
+  constexpr int RY = FQ_Y + 2, RX = FQ_X + 2;      // cells incl. halo
+  constexpr int PY = 2 * FQ_Y + 2, PX = 2 * FQ_X + 4;   // pixel image, origin (2qy0-1, 2qx0-1)
+  __shared__ __attribute__((aligned(16))) float img[FQ_C][PY][PX];
   const int tid = threadIdx.x;
   const int H2 = H / 2, W2 = W / 2;
   const int tiles_x = (W2 + FQ_X - 1) / FQ_X;
@@ -381,42 +382,47 @@ __global__ __launch_bounds__(256) void first_layer_bwd_pooled_kernel(const float
   for (int c0 = 0; c0 < C; c0 += FQ_C) {
     __syncthreads();
     constexpr int NE = FQ_C * RY * RX;
+    constexpr int IT = (NE + 255) / 256;
+    float v[IT];
+    int sb[IT];
 #pragma unroll
-    for (int it = 0; it < (NE + 255) / 256; ++it) {
+    for (int it = 0; it < IT; ++it) {
+      const int idx = tid + it * 256;
+      const int ci = idx / (RY * RX), rem = idx % (RY * RX);
+      const int cy = qy0 - 1 + rem / RX, cx = qx0 - 1 + rem % RX, c = c0 + ci;
+      const bool ok = idx < NE && c < C && cy >= 0 && cy < H2 && cx >= 0 && cx < W2;
+      v[it] = ok ? g[(((size_t)bq * C + c) * H2 + cy) * W2 + cx] : 0.f;
+      sb[it] = ok ? (int)amax[(((size_t)bs * C + c) * H2 + cy) * W2 + cx] : 4;
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
       const int idx = tid + it * 256;
       if (idx < NE) {
         const int ci = idx / (RY * RX), rem = idx % (RY * RX);
         const int ry = rem / RX, rx = rem % RX;
-        const int cy = qy0 - 1 + ry, cx = qx0 - 1 + rx, c = c0 + ci;
-        float v = 0.f;
-        uint8_t s = 255;
-        if (c < C && cy >= 0 && cy < H2 && cx >= 0 && cx < W2) {
-          v = g[(((size_t)bq * C + c) * H2 + cy) * W2 + cx];
-          s = amax[(((size_t)bs * C + c) * H2 + cy) * W2 + cx];
+        // cell (ry, rx) = cell (qy0-1+ry, qx0-1+rx) -> pixel (2cy+sr, 2cx+sc) -> image (2ry-1+sr, 2rx-1+sc)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const int iy = 2 * ry - 1 + (s4 >> 1), ix = 2 * rx - 1 + (s4 & 1);
+          if (iy >= 0 && iy < PY && ix >= 0 && ix < PX) img[ci][iy][ix] = (sb[it] == s4) ? v[it] : 0.f;
         }
-        sg[ci][ry][rx] = v;
-        sa[ci][ry][rx] = s;
       }
     }
     __syncthreads();
-#pragma unroll 1
+#pragma unroll 2
     for (int ci = 0; ci < FQ_C; ++ci) {
       const int c = c0 + ci;
       float wv[9];
 #pragma unroll
       for (int t = 0; t < 9; ++t) wv[t] = (c < C) ? w2[c * 9 + t] : 0.f;
-      // patch P[i][j]: pixel (2qy - 1 + i, 2qx - 1 + j); its cell row offset and sub-row:
-      //   i = 0 -> cell qy-1, sub-row 1;  i = 1 -> qy, 0;  i = 2 -> qy, 1;  i = 3 -> qy+1, 0
+      // patch P[i][j] = pixel (2qy - 1 + i, 2qx - 1 + j) = img[2ty + i][2tx + j]  (8-byte aligned pairs)
       float P[4][4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int dcy = (i == 0) ? -1 : ((i == 3) ? 1 : 0), sr = (i == 1 || i == 3) ? 0 : 1;
-          const int dcx = (j == 0) ? -1 : ((j == 3) ? 1 : 0), sc = (j == 1 || j == 3) ? 0 : 1;
-          const uint8_t s = sa[ci][ty + 1 + dcy][tx + 1 + dcx];
-          P[i][j] = (s == (uint8_t)(sr * 2 + sc)) ? sg[ci][ty + 1 + dcy][tx + 1 + dcx] : 0.f;
-        }
+      for (int i = 0; i < 4; ++i) {
+        const float2 p0 = *reinterpret_cast<const float2*>(&img[ci][2 * ty + i][2 * tx]);
+        const float2 p1 = *reinterpret_cast<const float2*>(&img[ci][2 * ty + i][2 * tx + 2]);
+        P[i][0] = p0.x; P[i][1] = p0.y; P[i][2] = p1.x; P[i][3] = p1.y;
+      }
 #pragma unroll
       for (int py = 0; py < 2; ++py)
 #pragma unroll
@@ -431,8 +437,8 @@ __global__ __launch_bounds__(256) void first_layer_bwd_pooled_kernel(const float
   if (qy < H2 && qx < W2) {
 #pragma unroll
     for (int py = 0; py < 2; ++py) {
-      float2 v = make_float2(acc[py * 2], acc[py * 2 + 1]);
-      *reinterpret_cast<float2*>(out + ((size_t)bq * H + 2 * qy + py) * W + 2 * qx) = v;
+      float2 v2 = make_float2(acc[py * 2], acc[py * 2 + 1]);
+      *reinterpret_cast<float2*>(out + ((size_t)bq * H + 2 * qy + py) * W + 2 * qx) = v2;
     }
   }
 }
