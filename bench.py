@@ -152,6 +152,32 @@ def drsa_bench(device, steps=200):
             "objective_max_rel_err_vs_oracle_10_steps": rel, "objective_final": float(traj[-1])}
 
 
+def drsa_sharded_bench(device, world, rank, steps=100):
+    """C4-style row-sharded DRSA: 20000 rows per rank (weak), d=64, K=4; one RCCL all-reduce of the
+    [d*d+K] partial per step (drsa_audio_amd/xai/drsa/distributed.py)."""
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from gen_fixtures import drsa_inputs
+    from drsa_audio_amd.xai.drsa.distributed import sharded_run
+    n, d, K = 20000, 64, 4
+    A, C = drsa_inputs(n, d, 100 + rank)
+    U0 = np.load(os.path.join(ROOT, "tests", "golden", "u64_seed42.npy"))
+    Ag, Cg, Ug = (torch.from_numpy(v).to(device) for v in (A, C, U0))
+    sharded_run(Ag, Cg, Ug, K, 3)
+    torch.cuda.synchronize(device)
+    dist.barrier()
+    t0 = time.perf_counter()
+    U, traj = sharded_run(Ag, Cg, Ug, K, steps)
+    torch.cuda.synchronize(device)
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t)
+    return {"config": f"row-sharded DRSA: {n} rows/rank x {world} ranks, d={d}, K={K}, all-reduce {d*d+K} fp32/step",
+            "ms_per_step": dt / steps * 1e3, "vector_steps_per_s": n * world * steps / dt, "steps": steps,
+            "objective_final": float(traj[-1])}
+
+
 # --------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
@@ -161,6 +187,8 @@ def main():
     ap.add_argument("--batch", type=int, default=512, help="explained samples per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-drsa", action="store_true")
+    ap.add_argument("--tag-order", default=None,
+                    help="write the per-step kernel tag order (JSON) for scripts/tag_profile.py")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -212,7 +240,12 @@ def main():
     per = {}
     for tag, e0, e1 in eng.trace:
         per.setdefault(tag, []).append(e0.elapsed_time(e1))
+    tags = [t for t, _, _ in eng.trace]
     eng.trace = None
+    if args.tag_order and rank == 0:
+        L = len(tags) // 3
+        with open(args.tag_order, "w") as fh:
+            json.dump({"tags": tags[:L], "main_steps": args.warmup + args.steps + 3, "batch": B}, fh)
     macs = kernel_macs(eng, B, K)
     kernels = {}
     for tag, ts in per.items():
@@ -261,6 +294,9 @@ def main():
     drsa = None
     if not args.no_drsa and rank == 0:
         drsa = drsa_bench(device)
+    drsa_sharded = None
+    if not args.no_drsa and world > 1:
+        drsa_sharded = drsa_sharded_bench(device, world, rank)
     cpu = None
     if not args.no_cpu_baseline and rank == 0 and world == 1:
         cpu = cpu_baseline()
@@ -290,7 +326,8 @@ def main():
                            "achieved_tflops": 2.0 * total_macs * value / B / world / 1e12},
             "kernels": kernels,
             "secondary": {"standard_lrp_c2_bs64_samples_per_s": c2 * world,
-                          "explained_samples_per_s_bs64": bs64 * world, "drsa": drsa},
+                          "explained_samples_per_s_bs64": bs64 * world, "drsa": drsa,
+                          "drsa_sharded": drsa_sharded},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -1,0 +1,112 @@
+"""Row-sharded DRSA optimisation across ranks (one process per GPU).
+
+Each rank holds a shard of the activation/context rows.  One step:
+
+    gs_local = [A_r^T (R (.) C_r U) + C_r^T (R (.) A_r U)  |  S_k,r]     (drsa_amd_drsa_partial)
+    gs       = all_reduce(gs_local, SUM)                                  (RCCL over xGMI: d*d+K fp32)
+    f, U'    = finish(gs, N_total)                                         (drsa_amd_drsa_finish)
+
+The all-reduce payload is 16.4 KB at d=64 (64.1 KB at d=128): latency-bound, one collective
+per step.  Every rank receives identical reduced bytes and runs the identical deterministic
+polar step, so U stays replicated without a broadcast.  The step math is the reference's
+(``drsa.py:84-106``); sharding is exact up to the fp32 summation order of the partials.
+
+The per-step kernels are pluggable (``backend``) so the orchestration is tested on CPU with
+gloo (tests/test_dist_cpu.py) using the oracle's closed form; the product backend is HIP.
+"""
+from __future__ import annotations
+
+import os
+from typing import Callable, List, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ... import _capi
+
+
+class HipBackend:
+    """libdrsa_amd kernels on the rank's GPU."""
+
+    def __init__(self, A: torch.Tensor, C: torch.Tensor, d: int, K: int):
+        from .drsa import DrsaWorkspace
+        self.A, self.C, self.d, self.K = A, C, d, K
+        self.ws = DrsaWorkspace(max(A.size(0), 1), d, K, A.device)
+        self.gs = torch.empty(d * d + K, device=A.device, dtype=torch.float32)
+        self.f = torch.empty(1, device=A.device, dtype=torch.float32)
+
+    def partial(self, U: torch.Tensor) -> torch.Tensor:
+        _capi.call("drsa_amd_drsa_partial", self.A.data_ptr(), self.C.data_ptr(), self.A.size(0), self.d, self.K,
+                   U.data_ptr(), self.gs.data_ptr(), self.ws.ptr, self.ws.nbytes, _capi.stream_ptr(U.device))
+        return self.gs
+
+    def finish(self, gs: torch.Tensor, N_total: int, U: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        U_new = torch.empty_like(U)
+        _capi.call("drsa_amd_drsa_finish", gs.data_ptr(), int(N_total), self.d, self.K, U.data_ptr(),
+                   U_new.data_ptr(), self.f.data_ptr(), 0, None, _capi.stream_ptr(U.device))
+        return U_new, self.f.clone()
+
+    def objective(self, gs: torch.Tensor, N_total: int, U: torch.Tensor) -> torch.Tensor:
+        _capi.call("drsa_amd_drsa_finish", gs.data_ptr(), int(N_total), self.d, self.K, U.data_ptr(), None,
+                   self.f.data_ptr(), 1, None, _capi.stream_ptr(U.device))
+        return self.f.clone()
+
+
+def sharded_run(A_local: torch.Tensor, C_local: torch.Tensor, U0: torch.Tensor, K: int, steps: int,
+                group=None, backend=None) -> Tuple[torch.Tensor, np.ndarray]:
+    """SubspaceOptimizer.run over row shards.  Returns (U_steps, trajectory [steps+1]) on every rank."""
+    d = U0.size(0)
+    backend = backend or HipBackend(A_local.contiguous(), C_local.contiguous(), d, K)
+    n = torch.tensor([A_local.size(0)], dtype=torch.int64, device=U0.device)
+    if dist.is_initialized():
+        dist.all_reduce(n, op=dist.ReduceOp.SUM, group=group)
+    N_total = int(n.item())
+    U = U0.detach().clone().contiguous()
+    traj: List[torch.Tensor] = []
+    for _ in range(steps):
+        gs = backend.partial(U)
+        if dist.is_initialized():
+            dist.all_reduce(gs, op=dist.ReduceOp.SUM, group=group)
+        U, f = backend.finish(gs, N_total, U)
+        traj.append(f)
+    gs = backend.partial(U)
+    if dist.is_initialized():
+        dist.all_reduce(gs, op=dist.ReduceOp.SUM, group=group)
+    traj.append(backend.objective(gs, N_total, U))
+    return U, torch.cat([t.reshape(1) for t in traj]).cpu().numpy()
+
+
+def shard_rows(N: int, world: int, rank: int) -> slice:
+    """Contiguous, balanced row range of ``rank``."""
+    base, rem = divmod(N, world)
+    start = rank * base + min(rank, rem)
+    return slice(start, start + base + (1 if rank < rem else 0))
+
+
+def main_sharded(activation_vecs: torch.Tensor, context_vecs: torch.Tensor, model_root: str,
+                 num_concepts: int = 4, steps: int = 2000, runs: int = 3, seed: int = 42) -> Optional[List[str]]:
+    """drsa.main semantics (drsa.py:241-301) with the rows split over the process group; rank 0
+    writes ``run{r}/projection_matrix.pkl`` and ``run{r}/train_stats.csv``."""
+    import pickle
+    from .drsa import initial_projections
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    dev = torch.device("cuda", torch.cuda.current_device())
+    sl = shard_rows(activation_vecs.size(0), world, rank)
+    A = activation_vecs[sl].to(dev, torch.float32).contiguous()
+    C = context_vecs[sl].to(dev, torch.float32).contiguous()
+    d = A.size(1)
+    paths = []
+    for r, U in enumerate(initial_projections(d, runs, seed), start=1):
+        Uf, traj = sharded_run(A, C, torch.tensor(U, dtype=torch.float32, device=dev), num_concepts, steps)
+        if rank == 0:
+            path = os.path.join(model_root, f"run{r}")
+            os.makedirs(path, exist_ok=True)
+            with open(os.path.join(path, "projection_matrix.pkl"), "wb") as fh:
+                pickle.dump(Uf.cpu().numpy(), fh)
+            import pandas as pd
+            pd.DataFrame({"loss": [np.asarray(v, dtype=np.float32) for v in traj]}).to_csv(
+                os.path.join(path, "train_stats.csv"))
+            paths.append(path)
+    return paths if rank == 0 else None

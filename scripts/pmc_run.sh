@@ -1,13 +1,15 @@
 #!/bin/bash
-# PMC passes (separate runs, kernel-trace only) over a short bench; outputs under gpurun_out/pmc_*.
+# HBM traffic passes for the bench workload: FETCH_SIZE and WRITE_SIZE in separate rocprofv3 runs
+# (kernel-trace only, no other tracing), mapped to engine tags by scripts/tag_profile.py.
 set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-drsa"
-rocprofv3 -L > gpurun_out/counters_list.txt 2>&1 || true
-for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
-            "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VMEM" \
-            "FETCH_SIZE" "WRITE_SIZE"; do
-  tag=$(echo $pass | cut -d' ' -f1)
-  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $pass --output-format csv -d gpurun_out/pmc_$tag -o run -- $B > gpurun_out/pmc_$tag.log 2>&1 || echo "pass $tag failed"
+OUT=${1:-gpurun_out/pmc}
+mkdir -p $OUT
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $OUT/pmc_$c -o run -- \
+    python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-drsa --tag-order $OUT/tags_$c.json \
+    > $OUT/pmc_$c.log 2>&1
 done
+cp $OUT/tags_FETCH_SIZE.json $OUT/tags.json
+python scripts/tag_profile.py pmc $OUT $OUT/tags.json $OUT/pmc_traffic.json > /dev/null

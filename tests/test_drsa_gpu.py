@@ -140,3 +140,53 @@ def test_objective_api_and_optimizer_files(tmp_path, fx):
     with open(tmp_path / "projection_matrix.pkl", "rb") as fh:   # file written by this test
         U = pickle.load(fh)
     assert U.dtype == np.float32 and U.shape == (d, d)
+
+
+def _sharded_worker(rank, world, port, A, C, U0, K, steps, q):
+    import os, sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from drsa_audio_amd.xai.drsa.distributed import shard_rows, sharded_run
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    sl = shard_rows(A.shape[0], world, rank)
+    U, traj = sharded_run(torch.from_numpy(A[sl]).to(dev), torch.from_numpy(C[sl]).to(dev),
+                          torch.from_numpy(U0).to(dev), K, steps)
+    q.put((rank, U.cpu().numpy(), traj))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_run_two_ranks_gloo_matches_single():
+    """Two ranks on cuda:0 (gloo carries the [d*d+K] all-reduce): identical U on both ranks and
+    the same trajectory as the single-process HIP run up to the partial-sum order."""
+    import socket
+    import torch.multiprocessing as mp
+    from gen_fixtures import drsa_inputs
+    from drsa_audio_amd.xai.drsa.drsa import DrsaWorkspace, drsa_run
+    A, C = drsa_inputs(5001, 64, 11)
+    U0 = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "u64_seed42.npy"))
+    K, steps = 4, 20
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, 2, port, A, C, U0, K, steps, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (u, t) for r, u, t in (q.get(timeout=300) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert np.array_equal(res[0][0], res[1][0]) and np.array_equal(res[0][1], res[1][1])
+    dev = torch.device("cuda", 0)
+    ws = DrsaWorkspace(A.shape[0], 64, K, dev)
+    U1, traj1 = drsa_run(torch.from_numpy(A).to(dev), torch.from_numpy(C).to(dev), torch.from_numpy(U0).to(dev),
+                         K, steps, ws)
+    traj1 = traj1.cpu().numpy()
+    assert np.max(np.abs(res[0][1] - traj1) / np.abs(traj1)) < 1e-5
+    assert np.abs(res[0][0] - U1.cpu().numpy()).max() < 1e-4
