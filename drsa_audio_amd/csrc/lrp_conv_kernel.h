@@ -46,10 +46,14 @@ constexpr int halo_stride(int hx, int mw) {
 enum AMode { A_DENSE = 0, A_POOLSPARSE = 1 };
 enum Epi { EPI_FWD_POOL = 0, EPI_FWD_RELU = 1, EPI_BWD = 2 };
 
+// halo column c (pixel tx0 - 1 + c) lives at LDS column c + XO, so the tile interior starts
+// 16-byte aligned (float4 staging stores) and pool cells cover aligned float2 pairs.
+constexpr int XO = 3;
+
 template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI>
 struct ConvCfg {
   static constexpr int HY = TH + 2, HX = TW + 2;
-  static constexpr int RS = halo_stride(HX, MW);
+  static constexpr int RS = halo_stride(HX + XO, MW);
   static constexpr int PLANE_RAW = HY * RS;
   static constexpr int PLANE = PLANE_RAW + ((PLANE_RAW % 32) == 0 ? 4 : 0);
   static constexpr int MTH = 16 / MW;      // M-tile height (pixels)
@@ -74,6 +78,8 @@ struct ConvCfg {
   static_assert(CIN % CIC == 0, "CIN must be a multiple of the chunk");
   static_assert(MT % WM == 0 && NT % WN == 0 && WM * WN <= 4, "wave split");
 };
+
+#define TCH_OF(C) (C::TCH)
 
 template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI>
 __global__ __launch_bounds__(kThreads) void conv3x3_kernel(ConvArgs a) {
@@ -110,7 +116,7 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(ConvArgs a) {
     const int p = lane & 31, win = p >> 2, sub = p & 3;
     pix_y[u] = (mt / MTX) * MTH + 2 * (win / MW) + (sub >> 1);
     pix_x[u] = (mt % MTX) * MTW + 2 * (win % MW) + (sub & 1);
-    pix_off[u] = pix_y[u] * RS + pix_x[u];
+    pix_off[u] = pix_y[u] * RS + pix_x[u] + XO;
   }
 
   f32x16 acc[NG][MPW][NPW];
@@ -123,84 +129,201 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(ConvArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[g][u][v][r] = 0.f;
 
-  for (int chunk = 0; chunk < Cfg::NCHUNK; ++chunk) {
-    const int c0 = chunk * CIC;
-    __syncthreads();
-    if constexpr (AMODE == A_DENSE) {
-      // ---- halo [CIC][HY][HX] straight from the NCHW input (loads issued before stores) ----
-      constexpr int NE = CIC * HY * HX, IT = (NE + kThreads - 1) / kThreads;
-      float v[IT];
+  // ---- staging: registers <- global (load), LDS <- registers (store).  The loads of chunk
+  //      c+1 are issued before the MFMA loop of chunk c, so their latency hides behind it. ----
+  const bool vec = (W & 3) == 0;                 // float4 rows (else per-element loads)
+  // dense halo: interior rows of TW/4 float4 + the two halo columns
+  constexpr int Q4 = TW / 4, DROWS = CIC * HY;
+  constexpr int DI = (DROWS * Q4 + kThreads - 1) / kThreads, DH = (DROWS * 2 + kThreads - 1) / kThreads;
+  // pool-sparse cells: interior rows of TW/8 float4 (4 cells) + the two halo cell columns
+  constexpr int CY = TH / 2 + 2, CX = TW / 2 + 2, Q8 = TW / 8 > 0 ? TW / 8 : 1, SROWS = CIC * CY;
+  constexpr int SI = (SROWS * Q8 + kThreads - 1) / kThreads, SH = (SROWS * 2 + kThreads - 1) / kThreads;
+  constexpr bool DENSE = AMODE == A_DENSE;
+  constexpr int NI = DENSE ? DI : SI, NH = DENSE ? DH : SH;
+  constexpr int NWV = NG * KCP * (COUT / 4), WIT = (NWV + kThreads - 1) / kThreads;
+  float4 st_i[NI];
+  uint32_t st_ia[DENSE ? 1 : NI];
+  float st_h[NH];
+  int st_ha[DENSE ? 1 : NH];
+  float4 st_w[WIT];
+  const int H2 = H >> 1, W2 = W >> 1;
+  const bool noload = (a.dbg & 1) != 0;
+  auto stage_load = [&](int c0) {
+    if constexpr (DENSE) {
 #pragma unroll
-      for (int it = 0; it < IT; ++it) {
-        const int idx = tid + it * kThreads;
-        const int ci = idx / (HY * HX), rem = idx % (HY * HX);
-        const int hy = rem / HX, hx = rem % HX;
-        const int gy = ty0 - 1 + hy, gx = tx0 - 1 + hx, c = c0 + ci;
-        v[it] = (idx < NE && gy >= 0 && gy < H && gx >= 0 && gx < W && c < a.cin && !(a.dbg & 1))
-                    ? a.in[(((size_t)bq * a.cin + c) * H + gy) * W + gx] : 0.f;
+      for (int it = 0; it < DI; ++it) {
+        const int i = tid + it * kThreads;
+        const int row = i / Q4, q = i % Q4;
+        const int ci = row / HY, hy = row % HY;
+        const int gy = ty0 - 1 + hy, gx = tx0 + 4 * q, c = c0 + ci;
+        const bool rok = i < DROWS * Q4 && gy >= 0 && gy < H && c < a.cin && !noload;
+        const float* src = a.in + (((size_t)bq * a.cin + c) * H + gy) * W + gx;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (rok) {
+          if (vec) {
+            if (gx < W) v = *reinterpret_cast<const float4*>(src);
+          } else {
+            v.x = gx < W ? src[0] : 0.f;
+            v.y = gx + 1 < W ? src[1] : 0.f;
+            v.z = gx + 2 < W ? src[2] : 0.f;
+            v.w = gx + 3 < W ? src[3] : 0.f;
+          }
+        }
+        st_i[it] = v;
       }
 #pragma unroll
-      for (int it = 0; it < IT; ++it) {
-        const int idx = tid + it * kThreads;
-        if (idx < NE) {
-          const int ci = idx / (HY * HX), rem = idx % (HY * HX);
-          halo[ci * PLANE + (rem / HX) * RS + rem % HX] = v[it];
+      for (int it = 0; it < DH; ++it) {
+        const int i = tid + it * kThreads;
+        const int row = i >> 1, side = i & 1;
+        const int ci = row / HY, hy = row % HY;
+        const int gy = ty0 - 1 + hy, gx = side ? tx0 + TW : tx0 - 1, c = c0 + ci;
+        const bool ok = i < DROWS * 2 && gy >= 0 && gy < H && gx >= 0 && gx < W && c < a.cin && !noload;
+        st_h[it] = ok ? a.in[(((size_t)bq * a.cin + c) * H + gy) * W + gx] : 0.f;
+      }
+    } else {
+      const int qy0 = (ty0 >> 1) - 1, qx0 = (tx0 >> 1) - 1;
+#pragma unroll
+      for (int it = 0; it < SI; ++it) {
+        const int i = tid + it * kThreads;
+        const int row = i / Q8, q = i % Q8;
+        const int ci = row / CY, ry = row % CY;
+        const int cy = qy0 + ry, cx = qx0 + 1 + 4 * q, c = c0 + ci;
+        const bool rok = i < SROWS * Q8 && 4 * q < TW / 2 && cy >= 0 && cy < H2 && c < a.cin && !noload;
+        const size_t o = (((size_t)bq * a.cin + c) * H2 + cy) * W2 + cx;
+        const size_t oa = (((size_t)bs * a.cin + c) * H2 + cy) * W2 + cx;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        uint32_t am = 0x04040404u;
+        if (rok) {
+          if ((W2 & 3) == 0) {
+            if (cx < W2) {
+              v = *reinterpret_cast<const float4*>(a.in + o);
+              am = *reinterpret_cast<const uint32_t*>(a.in_amax + oa);
+            }
+          } else {
+            float vv[4];
+            uint32_t aa = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const bool eok = cx + e < W2 && 4 * q + e < TW / 2;
+              vv[e] = eok ? a.in[o + e] : 0.f;
+              aa |= (eok ? (uint32_t)a.in_amax[oa + e] : 4u) << (8 * e);
+            }
+            v = make_float4(vv[0], vv[1], vv[2], vv[3]);
+            am = aa;
+          }
+        }
+        st_i[it] = v;
+        st_ia[it] = am;
+      }
+#pragma unroll
+      for (int it = 0; it < SH; ++it) {
+        const int i = tid + it * kThreads;
+        const int row = i >> 1, side = i & 1;
+        const int ci = row / CY, ry = row % CY;
+        const int cy = qy0 + ry, cx = side ? qx0 + CX - 1 : qx0, c = c0 + ci;
+        const bool ok = i < SROWS * 2 && cy >= 0 && cy < H2 && cx >= 0 && cx < W2 && c < a.cin && !noload;
+        st_h[it] = ok ? a.in[(((size_t)bq * a.cin + c) * H2 + cy) * W2 + cx] : 0.f;
+        st_ha[it] = ok ? (int)a.in_amax[(((size_t)bs * a.cin + c) * H2 + cy) * W2 + cx] : 4;
+      }
+    }
+    // weights: rows [c0*9, c0*9 + KC) of every set, contiguous (k = ci*9 + tap)
+#pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      const int idx = tid + it * kThreads;
+      const int g = idx / (KCP * (COUT / 4)), rem = idx % (KCP * (COUT / 4));
+      const int k = rem / (COUT / 4), c4 = (rem % (COUT / 4)) * 4;
+      st_w[it] = (idx < NWV && k < KC)
+                     ? *reinterpret_cast<const float4*>(a.wts + ((size_t)g * 9 * CIN + c0 * 9 + k) * COUT + c4)
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  // one pool cell -> its 2x2 pixels at halo rows 2ry-1, 2ry and LDS columns 2rx-1+XO, 2rx+XO
+  auto put_cell = [&](int ci, int ry, int rx, float v, int sb) {
+    float* d = halo + ci * PLANE + (2 * ry - 1) * RS + 2 * rx - 1 + XO;
+    if (ry > 0)
+      *reinterpret_cast<float2*>(d) = make_float2(sb == 0 ? v : 0.f, sb == 1 ? v : 0.f);
+    if (ry < CY - 1)
+      *reinterpret_cast<float2*>(d + RS) = make_float2(sb == 2 ? v : 0.f, sb == 3 ? v : 0.f);
+  };
+  auto stage_store = [&]() {
+    if constexpr (DENSE) {
+#pragma unroll
+      for (int it = 0; it < DI; ++it) {
+        const int i = tid + it * kThreads;
+        if (i < DROWS * Q4) {
+          const int row = i / Q4, q = i % Q4;
+          const int ci = row / HY, hy = row % HY;
+          *reinterpret_cast<float4*>(halo + ci * PLANE + hy * RS + 1 + XO + 4 * q) = st_i[it];
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < DH; ++it) {
+        const int i = tid + it * kThreads;
+        if (i < DROWS * 2) {
+          const int row = i >> 1, side = i & 1;
+          const int ci = row / HY, hy = row % HY;
+          halo[ci * PLANE + hy * RS + (side ? HX - 1 : 0) + XO] = st_h[it];
         }
       }
     } else {
-      // ---- pool-sparse source: cells (g at pool resolution + argmax) cover the halo; each
-      //      cell writes its 2x2 pixels (value at the argmax position, zeros elsewhere) ----
-      constexpr int CY = TH / 2 + 2, CX = TW / 2 + 2, NE = CIC * CY * CX;
-      constexpr int IT = (NE + kThreads - 1) / kThreads;
-      const int H2 = H >> 1, W2 = W >> 1;
-      const int qy0 = (ty0 >> 1) - 1, qx0 = (tx0 >> 1) - 1;
-      float v[IT];
-      int sb[IT];
 #pragma unroll
-      for (int it = 0; it < IT; ++it) {
-        const int idx = tid + it * kThreads;
-        const int ci = idx / (CY * CX), rem = idx % (CY * CX);
-        const int cy = qy0 + rem / CX, cx = qx0 + rem % CX, c = c0 + ci;
-        const bool ok = idx < NE && cy >= 0 && cy < H2 && cx >= 0 && cx < W2 && c < a.cin && !(a.dbg & 1);
-        v[it] = ok ? a.in[(((size_t)bq * a.cin + c) * H2 + cy) * W2 + cx] : 0.f;
-        sb[it] = ok ? (int)a.in_amax[(((size_t)bs * a.cin + c) * H2 + cy) * W2 + cx] : 0;
+      for (int it = 0; it < SI; ++it) {
+        const int i = tid + it * kThreads;
+        const int q = i % Q8;
+        if (i < SROWS * Q8 && 4 * q < TW / 2) {
+          const int row = i / Q8;
+          const int ci = row / CY, ry = row % CY;
+          const float vv[4] = {st_i[it].x, st_i[it].y, st_i[it].z, st_i[it].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (4 * q + e < TW / 2) put_cell(ci, ry, 1 + 4 * q + e, vv[e], (int)((st_ia[it] >> (8 * e)) & 0xffu));
+        }
       }
 #pragma unroll
-      for (int it = 0; it < IT; ++it) {
-        const int idx = tid + it * kThreads;
-        if (idx < NE) {
-          const int ci = idx / (CY * CX), rem = idx % (CY * CX);
-          const int ry = rem / CX, rx = rem % CX;
-          // cell (ry, rx) covers halo rows 2ry-1, 2ry and cols 2rx-1, 2rx (halo origin = pixel ty0-1)
-#pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4) {
-            const int hy = 2 * ry - 1 + (s4 >> 1), hx = 2 * rx - 1 + (s4 & 1);
-            if (hy >= 0 && hy < HY && hx >= 0 && hx < HX)
-              halo[ci * PLANE + hy * RS + hx] = (sb[it] == s4) ? v[it] : 0.f;
-          }
+      for (int it = 0; it < SH; ++it) {
+        const int i = tid + it * kThreads;
+        if (i < SROWS * 2) {
+          const int row = i >> 1, side = i & 1;
+          put_cell(row / CY, row % CY, side ? CX - 1 : 0, st_h[it], st_ha[it]);
         }
       }
     }
-    {
-      // ---- weights: rows [c0*9, c0*9 + KC) of every set, contiguous (k = ci*9 + tap) ----
-      constexpr int NV = NG * KCP * (COUT / 4), IT = (NV + kThreads - 1) / kThreads;
-      float4 wv[IT];
 #pragma unroll
-      for (int it = 0; it < IT; ++it) {
-        const int idx = tid + it * kThreads;
-        const int g = idx / (KCP * (COUT / 4)), rem = idx % (KCP * (COUT / 4));
-        const int k = rem / (COUT / 4), c4 = (rem % (COUT / 4)) * 4;
-        wv[it] = (idx < NV && k < KC)
-                     ? *reinterpret_cast<const float4*>(a.wts + ((size_t)g * 9 * CIN + c0 * 9 + k) * COUT + c4)
-                     : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
+    for (int it = 0; it < WIT; ++it) {
+      const int idx = tid + it * kThreads;
+      if (idx < NWV) *reinterpret_cast<float4*>(wl + (size_t)idx * 4) = st_w[it];
+    }
+  };
+
+  // BWD epilogue inputs of the first n-tile pass (x, den), prefetched behind the last chunk
+  constexpr int V4E = (TCH_OF(Cfg) * TH * TW / 4 + kThreads - 1) / kThreads;
+  constexpr bool EPF = false && EPI == EPI_BWD;
+  float4 ex[EPF ? V4E : 1], ed[EPF ? V4E : 1];
+  auto epi_prefetch = [&]() {
+    if constexpr (EPF) {
 #pragma unroll
-      for (int it = 0; it < IT; ++it) {
-        const int idx = tid + it * kThreads;
-        if (idx < NV) *reinterpret_cast<float4*>(wl + (size_t)idx * 4) = wv[it];
+      for (int it = 0; it < V4E; ++it) {
+        const int i = tid + it * kThreads;
+        const int cl = i / (TH * TW / 4), rem = i % (TH * TW / 4);
+        const int py = rem / (TW / 4), px = (rem % (TW / 4)) * 4;
+        const int co = ((cl >> 5) * NPW) * 32 + (cl & 31);
+        const bool ok = i < TCH_OF(Cfg) * TH * TW / 4 && co < a.cout && ty0 + py < H && tx0 + px < W;
+        const size_t os = (((size_t)bs * a.cout + co) * H + ty0 + py) * W + tx0 + px;
+        ex[it] = (ok && (a.xmode != XM_NONE || a.post != POST_NONE)) ? *reinterpret_cast<const float4*>(a.x + os)
+                                                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+        ed[it] = (ok && a.post == POST_DIV) ? *reinterpret_cast<const float4*>(a.den + os)
+                                            : make_float4(1.f, 1.f, 1.f, 1.f);
       }
     }
+  };
+
+  stage_load(0);
+  for (int chunk = 0; chunk < Cfg::NCHUNK; ++chunk) {
     __syncthreads();
+    stage_store();
+    __syncthreads();
+    if (chunk + 1 < Cfg::NCHUNK) stage_load((chunk + 1) * CIC);
+    else epi_prefetch();
     if (!active || (a.dbg & 4)) continue;
     // ---- MFMA over the chunk.  k = k0 + h (h = lane half) with k = ci*9 + tap: the halo
     //      offset pattern repeats every 9 k-steps (two channels), so the 9 per-lane bases
@@ -434,7 +557,8 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(ConvArgs a) {
             if (a.xmode == XM_NONE || (a.dbg & 2)) {
               Rk[it] = t;
             } else {
-              const float4 x = *reinterpret_cast<const float4*>(a.x + (((size_t)bs * a.cout + co) * H + ty0 + py) * W + tx0 + px);
+              const float4 x = (EPF && v == 0) ? ex[it]
+                                        : *reinterpret_cast<const float4*>(a.x + (((size_t)bs * a.cout + co) * H + ty0 + py) * W + tx0 + px);
               if (a.xmode == XM_MUL) {
                 Rk[it] = make_float4(x.x * t.x, x.y * t.y, x.z * t.z, x.w * t.w);
               } else {
@@ -457,7 +581,8 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(ConvArgs a) {
               const int co = gch(cl, v);
               if (co < a.cout && ty0 + py < H && tx0 + px < W) {
                 const float4 t = *reinterpret_cast<const float4*>(T + (cl * TH + py) * TWP + px);
-                const float4 x = *reinterpret_cast<const float4*>(a.x + (((size_t)bs * a.cout + co) * H + ty0 + py) * W + tx0 + px);
+                const float4 x = (EPF && v == 0) ? ex[it]
+                                          : *reinterpret_cast<const float4*>(a.x + (((size_t)bs * a.cout + co) * H + ty0 + py) * W + tx0 + px);
                 Rk[it].x += fminf(x.x, 0.f) * t.x;
                 Rk[it].y += fminf(x.y, 0.f) * t.y;
                 Rk[it].z += fminf(x.z, 0.f) * t.z;
@@ -483,14 +608,14 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(ConvArgs a) {
               continue;
             }
             if (a.post == POST_DIV) {
-              const float4 x = *reinterpret_cast<const float4*>(a.x + os);
-              const float4 d = *reinterpret_cast<const float4*>(a.den + os);
+              const float4 x = (EPF && v == 0) ? ex[it] : *reinterpret_cast<const float4*>(a.x + os);
+              const float4 d = (EPF && v == 0) ? ed[it] : *reinterpret_cast<const float4*>(a.den + os);
               R.x = (x.x > 0.f) ? R.x / stab(d.x, a.eps) : 0.f;
               R.y = (x.y > 0.f) ? R.y / stab(d.y, a.eps) : 0.f;
               R.z = (x.z > 0.f) ? R.z / stab(d.z, a.eps) : 0.f;
               R.w = (x.w > 0.f) ? R.w / stab(d.w, a.eps) : 0.f;
             } else if (a.post == POST_MASK) {
-              const float4 x = *reinterpret_cast<const float4*>(a.x + os);
+              const float4 x = (EPF && v == 0) ? ex[it] : *reinterpret_cast<const float4*>(a.x + os);
               R.x = (x.x > 0.f) ? R.x : 0.f;
               R.y = (x.y > 0.f) ? R.y : 0.f;
               R.z = (x.z > 0.f) ? R.z : 0.f;

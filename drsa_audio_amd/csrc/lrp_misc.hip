@@ -199,8 +199,10 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
 //   g2    = R_h / stab(h, eps_proj)                  Epsilon on projection (after the mask)
 //   clone 0: v = g2 U^T ; clone k: v = g2[block k-1] U[:, block k-1]^T   (SubspaceHook mask)
 //   G_q   = [a > 0] (a (.) v) / stab(den, eps_den)   ReLU-backward + the conv rule's division below
-// Tiles of 2 x 32 pixels, lanes = pixels; U staged once per workgroup (PT tiles).
+// Tiles of 64 pixels (RPT rows x TW cols), lanes = pixels; one tile per workgroup.
 // ===========================================================================
+constexpr int PT_BWD = 1;   // tiles per workgroup (backward): one tile, many workgroups
+
 template <int D>
 __global__ __launch_bounds__(256) void projection_bwd_kernel(
     const float* __restrict__ gp, const uint8_t* __restrict__ amax, const float* __restrict__ ap,
@@ -208,6 +210,10 @@ __global__ __launch_bounds__(256) void projection_bwd_kernel(
     const float* __restrict__ U, float* __restrict__ G, int H, int W, int K, float eps_proj, float eps_den,
     int sparse, int has_den, int fanout) {
   constexpr int P = 64, LD = D + 1, PL = P + 4;
+  constexpr int NB = D / 16, TILES = NB * (P / 16), QW = TILES / 4;   // 16x16 blocks; per wave
+  // Per wave: pixel block pb = wave, channel blocks cb = 0..NB-1 (q = wave + 4 i).  Its h, a,
+  // den values (MFMA output layout) are prefetched at the start, with the staging loads.
+  constexpr bool PF = D <= 64;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* Us = sm;               // [D][LD]
   float* g1 = Us + D * LD;      // [D][PL]
@@ -217,14 +223,30 @@ __global__ __launch_bounds__(256) void projection_bwd_kernel(
   const int TW = W < 32 ? W : 32, RPT = P / TW;
   const int HW = H * W, xt = W / TW;
   const int dk = D / K;
-  for (int i = tid; i < D * D; i += 256) Us[(i / D) * LD + i % D] = U[i];
-  constexpr int NB = D / 16, TILES = NB * (P / 16);
   const int nq = fanout ? (K + 1) : 1;
-  for (int t = 0; t < PT; ++t) {
-    const int tile = blockIdx.x * PT + t;
+  for (int t = 0; t < PT_BWD; ++t) {
+    const int tile = blockIdx.x * PT_BWD + t;
     if (tile >= (H / RPT) * xt) break;
     const int y0 = (tile / xt) * RPT, x0 = (tile % xt) * TW;
+    // this lane's pixel in its wave's 16-pixel block, and the channel rows it owns
+    const int pl = w * 16 + (lane & 15);
+    const size_t pixl = (size_t)(y0 + pl / TW) * W + x0 + pl % TW;
+    float hv[PF ? QW * 4 : 1], av[PF ? QW * 4 : 1], dv[PF ? QW * 4 : 1];
+    if constexpr (PF) {
+#pragma unroll
+      for (int i = 0; i < QW; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = i * 16 + (lane >> 4) * 4 + r;
+          const size_t os = ((size_t)b * D + c) * HW + pixl;
+          hv[i * 4 + r] = h[os];
+          av[i * 4 + r] = a[os];
+          dv[i * 4 + r] = has_den ? den[os] : 1.f;
+        }
+    }
     __syncthreads();
+    if (t == 0)
+      for (int i = tid; i < D * D; i += 256) Us[(i / D) * LD + i % D] = U[i];
     for (int i = tid; i < D * P; i += 256) {
       const int c = i / P, p = i % P;
       const int y = y0 + p / TW, x = x0 + p % TW;
@@ -240,46 +262,54 @@ __global__ __launch_bounds__(256) void projection_bwd_kernel(
     }
     __syncthreads();
     // t[j][p] = sum_c U[c][j] g1[c][p];  R_h = h (.) t;  g2 = R_h / stab(h)
-    for (int q = w; q < TILES; q += 4) {
-      const int jb = q / (P / 16), pb = q % (P / 16);
+#pragma unroll
+    for (int i = 0; i < QW; ++i) {
+      const int jb = i, pb = w;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
       for (int k0 = 0; k0 < D; k0 += 4) {
         const int c = k0 + (lane >> 4);
         acc = mfma16(Us[c * LD + jb * 16 + (lane & 15)], g1[c * PL + pb * 16 + (lane & 15)], acc);
       }
+#pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int j = jb * 16 + (lane >> 4) * 4 + r, p = pb * 16 + (lane & 15);
-        const float hv = h[((size_t)b * D + j) * HW + (y0 + p / TW) * W + x0 + p % TW];
-        const float Rh = hv * acc[r];
-        g2[j * PL + p] = Rh / stab(hv, eps_proj);
+        float hx;
+        if constexpr (PF) hx = hv[i * 4 + r];
+        else hx = h[((size_t)b * D + j) * HW + pixl];
+        const float Rh = hx * acc[r];
+        g2[j * PL + p] = Rh / stab(hx, eps_proj);
       }
     }
     __syncthreads();
-    for (int q2 = w; q2 < nq * TILES; q2 += 4) {
-      const int qi = q2 / TILES, tt = q2 % TILES;
+    for (int qi = 0; qi < nq; ++qi) {
       const int q = fanout ? qi : b % (K + 1);
-      const int cb = tt / (P / 16), pb = tt % (P / 16);
       const int j0 = q == 0 ? 0 : (q - 1) * dk, j1 = q == 0 ? D : q * dk;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      for (int k0 = j0; k0 < j1; k0 += 4) {
-        const int j = k0 + (lane >> 4);
-        const bool ok = j < j1;
-        const float av = ok ? Us[(cb * 16 + (lane & 15)) * LD + j] : 0.f;
-        const float bv = ok ? g2[j * PL + pb * 16 + (lane & 15)] : 0.f;
-        acc = mfma16(av, bv, acc);
-      }
       const size_t orow = fanout ? (size_t)b * (K + 1) + q : (size_t)b;
-      for (int r = 0; r < 4; ++r) {
-        const int c = cb * 16 + (lane >> 4) * 4 + r, p = pb * 16 + (lane & 15);
-        const size_t pix = (size_t)(y0 + p / TW) * W + x0 + p % TW;
-        const size_t os = ((size_t)b * D + c) * HW + pix;
-        const float av = a[os];
-        const float Rv = av * acc[r];
-        float g;
-        if (has_den) g = (av > 0.f) ? Rv / stab(den[os], eps_den) : 0.f;
-        else g = (av > 0.f) ? Rv : 0.f;
-        G[(orow * D + c) * HW + pix] = g;
+#pragma unroll
+      for (int i = 0; i < QW; ++i) {
+        const int cb = i, pb = w;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int k0 = j0; k0 < j1; k0 += 4) {
+          const int j = k0 + (lane >> 4);
+          const bool ok = j < j1;
+          const float ua = ok ? Us[(cb * 16 + (lane & 15)) * LD + j] : 0.f;
+          const float gb = ok ? g2[j * PL + pb * 16 + (lane & 15)] : 0.f;
+          acc = mfma16(ua, gb, acc);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = cb * 16 + (lane >> 4) * 4 + r;
+          const size_t os = ((size_t)b * D + c) * HW + pixl;
+          float ax, dx;
+          if constexpr (PF) { ax = av[i * 4 + r]; dx = dv[i * 4 + r]; }
+          else { ax = a[os]; dx = has_den ? den[os] : 1.f; }
+          const float Rv = ax * acc[r];
+          float gq;
+          if (has_den) gq = (ax > 0.f) ? Rv / stab(dx, eps_den) : 0.f;
+          else gq = (ax > 0.f) ? Rv : 0.f;
+          G[(orow * D + c) * HW + pixl] = gq;
+        }
       }
     }
   }
@@ -354,91 +384,127 @@ __global__ __launch_bounds__(256) void first_layer_bwd_kernel(const float* __res
   }
 }
 
-// Pool-sparse variant (the VGG case: conv0 -> ReLU -> MaxPool2d(2)).  One thread per pool
-// cell = 2x2 output pixels.  The cells of the tile (+1 halo) are expanded to pixels while
-// staging (value at the argmax position, zeros elsewhere) into an LDS image whose origin is
-// pixel (2qy0-1, 2qx0-1), so every row of a thread's 4x4 input patch starts at an even column
-// and is two aligned 8-byte reads.  Then 9
-// fmas per pixel and channel in the dense chain order (channel, dy, dx) — the chain of the
-// dense kernel above and of oracle/lrp_exact.c, zeros included.
-constexpr int FQ_Y = 8, FQ_X = 32, FQ_C = 8;
+// Pool-sparse variant (the VGG case: conv0 -> ReLU -> MaxPool2d(2)).  A workgroup covers
+// 16 x 64 pool cells (32 x 128 output pixels); each thread owns 2 x 2 cells = a 4 x 4 pixel
+// block.  Per group of FQ_C channels the cells of the tile (+1 halo) are expanded to pixels
+// while staging (value at the argmax position, zeros elsewhere; two 8-byte LDS writes per
+// cell) into an image with origin pixel (2qy0-2, 2qx0-2); the next group's cells are
+// prefetched into registers while the current group is consumed.  Every thread reads its
+// 6 x 6 patch per channel and runs 9 fmas per pixel in the dense chain order
+// (channel, dy, dx) — the chain of the dense kernel above and of oracle/lrp_exact.c (the
+// zero terms included: fma(0, w, acc) == acc).
+constexpr int FQ_Y = 16, FQ_X = 64, FQ_C = 4;
+constexpr int FQ_RY = FQ_Y + 2, FQ_RX = FQ_X + 2;            // cells incl. halo
+constexpr int FQ_PY = 2 * FQ_RY, FQ_PX = 2 * FQ_RX + 4;      // pixel image (row pad 4)
+constexpr int FQ_KR = (FQ_RY + 3) / 4;                       // row passes of 4 waves
+constexpr int FQ_NS = FQ_C * FQ_KR + 1;                      // staged cells per thread
+
+__device__ __forceinline__ void fq_put(float* img, int ci, int ry, int rx, float v, int sb) {
+  float* d = img + (ci * FQ_PY + 2 * ry) * FQ_PX + 2 * rx;
+  *reinterpret_cast<float2*>(d) = make_float2(sb == 0 ? v : 0.f, sb == 1 ? v : 0.f);
+  *reinterpret_cast<float2*>(d + FQ_PX) = make_float2(sb == 2 ? v : 0.f, sb == 3 ? v : 0.f);
+}
 
 __global__ __launch_bounds__(256) void first_layer_bwd_pooled_kernel(const float* __restrict__ g,
                                                                      const uint8_t* __restrict__ amax,
                                                                      const float* __restrict__ w2,
                                                                      float* __restrict__ out, int C, int H, int W,
                                                                      int clones) {
-  constexpr int RY = FQ_Y + 2, RX = FQ_X + 2;      // cells incl. halo
-  constexpr int PY = 2 * FQ_Y + 2, PX = 2 * FQ_X + 4;   // pixel image, origin (2qy0-1, 2qx0-1)
-  __shared__ __attribute__((aligned(16))) float img[FQ_C][PY][PX];
-  const int tid = threadIdx.x;
+  extern __shared__ __attribute__((aligned(16))) float img[];    // [FQ_C][FQ_PY][FQ_PX]
+  const int tid = threadIdx.x, lane = tid & 63, wv4 = tid >> 6;
   const int H2 = H / 2, W2 = W / 2;
   const int tiles_x = (W2 + FQ_X - 1) / FQ_X;
   const int qy0 = (blockIdx.x / tiles_x) * FQ_Y, qx0 = (blockIdx.x % tiles_x) * FQ_X;
   const int bq = blockIdx.y, bs = bq / clones;
-  const int ty = tid / FQ_X, tx = tid % FQ_X;
-  const int qy = qy0 + ty, qx = qx0 + tx;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  const int ty = tid / (FQ_X / 2), tx = tid % (FQ_X / 2);      // 8 x 32 threads, 2x2 cells each
+  const size_t plane = (size_t)H2 * W2;
+  const float* gb = g + (size_t)bq * C * plane;
+  const uint8_t* ab = amax + (size_t)bs * C * plane;
+  // staging map: interior columns rx = 1 + lane, rows ry = wave + 4k; the two halo columns
+  // (rx = 0, 65) of all rows and channels by threads tid < 2 * FQ_RY * FQ_C
+  const int hci = tid / (2 * FQ_RY), hr = tid % (2 * FQ_RY);
+  const int hry = hr >> 1, hrx = (hr & 1) ? FQ_RX - 1 : 0;
+  const bool hact = tid < 2 * FQ_RY * FQ_C;
+  float v[FQ_NS];
+  int sb[FQ_NS];
+  auto fetch = [&](int c0) {
+    const int cx = qx0 + lane;
+#pragma unroll
+    for (int ci = 0; ci < FQ_C; ++ci)
+#pragma unroll
+      for (int k = 0; k < FQ_KR; ++k) {
+        const int ry = wv4 + 4 * k, cy = qy0 - 1 + ry, c = c0 + ci;
+        const bool ok = ry < FQ_RY && c < C && cy >= 0 && cy < H2 && cx < W2;
+        const size_t o = c * plane + (size_t)cy * W2 + cx;
+        v[ci * FQ_KR + k] = ok ? gb[o] : 0.f;
+        sb[ci * FQ_KR + k] = ok ? (int)ab[o] : 4;
+      }
+    {
+      const int c = c0 + hci, cy = qy0 - 1 + hry, cxh = qx0 - 1 + hrx;
+      const bool ok = hact && c < C && cy >= 0 && cy < H2 && cxh >= 0 && cxh < W2;
+      const size_t o = c * plane + (size_t)cy * W2 + cxh;
+      v[FQ_NS - 1] = ok ? gb[o] : 0.f;
+      sb[FQ_NS - 1] = ok ? (int)ab[o] : 4;
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int ci = 0; ci < FQ_C; ++ci)
+#pragma unroll
+      for (int k = 0; k < FQ_KR; ++k) {
+        const int ry = wv4 + 4 * k;
+        if (ry < FQ_RY) fq_put(img, ci, ry, 1 + lane, v[ci * FQ_KR + k], sb[ci * FQ_KR + k]);
+      }
+    if (hact) fq_put(img, hci, hry, hrx, v[FQ_NS - 1], sb[FQ_NS - 1]);
+  };
+  float acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  fetch(0);
   for (int c0 = 0; c0 < C; c0 += FQ_C) {
     __syncthreads();
-    constexpr int NE = FQ_C * RY * RX;
-    constexpr int IT = (NE + 255) / 256;
-    float v[IT];
-    int sb[IT];
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int idx = tid + it * 256;
-      const int ci = idx / (RY * RX), rem = idx % (RY * RX);
-      const int cy = qy0 - 1 + rem / RX, cx = qx0 - 1 + rem % RX, c = c0 + ci;
-      const bool ok = idx < NE && c < C && cy >= 0 && cy < H2 && cx >= 0 && cx < W2;
-      v[it] = ok ? g[(((size_t)bq * C + c) * H2 + cy) * W2 + cx] : 0.f;
-      sb[it] = ok ? (int)amax[(((size_t)bs * C + c) * H2 + cy) * W2 + cx] : 4;
-    }
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int idx = tid + it * 256;
-      if (idx < NE) {
-        const int ci = idx / (RY * RX), rem = idx % (RY * RX);
-        const int ry = rem / RX, rx = rem % RX;
-        // cell (ry, rx) = cell (qy0-1+ry, qx0-1+rx) -> pixel (2cy+sr, 2cx+sc) -> image (2ry-1+sr, 2rx-1+sc)
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-          const int iy = 2 * ry - 1 + (s4 >> 1), ix = 2 * rx - 1 + (s4 & 1);
-          if (iy >= 0 && iy < PY && ix >= 0 && ix < PX) img[ci][iy][ix] = (sb[it] == s4) ? v[it] : 0.f;
-        }
-      }
-    }
+    stage();
     __syncthreads();
-#pragma unroll 2
+    if (c0 + FQ_C < C) fetch(c0 + FQ_C);
+#pragma unroll 1
     for (int ci = 0; ci < FQ_C; ++ci) {
       const int c = c0 + ci;
       float wv[9];
 #pragma unroll
       for (int t = 0; t < 9; ++t) wv[t] = (c < C) ? w2[c * 9 + t] : 0.f;
-      // patch P[i][j] = pixel (2qy - 1 + i, 2qx - 1 + j) = img[2ty + i][2tx + j]  (8-byte aligned pairs)
-      float P[4][4];
+      // patch P[i][j] = pixel (2qy0 + 4ty - 1 + i, 2qx0 + 4tx - 1 + j) = img[4ty + 1 + i][4tx + 1 + j]
+      float P[6][6];
+      const float* base = img + (ci * FQ_PY + 4 * ty + 1) * FQ_PX + 4 * tx;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float2 p0 = *reinterpret_cast<const float2*>(&img[ci][2 * ty + i][2 * tx]);
-        const float2 p1 = *reinterpret_cast<const float2*>(&img[ci][2 * ty + i][2 * tx + 2]);
-        P[i][0] = p0.x; P[i][1] = p0.y; P[i][2] = p1.x; P[i][3] = p1.y;
+      for (int i = 0; i < 6; ++i) {
+        const float* r = base + i * FQ_PX;
+        const float2 a0 = *reinterpret_cast<const float2*>(r);
+        const float2 a1 = *reinterpret_cast<const float2*>(r + 2);
+        const float2 a2 = *reinterpret_cast<const float2*>(r + 4);
+        const float2 a3 = *reinterpret_cast<const float2*>(r + 6);
+        P[i][0] = a0.y; P[i][1] = a1.x; P[i][2] = a1.y; P[i][3] = a2.x; P[i][4] = a2.y; P[i][5] = a3.x;
       }
 #pragma unroll
-      for (int py = 0; py < 2; ++py)
+      for (int py = 0; py < 4; ++py)
 #pragma unroll
-        for (int px = 0; px < 2; ++px)
+        for (int dy = -1; dy <= 1; ++dy)
 #pragma unroll
-          for (int dy = -1; dy <= 1; ++dy)
+          for (int dx = -1; dx <= 1; ++dx) {
+            const float w = wv[(1 - dy) * 3 + (1 - dx)];
 #pragma unroll
-            for (int dx = -1; dx <= 1; ++dx)
-              acc[py * 2 + px] = fmaf(P[py + 1 + dy][px + 1 + dx], wv[(1 - dy) * 3 + (1 - dx)], acc[py * 2 + px]);
+            for (int px = 0; px < 4; ++px) acc[py][px] = fmaf(P[py + 1 + dy][px + 1 + dx], w, acc[py][px]);
+          }
     }
   }
-  if (qy < H2 && qx < W2) {
+  const int oy = 2 * qy0 + 4 * ty, ox = 2 * qx0 + 4 * tx;
+  if (2 * (qx0 + 2 * tx) < W && ox < W) {
 #pragma unroll
-    for (int py = 0; py < 2; ++py) {
-      float2 v2 = make_float2(acc[py * 2], acc[py * 2 + 1]);
-      *reinterpret_cast<float2*>(out + ((size_t)bq * H + 2 * qy + py) * W + 2 * qx) = v2;
+    for (int py = 0; py < 4; ++py) {
+      if (oy + py < H)
+        *reinterpret_cast<float4*>(out + ((size_t)bq * H + oy + py) * W + ox) =
+            make_float4(acc[py][0], acc[py][1], acc[py][2], acc[py][3]);
     }
   }
 }
@@ -600,7 +666,7 @@ int drsa_amd_projection_bwd(const float* gp, const uint8_t* amax, const float* a
   DRSA_REQUIRE(K > 0 && D % K == 0, "projection_bwd: K must divide d");
   hipStream_t s = (hipStream_t)stream;
   const int tiles = (H / (64 / TW)) * (W / TW);
-  const dim3 grid((tiles + PT - 1) / PT, B);
+  const dim3 grid((tiles + PT_BWD - 1) / PT_BWD, B);
   const int sparse = amax != nullptr, has_den = den != nullptr;
   switch (D) {
 #define PB(DD)                                                                                        \
@@ -628,8 +694,15 @@ int drsa_amd_first_layer_bwd(const float* g, const uint8_t* amax, const float* w
     DRSA_REQUIRE(H % 2 == 0 && W % 4 == 0, "first_layer_bwd: pooled path needs even H and W % 4 == 0");
     const int H2 = H / 2, W2 = W / 2;
     const dim3 grid(((H2 + FQ_Y - 1) / FQ_Y) * ((W2 + FQ_X - 1) / FQ_X), Bq);
-    hipLaunchKernelGGL(first_layer_bwd_pooled_kernel, grid, dim3(256), 0, (hipStream_t)stream, g, amax, w2f, out, C,
-                       H, W, clones);
+    constexpr size_t lds = sizeof(float) * FQ_C * FQ_PY * FQ_PX;
+    static bool set = false;
+    if (!set) {
+      DRSA_HIP(hipFuncSetAttribute((const void*)first_layer_bwd_pooled_kernel,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      set = true;
+    }
+    hipLaunchKernelGGL(first_layer_bwd_pooled_kernel, grid, dim3(256), lds, (hipStream_t)stream, g, amax, w2f, out,
+                       C, H, W, clones);
   } else {
     const dim3 grid(((H + FL_TH - 1) / FL_TH) * ((W + FL_TW - 1) / FL_TW), Bq);
     hipLaunchKernelGGL(first_layer_bwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, g, amax, w2f, out, C, H, W,
