@@ -59,7 +59,6 @@ int launch(const Entry* e, const ConvArgs& args, int batch, hipStream_t s) {
 
 int cin_pad(int cin) { return cin == 1 ? 1 : pad32(cin); }
 
-
 }  // namespace
 
 extern "C" {
@@ -96,16 +95,16 @@ int drsa_amd_conv_bwd(const float* g, const uint8_t* g_amax, const float* wts, c
   DRSA_REQUIRE(xmode == XM_NONE || x, "conv_bwd: xmode needs x");
   DRSA_REQUIRE(post == POST_NONE || (x && (den || post == POST_MASK)), "conv_bwd: POST_DIV needs x and den");
   const int cin_p = pad32(cin), cout_p = pad32(cout);
-  const Entry* e = find(cin_p, cout_p, W, ng, g_amax ? A_POOLSPARSE : A_DENSE, EPI_BWD);
-  if (!e) {
-    drsa::set_error("conv_bwd: no kernel for cin=%d cout=%d W=%d ng=%d sparse=%d", cin, cout, W, ng, g_amax != nullptr);
-    return DRSA_EUNSUPPORTED;
-  }
   ConvArgs a{};
   a.in = g; a.in_amax = g_amax; a.wts = wts; a.x = x; a.den = den; a.out = out; a.H = H; a.W = W;
   a.cin = cin; a.cout = cout; a.clones = clones; a.xmode = xmode; a.post = post; a.eps = eps;
   static const int dbg = env_int("DRSA_AMD_CONV_DBG", 0);
   a.dbg = dbg;
+  const Entry* e = find(cin_p, cout_p, W, ng, g_amax ? A_POOLSPARSE : A_DENSE, EPI_BWD);
+  if (!e) {
+    drsa::set_error("conv_bwd: no kernel for cin=%d cout=%d W=%d ng=%d sparse=%d", cin, cout, W, ng, g_amax != nullptr);
+    return DRSA_EUNSUPPORTED;
+  }
   return launch(e, a, Bq, (hipStream_t)stream);
 }
 

@@ -52,6 +52,8 @@ constexpr int XO = 3;
 
 template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI>
 struct ConvCfg {
+  static constexpr int CIN_ = CIN, COUT_ = COUT, TH_ = TH, TW_ = TW, MW_ = MW, CIC_ = CIC, NG_ = NG;
+  static constexpr int AMODE_ = AMODE, EPI_ = EPI;
   static constexpr int HY = TH + 2, HX = TW + 2;
   static constexpr int RS = halo_stride(HX + XO, MW);
   static constexpr int PLANE_RAW = HY * RS;
@@ -79,7 +81,261 @@ struct ConvCfg {
   static_assert(MT % WM == 0 && NT % WN == 0 && WM * WN <= 4, "wave split");
 };
 
-#define TCH_OF(C) (C::TCH)
+// ---- staging of one input-channel chunk: registers <- global (load), LDS <- registers
+//      (store), split so that the loads of the next chunk can be issued before the MFMA loop
+//      of the current one.  NT_ threads take part (tid in [0, NT_)). ----
+template <class Cfg, int NT_ = kThreads>
+struct Stager {
+  static constexpr int CIN = Cfg::CIN_, COUT = Cfg::COUT_, TH = Cfg::TH_, TW = Cfg::TW_, CIC = Cfg::CIC_;
+  static constexpr int NG = Cfg::NG_, HY = Cfg::HY, HX = Cfg::HX, RS = Cfg::RS, PLANE = Cfg::PLANE;
+  static constexpr int KC = Cfg::KC, KCP = Cfg::KCP;
+  static constexpr bool DENSE = Cfg::AMODE_ == A_DENSE;
+  // dense halo: interior rows of TW/4 float4 + the two halo columns
+  static constexpr int Q4 = TW / 4, DROWS = CIC * HY;
+  static constexpr int DI = (DROWS * Q4 + NT_ - 1) / NT_, DH = (DROWS * 2 + NT_ - 1) / NT_;
+  // pool-sparse cells: interior rows of TW/8 float4 (4 cells) + the two halo cell columns
+  static constexpr int CY = TH / 2 + 2, CX = TW / 2 + 2, Q8 = TW / 8 > 0 ? TW / 8 : 1, SROWS = CIC * CY;
+  static constexpr int SI = (SROWS * Q8 + NT_ - 1) / NT_, SH = (SROWS * 2 + NT_ - 1) / NT_;
+  static constexpr int NI = DENSE ? DI : SI, NH = DENSE ? DH : SH;
+  static constexpr int NWV = NG * KCP * (COUT / 4), WIT = (NWV + NT_ - 1) / NT_;
+  float4 st_i[NI];
+  uint32_t st_ia[DENSE ? 1 : NI];
+  float st_h[NH];
+  int st_ha[DENSE ? 1 : NH];
+  float4 st_w[WIT];
+
+  // Loads are unconditional from a clamped (always valid) address and masked afterwards, so
+  // the compiler issues them back to back without exec branches or per-load waits.
+  __device__ __forceinline__ void load(const ConvArgs& a, int c0, int tid, int ty0, int tx0, int bq, int bs) {
+    const int H = a.H, W = a.W, H2 = H >> 1, W2 = W >> 1;
+    const bool noload = (a.dbg & 1) != 0;
+    if constexpr (DENSE) {
+      if ((W & 3) == 0) {
+#pragma unroll
+        for (int it = 0; it < DI; ++it) {
+          const int i = tid + it * NT_;
+          const int row = i / Q4, q = i % Q4;
+          const int ci = row / HY, hy = row % HY;
+          const int gy = ty0 - 1 + hy, gx = tx0 + 4 * q, c = c0 + ci;
+          const bool ok = i < DROWS * Q4 && gy >= 0 && gy < H && c < a.cin && gx < W && !noload;
+          const size_t o = ok ? (((size_t)bq * a.cin + c) * H + gy) * W + gx : 0;
+          const float4 v = *reinterpret_cast<const float4*>(a.in + o);
+          st_i[it] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      } else {
+#pragma unroll
+        for (int it = 0; it < DI; ++it) {
+          const int i = tid + it * NT_;
+          const int row = i / Q4, q = i % Q4;
+          const int ci = row / HY, hy = row % HY;
+          const int gy = ty0 - 1 + hy, gx = tx0 + 4 * q, c = c0 + ci;
+          const bool rok = i < DROWS * Q4 && gy >= 0 && gy < H && c < a.cin && !noload;
+          float vv[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool ok = rok && gx + e < W;
+            const size_t o = ok ? (((size_t)bq * a.cin + c) * H + gy) * W + gx + e : 0;
+            const float v = a.in[o];
+            vv[e] = ok ? v : 0.f;
+          }
+          st_i[it] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < DH; ++it) {
+        const int i = tid + it * NT_;
+        const int row = i >> 1, side = i & 1;
+        const int ci = row / HY, hy = row % HY;
+        const int gy = ty0 - 1 + hy, gx = side ? tx0 + TW : tx0 - 1, c = c0 + ci;
+        const bool ok = i < DROWS * 2 && gy >= 0 && gy < H && gx >= 0 && gx < W && c < a.cin && !noload;
+        const size_t o = ok ? (((size_t)bq * a.cin + c) * H + gy) * W + gx : 0;
+        const float v = a.in[o];
+        st_h[it] = ok ? v : 0.f;
+      }
+    } else {
+      const int qy0 = (ty0 >> 1) - 1, qx0 = (tx0 >> 1) - 1;
+      if ((W2 & 3) == 0) {
+#pragma unroll
+        for (int it = 0; it < SI; ++it) {
+          const int i = tid + it * NT_;
+          const int row = i / Q8, q = i % Q8;
+          const int ci = row / CY, ry = row % CY;
+          const int cy = qy0 + ry, cx = qx0 + 1 + 4 * q, c = c0 + ci;
+          const bool ok = i < SROWS * Q8 && 4 * q < TW / 2 && cy >= 0 && cy < H2 && c < a.cin && cx < W2 && !noload;
+          const size_t o = ok ? (((size_t)bq * a.cin + c) * H2 + cy) * W2 + cx : 0;
+          const size_t oa = ok ? (((size_t)bs * a.cin + c) * H2 + cy) * W2 + cx : 0;
+          const float4 v = *reinterpret_cast<const float4*>(a.in + o);
+          const uint32_t am = *reinterpret_cast<const uint32_t*>(a.in_amax + oa);
+          st_i[it] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+          st_ia[it] = ok ? am : 0x04040404u;
+        }
+      } else {
+#pragma unroll
+        for (int it = 0; it < SI; ++it) {
+          const int i = tid + it * NT_;
+          const int row = i / Q8, q = i % Q8;
+          const int ci = row / CY, ry = row % CY;
+          const int cy = qy0 + ry, cx = qx0 + 1 + 4 * q, c = c0 + ci;
+          const bool rok = i < SROWS * Q8 && 4 * q < TW / 2 && cy >= 0 && cy < H2 && c < a.cin && !noload;
+          float vv[4];
+          uint32_t aa = 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool ok = rok && cx + e < W2 && 4 * q + e < TW / 2;
+            const size_t o = ok ? (((size_t)bq * a.cin + c) * H2 + cy) * W2 + cx + e : 0;
+            const size_t oa = ok ? (((size_t)bs * a.cin + c) * H2 + cy) * W2 + cx + e : 0;
+            const float v = a.in[o];
+            const uint32_t am = a.in_amax[oa];
+            vv[e] = ok ? v : 0.f;
+            aa |= (ok ? am : 4u) << (8 * e);
+          }
+          st_i[it] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+          st_ia[it] = aa;
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < SH; ++it) {
+        const int i = tid + it * NT_;
+        const int row = i >> 1, side = i & 1;
+        const int ci = row / CY, ry = row % CY;
+        const int cy = qy0 + ry, cx = side ? qx0 + CX - 1 : qx0, c = c0 + ci;
+        const bool ok = i < SROWS * 2 && cy >= 0 && cy < H2 && cx >= 0 && cx < W2 && c < a.cin && !noload;
+        const size_t o = ok ? (((size_t)bq * a.cin + c) * H2 + cy) * W2 + cx : 0;
+        const size_t oa = ok ? (((size_t)bs * a.cin + c) * H2 + cy) * W2 + cx : 0;
+        const float v = a.in[o];
+        const int am = (int)a.in_amax[oa];
+        st_h[it] = ok ? v : 0.f;
+        st_ha[it] = ok ? am : 4;
+      }
+    }
+    // weights: rows [c0*9, c0*9 + KC) of every set, contiguous (k = ci*9 + tap)
+#pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      const int idx = tid + it * NT_;
+      const int g = idx / (KCP * (COUT / 4)), rem = idx % (KCP * (COUT / 4));
+      const int k = rem / (COUT / 4), c4 = (rem % (COUT / 4)) * 4;
+      const bool ok = idx < NWV && k < KC;
+      const float4 v = *reinterpret_cast<const float4*>(a.wts + (ok ? ((size_t)g * 9 * CIN + c0 * 9 + k) * COUT + c4 : 0));
+      st_w[it] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+
+  // one pool cell -> its 2x2 pixels at halo rows 2ry-1, 2ry and LDS columns 2rx-1+XO, 2rx+XO
+  __device__ __forceinline__ static void put_cell(float* halo, int ci, int ry, int rx, float v, int sb) {
+    float* d = halo + ci * PLANE + (2 * ry - 1) * RS + 2 * rx - 1 + XO;
+    if (ry > 0) *reinterpret_cast<float2*>(d) = make_float2(sb == 0 ? v : 0.f, sb == 1 ? v : 0.f);
+    if (ry < CY - 1) *reinterpret_cast<float2*>(d + RS) = make_float2(sb == 2 ? v : 0.f, sb == 3 ? v : 0.f);
+  }
+
+  __device__ __forceinline__ void store(float* halo, float* wl, int tid) const {
+    if constexpr (DENSE) {
+#pragma unroll
+      for (int it = 0; it < DI; ++it) {
+        const int i = tid + it * NT_;
+        if (i < DROWS * Q4) {
+          const int row = i / Q4, q = i % Q4;
+          const int ci = row / HY, hy = row % HY;
+          *reinterpret_cast<float4*>(halo + ci * PLANE + hy * RS + 1 + XO + 4 * q) = st_i[it];
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < DH; ++it) {
+        const int i = tid + it * NT_;
+        if (i < DROWS * 2) {
+          const int row = i >> 1, side = i & 1;
+          const int ci = row / HY, hy = row % HY;
+          halo[ci * PLANE + hy * RS + (side ? HX - 1 : 0) + XO] = st_h[it];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int it = 0; it < SI; ++it) {
+        const int i = tid + it * NT_;
+        const int q = i % Q8;
+        if (i < SROWS * Q8 && 4 * q < TW / 2) {
+          const int row = i / Q8;
+          const int ci = row / CY, ry = row % CY;
+          const float vv[4] = {st_i[it].x, st_i[it].y, st_i[it].z, st_i[it].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (4 * q + e < TW / 2) put_cell(halo, ci, ry, 1 + 4 * q + e, vv[e], (int)((st_ia[it] >> (8 * e)) & 0xffu));
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < SH; ++it) {
+        const int i = tid + it * NT_;
+        if (i < SROWS * 2) {
+          const int row = i >> 1, side = i & 1;
+          put_cell(halo, row / CY, row % CY, side ? CX - 1 : 0, st_h[it], st_ha[it]);
+        }
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      const int idx = tid + it * NT_;
+      if (idx < NWV) *reinterpret_cast<float4*>(wl + (size_t)idx * 4) = st_w[it];
+    }
+  }
+};
+
+// ---- MFMA over one staged chunk.  k = k0 + h (h = lane half) with k = ci*9 + tap: the halo
+//      offset pattern repeats every 9 k-steps (two channels), so every LDS read in the fully
+//      unrolled loop is a per-lane base register + immediate.  Operands of step k0 are read
+//      one step ahead (explicit software pipeline). ----
+template <class Cfg, int PD = 1>
+__device__ __forceinline__ void mfma_chunk(const float* halo, const float* wl, const int (&pix_off)[Cfg::MPW],
+                                           int lane, int wn, f32x16 (&acc)[Cfg::NG_][Cfg::MPW][Cfg::NPW]) {
+  constexpr int MPW = Cfg::MPW, NPW = Cfg::NPW, NG = Cfg::NG_, COUT = Cfg::COUT_;
+  constexpr int KC = Cfg::KC, KCP = Cfg::KCP, PLANE = Cfg::PLANE, RS = Cfg::RS, EPI = Cfg::EPI_;
+  const int h = lane >> 5;
+  auto read_x = [&](int k0, float (&xv)[MPW]) {
+    const int jj = (k0 / 2) % 9, mm = (k0 / 2) / 9;
+    const int kk = 2 * jj + h;
+    const int off = (kk / 9) * PLANE + ((kk % 9) / 3) * RS + (kk % 3) + mm * 2 * PLANE;
+#pragma unroll
+    for (int u = 0; u < MPW; ++u) {
+      if constexpr (KC % 2 == 0) xv[u] = halo[off + pix_off[u]];
+      else xv[u] = (k0 + h < KC) ? halo[off + pix_off[u]] : 0.f;
+    }
+  };
+  auto read_w = [&](int k0, float (&wv)[NG][NPW]) {
+#pragma unroll
+    for (int v = 0; v < NPW; ++v)
+#pragma unroll
+      for (int g = 0; g < NG; ++g) wv[g][v] = wl[((size_t)g * KCP + k0 + h) * COUT + (wn * NPW + v) * 32 + (lane & 31)];
+  };
+  // operand ring: step k0's operands are read PD steps ahead
+  float xr[PD + 1][MPW], wr[PD + 1][NG][NPW];
+#pragma unroll
+  for (int d = 0; d < PD; ++d)
+    if (2 * d < KCP) {
+      read_x(2 * d, xr[d]);
+      read_w(2 * d, wr[d]);
+    }
+#pragma unroll
+  for (int k0 = 0; k0 < KCP; k0 += 2) {
+    const int cur = (k0 / 2) % (PD + 1), nxt = (k0 / 2 + PD) % (PD + 1);
+    if (k0 + 2 * PD < KCP) {
+      read_x(k0 + 2 * PD, xr[nxt]);
+      read_w(k0 + 2 * PD, wr[nxt]);
+    }
+#pragma unroll
+    for (int v = 0; v < NPW; ++v)
+#pragma unroll
+      for (int g = 0; g < NG; ++g)
+#pragma unroll
+        for (int u = 0; u < MPW; ++u) {
+          float x = xr[cur][u];
+          if constexpr (EPI != EPI_BWD && NG == 3) {
+            x = (g == 0) ? x : (g == 1 ? fmaxf(x, 0.f) : fminf(x, 0.f));
+          } else if constexpr (EPI != EPI_BWD && NG == 2) {
+            x = (g == 0) ? x : fmaxf(x, 0.f);
+          }
+          acc[g][u][v] = mfma32(wr[cur][g][v], x, acc[g][u][v]);
+        }
+  }
+}
+
 
 template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI>
 __global__ __launch_bounds__(kThreads) void conv3x3_kernel(ConvArgs a) {
@@ -129,258 +385,15 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(ConvArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[g][u][v][r] = 0.f;
 
-  // ---- staging: registers <- global (load), LDS <- registers (store).  The loads of chunk
-  //      c+1 are issued before the MFMA loop of chunk c, so their latency hides behind it. ----
-  const bool vec = (W & 3) == 0;                 // float4 rows (else per-element loads)
-  // dense halo: interior rows of TW/4 float4 + the two halo columns
-  constexpr int Q4 = TW / 4, DROWS = CIC * HY;
-  constexpr int DI = (DROWS * Q4 + kThreads - 1) / kThreads, DH = (DROWS * 2 + kThreads - 1) / kThreads;
-  // pool-sparse cells: interior rows of TW/8 float4 (4 cells) + the two halo cell columns
-  constexpr int CY = TH / 2 + 2, CX = TW / 2 + 2, Q8 = TW / 8 > 0 ? TW / 8 : 1, SROWS = CIC * CY;
-  constexpr int SI = (SROWS * Q8 + kThreads - 1) / kThreads, SH = (SROWS * 2 + kThreads - 1) / kThreads;
-  constexpr bool DENSE = AMODE == A_DENSE;
-  constexpr int NI = DENSE ? DI : SI, NH = DENSE ? DH : SH;
-  constexpr int NWV = NG * KCP * (COUT / 4), WIT = (NWV + kThreads - 1) / kThreads;
-  float4 st_i[NI];
-  uint32_t st_ia[DENSE ? 1 : NI];
-  float st_h[NH];
-  int st_ha[DENSE ? 1 : NH];
-  float4 st_w[WIT];
-  const int H2 = H >> 1, W2 = W >> 1;
-  const bool noload = (a.dbg & 1) != 0;
-  auto stage_load = [&](int c0) {
-    if constexpr (DENSE) {
-#pragma unroll
-      for (int it = 0; it < DI; ++it) {
-        const int i = tid + it * kThreads;
-        const int row = i / Q4, q = i % Q4;
-        const int ci = row / HY, hy = row % HY;
-        const int gy = ty0 - 1 + hy, gx = tx0 + 4 * q, c = c0 + ci;
-        const bool rok = i < DROWS * Q4 && gy >= 0 && gy < H && c < a.cin && !noload;
-        const float* src = a.in + (((size_t)bq * a.cin + c) * H + gy) * W + gx;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (rok) {
-          if (vec) {
-            if (gx < W) v = *reinterpret_cast<const float4*>(src);
-          } else {
-            v.x = gx < W ? src[0] : 0.f;
-            v.y = gx + 1 < W ? src[1] : 0.f;
-            v.z = gx + 2 < W ? src[2] : 0.f;
-            v.w = gx + 3 < W ? src[3] : 0.f;
-          }
-        }
-        st_i[it] = v;
-      }
-#pragma unroll
-      for (int it = 0; it < DH; ++it) {
-        const int i = tid + it * kThreads;
-        const int row = i >> 1, side = i & 1;
-        const int ci = row / HY, hy = row % HY;
-        const int gy = ty0 - 1 + hy, gx = side ? tx0 + TW : tx0 - 1, c = c0 + ci;
-        const bool ok = i < DROWS * 2 && gy >= 0 && gy < H && gx >= 0 && gx < W && c < a.cin && !noload;
-        st_h[it] = ok ? a.in[(((size_t)bq * a.cin + c) * H + gy) * W + gx] : 0.f;
-      }
-    } else {
-      const int qy0 = (ty0 >> 1) - 1, qx0 = (tx0 >> 1) - 1;
-#pragma unroll
-      for (int it = 0; it < SI; ++it) {
-        const int i = tid + it * kThreads;
-        const int row = i / Q8, q = i % Q8;
-        const int ci = row / CY, ry = row % CY;
-        const int cy = qy0 + ry, cx = qx0 + 1 + 4 * q, c = c0 + ci;
-        const bool rok = i < SROWS * Q8 && 4 * q < TW / 2 && cy >= 0 && cy < H2 && c < a.cin && !noload;
-        const size_t o = (((size_t)bq * a.cin + c) * H2 + cy) * W2 + cx;
-        const size_t oa = (((size_t)bs * a.cin + c) * H2 + cy) * W2 + cx;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        uint32_t am = 0x04040404u;
-        if (rok) {
-          if ((W2 & 3) == 0) {
-            if (cx < W2) {
-              v = *reinterpret_cast<const float4*>(a.in + o);
-              am = *reinterpret_cast<const uint32_t*>(a.in_amax + oa);
-            }
-          } else {
-            float vv[4];
-            uint32_t aa = 0;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const bool eok = cx + e < W2 && 4 * q + e < TW / 2;
-              vv[e] = eok ? a.in[o + e] : 0.f;
-              aa |= (eok ? (uint32_t)a.in_amax[oa + e] : 4u) << (8 * e);
-            }
-            v = make_float4(vv[0], vv[1], vv[2], vv[3]);
-            am = aa;
-          }
-        }
-        st_i[it] = v;
-        st_ia[it] = am;
-      }
-#pragma unroll
-      for (int it = 0; it < SH; ++it) {
-        const int i = tid + it * kThreads;
-        const int row = i >> 1, side = i & 1;
-        const int ci = row / CY, ry = row % CY;
-        const int cy = qy0 + ry, cx = side ? qx0 + CX - 1 : qx0, c = c0 + ci;
-        const bool ok = i < SROWS * 2 && cy >= 0 && cy < H2 && cx >= 0 && cx < W2 && c < a.cin && !noload;
-        st_h[it] = ok ? a.in[(((size_t)bq * a.cin + c) * H2 + cy) * W2 + cx] : 0.f;
-        st_ha[it] = ok ? (int)a.in_amax[(((size_t)bs * a.cin + c) * H2 + cy) * W2 + cx] : 4;
-      }
-    }
-    // weights: rows [c0*9, c0*9 + KC) of every set, contiguous (k = ci*9 + tap)
-#pragma unroll
-    for (int it = 0; it < WIT; ++it) {
-      const int idx = tid + it * kThreads;
-      const int g = idx / (KCP * (COUT / 4)), rem = idx % (KCP * (COUT / 4));
-      const int k = rem / (COUT / 4), c4 = (rem % (COUT / 4)) * 4;
-      st_w[it] = (idx < NWV && k < KC)
-                     ? *reinterpret_cast<const float4*>(a.wts + ((size_t)g * 9 * CIN + c0 * 9 + k) * COUT + c4)
-                     : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  };
-  // one pool cell -> its 2x2 pixels at halo rows 2ry-1, 2ry and LDS columns 2rx-1+XO, 2rx+XO
-  auto put_cell = [&](int ci, int ry, int rx, float v, int sb) {
-    float* d = halo + ci * PLANE + (2 * ry - 1) * RS + 2 * rx - 1 + XO;
-    if (ry > 0)
-      *reinterpret_cast<float2*>(d) = make_float2(sb == 0 ? v : 0.f, sb == 1 ? v : 0.f);
-    if (ry < CY - 1)
-      *reinterpret_cast<float2*>(d + RS) = make_float2(sb == 2 ? v : 0.f, sb == 3 ? v : 0.f);
-  };
-  auto stage_store = [&]() {
-    if constexpr (DENSE) {
-#pragma unroll
-      for (int it = 0; it < DI; ++it) {
-        const int i = tid + it * kThreads;
-        if (i < DROWS * Q4) {
-          const int row = i / Q4, q = i % Q4;
-          const int ci = row / HY, hy = row % HY;
-          *reinterpret_cast<float4*>(halo + ci * PLANE + hy * RS + 1 + XO + 4 * q) = st_i[it];
-        }
-      }
-#pragma unroll
-      for (int it = 0; it < DH; ++it) {
-        const int i = tid + it * kThreads;
-        if (i < DROWS * 2) {
-          const int row = i >> 1, side = i & 1;
-          const int ci = row / HY, hy = row % HY;
-          halo[ci * PLANE + hy * RS + (side ? HX - 1 : 0) + XO] = st_h[it];
-        }
-      }
-    } else {
-#pragma unroll
-      for (int it = 0; it < SI; ++it) {
-        const int i = tid + it * kThreads;
-        const int q = i % Q8;
-        if (i < SROWS * Q8 && 4 * q < TW / 2) {
-          const int row = i / Q8;
-          const int ci = row / CY, ry = row % CY;
-          const float vv[4] = {st_i[it].x, st_i[it].y, st_i[it].z, st_i[it].w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (4 * q + e < TW / 2) put_cell(ci, ry, 1 + 4 * q + e, vv[e], (int)((st_ia[it] >> (8 * e)) & 0xffu));
-        }
-      }
-#pragma unroll
-      for (int it = 0; it < SH; ++it) {
-        const int i = tid + it * kThreads;
-        if (i < SROWS * 2) {
-          const int row = i >> 1, side = i & 1;
-          put_cell(row / CY, row % CY, side ? CX - 1 : 0, st_h[it], st_ha[it]);
-        }
-      }
-    }
-#pragma unroll
-    for (int it = 0; it < WIT; ++it) {
-      const int idx = tid + it * kThreads;
-      if (idx < NWV) *reinterpret_cast<float4*>(wl + (size_t)idx * 4) = st_w[it];
-    }
-  };
-
-  // BWD epilogue inputs of the first n-tile pass (x, den), prefetched behind the last chunk
-  constexpr int V4E = (TCH_OF(Cfg) * TH * TW / 4 + kThreads - 1) / kThreads;
-  constexpr bool EPF = false && EPI == EPI_BWD;
-  float4 ex[EPF ? V4E : 1], ed[EPF ? V4E : 1];
-  auto epi_prefetch = [&]() {
-    if constexpr (EPF) {
-#pragma unroll
-      for (int it = 0; it < V4E; ++it) {
-        const int i = tid + it * kThreads;
-        const int cl = i / (TH * TW / 4), rem = i % (TH * TW / 4);
-        const int py = rem / (TW / 4), px = (rem % (TW / 4)) * 4;
-        const int co = ((cl >> 5) * NPW) * 32 + (cl & 31);
-        const bool ok = i < TCH_OF(Cfg) * TH * TW / 4 && co < a.cout && ty0 + py < H && tx0 + px < W;
-        const size_t os = (((size_t)bs * a.cout + co) * H + ty0 + py) * W + tx0 + px;
-        ex[it] = (ok && (a.xmode != XM_NONE || a.post != POST_NONE)) ? *reinterpret_cast<const float4*>(a.x + os)
-                                                                     : make_float4(0.f, 0.f, 0.f, 0.f);
-        ed[it] = (ok && a.post == POST_DIV) ? *reinterpret_cast<const float4*>(a.den + os)
-                                            : make_float4(1.f, 1.f, 1.f, 1.f);
-      }
-    }
-  };
-
-  stage_load(0);
+  Stager<Cfg> stg;
+  stg.load(a, 0, tid, ty0, tx0, bq, bs);
   for (int chunk = 0; chunk < Cfg::NCHUNK; ++chunk) {
     __syncthreads();
-    stage_store();
+    stg.store(halo, wl, tid);
     __syncthreads();
-    if (chunk + 1 < Cfg::NCHUNK) stage_load((chunk + 1) * CIC);
-    else epi_prefetch();
+    if (chunk + 1 < Cfg::NCHUNK) stg.load(a, (chunk + 1) * CIC, tid, ty0, tx0, bq, bs);
     if (!active || (a.dbg & 4)) continue;
-    // ---- MFMA over the chunk.  k = k0 + h (h = lane half) with k = ci*9 + tap: the halo
-    //      offset pattern repeats every 9 k-steps (two channels), so the 9 per-lane bases
-    //      (one per step of the period, per m-tile) are computed once and every LDS read in
-    //      the fully unrolled loop is base register + immediate. ----
-    constexpr int NSTEP = KCP / 2;
-    // operands of step k0 are read one step ahead (explicit software pipeline)
-    auto read_x = [&](int k0, float (&xv)[MPW]) {
-      const int jj = (k0 / 2) % 9, mm = (k0 / 2) / 9;
-      const int kk = 2 * jj + h;
-      const int off = (kk / 9) * PLANE + ((kk % 9) / 3) * RS + (kk % 3) + mm * 2 * PLANE;
-#pragma unroll
-      for (int u = 0; u < MPW; ++u) {
-        if constexpr (KC % 2 == 0) xv[u] = halo[off + pix_off[u]];
-        else xv[u] = (k0 + h < KC) ? halo[off + pix_off[u]] : 0.f;
-      }
-    };
-    auto read_w = [&](int k0, float (&wv)[NG][NPW]) {
-#pragma unroll
-      for (int v = 0; v < NPW; ++v)
-#pragma unroll
-        for (int g = 0; g < NG; ++g) wv[g][v] = wl[((size_t)g * KCP + k0 + h) * COUT + (wn * NPW + v) * 32 + (lane & 31)];
-    };
-    float xa[MPW], wa[NG][NPW];
-    read_x(0, xa);
-    read_w(0, wa);
-#pragma unroll
-    for (int k0 = 0; k0 < KCP; k0 += 2) {
-      float xb[MPW], wb[NG][NPW];
-      if (k0 + 2 < KCP) {
-        read_x(k0 + 2, xb);
-        read_w(k0 + 2, wb);
-      }
-#pragma unroll
-      for (int v = 0; v < NPW; ++v)
-#pragma unroll
-        for (int g = 0; g < NG; ++g)
-#pragma unroll
-          for (int u = 0; u < MPW; ++u) {
-            float x = xa[u];
-            if constexpr (EPI != EPI_BWD && NG == 3) {
-              x = (g == 0) ? x : (g == 1 ? fmaxf(x, 0.f) : fminf(x, 0.f));
-            } else if constexpr (EPI != EPI_BWD && NG == 2) {
-              x = (g == 0) ? x : fmaxf(x, 0.f);
-            }
-            acc[g][u][v] = mfma32(wa[g][v], x, acc[g][u][v]);
-          }
-      if (k0 + 2 < KCP) {
-#pragma unroll
-        for (int u = 0; u < MPW; ++u) xa[u] = xb[u];
-#pragma unroll
-        for (int v = 0; v < NPW; ++v)
-#pragma unroll
-          for (int g = 0; g < NG; ++g) wa[g][v] = wb[g][v];
-      }
-    }
-    (void)NSTEP;
+    mfma_chunk<Cfg>(halo, wl, pix_off, lane, wn, acc);
   }
 
   // ---- epilogue, staged through LDS so global I/O is coalesced float4 rows ----
@@ -557,8 +570,7 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(ConvArgs a) {
             if (a.xmode == XM_NONE || (a.dbg & 2)) {
               Rk[it] = t;
             } else {
-              const float4 x = (EPF && v == 0) ? ex[it]
-                                        : *reinterpret_cast<const float4*>(a.x + (((size_t)bs * a.cout + co) * H + ty0 + py) * W + tx0 + px);
+              const float4 x = *reinterpret_cast<const float4*>(a.x + (((size_t)bs * a.cout + co) * H + ty0 + py) * W + tx0 + px);
               if (a.xmode == XM_MUL) {
                 Rk[it] = make_float4(x.x * t.x, x.y * t.y, x.z * t.z, x.w * t.w);
               } else {
@@ -581,8 +593,7 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(ConvArgs a) {
               const int co = gch(cl, v);
               if (co < a.cout && ty0 + py < H && tx0 + px < W) {
                 const float4 t = *reinterpret_cast<const float4*>(T + (cl * TH + py) * TWP + px);
-                const float4 x = (EPF && v == 0) ? ex[it]
-                                          : *reinterpret_cast<const float4*>(a.x + (((size_t)bs * a.cout + co) * H + ty0 + py) * W + tx0 + px);
+                const float4 x = *reinterpret_cast<const float4*>(a.x + (((size_t)bs * a.cout + co) * H + ty0 + py) * W + tx0 + px);
                 Rk[it].x += fminf(x.x, 0.f) * t.x;
                 Rk[it].y += fminf(x.y, 0.f) * t.y;
                 Rk[it].z += fminf(x.z, 0.f) * t.z;
@@ -608,14 +619,14 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(ConvArgs a) {
               continue;
             }
             if (a.post == POST_DIV) {
-              const float4 x = (EPF && v == 0) ? ex[it] : *reinterpret_cast<const float4*>(a.x + os);
-              const float4 d = (EPF && v == 0) ? ed[it] : *reinterpret_cast<const float4*>(a.den + os);
+              const float4 x = *reinterpret_cast<const float4*>(a.x + os);
+              const float4 d = *reinterpret_cast<const float4*>(a.den + os);
               R.x = (x.x > 0.f) ? R.x / stab(d.x, a.eps) : 0.f;
               R.y = (x.y > 0.f) ? R.y / stab(d.y, a.eps) : 0.f;
               R.z = (x.z > 0.f) ? R.z / stab(d.z, a.eps) : 0.f;
               R.w = (x.w > 0.f) ? R.w / stab(d.w, a.eps) : 0.f;
             } else if (a.post == POST_MASK) {
-              const float4 x = (EPF && v == 0) ? ex[it] : *reinterpret_cast<const float4*>(a.x + os);
+              const float4 x = *reinterpret_cast<const float4*>(a.x + os);
               R.x = (x.x > 0.f) ? R.x : 0.f;
               R.y = (x.y > 0.f) ? R.y : 0.f;
               R.z = (x.z > 0.f) ? R.z : 0.f;
@@ -668,5 +679,6 @@ struct Table {
   const Entry* entries;
   int n;
 };
+
 
 }  // namespace drsa_conv

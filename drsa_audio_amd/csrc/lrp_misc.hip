@@ -393,7 +393,7 @@ __global__ __launch_bounds__(256) void first_layer_bwd_kernel(const float* __res
 // 6 x 6 patch per channel and runs 9 fmas per pixel in the dense chain order
 // (channel, dy, dx) — the chain of the dense kernel above and of oracle/lrp_exact.c (the
 // zero terms included: fma(0, w, acc) == acc).
-constexpr int FQ_Y = 16, FQ_X = 64, FQ_C = 4;
+constexpr int FQ_Y = 16, FQ_X = 64, FQ_C = 2;
 constexpr int FQ_RY = FQ_Y + 2, FQ_RX = FQ_X + 2;            // cells incl. halo
 constexpr int FQ_PY = 2 * FQ_RY, FQ_PX = 2 * FQ_RX + 4;      // pixel image (row pad 4)
 constexpr int FQ_KR = (FQ_RY + 3) / 4;                       // row passes of 4 waves

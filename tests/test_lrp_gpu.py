@@ -159,3 +159,21 @@ def test_bench_size_properties(net):
     assert torch.isfinite(a["subspace_heatmaps"]).all()
     rel = a["subspace_relevances"]
     assert bool((rel[:, :-1] >= rel[:, 1:]).all())
+    # batch independence: the B=64 results of the first samples equal a B=3 run bit for bit
+    # (the persistent kernels walk many tiles per workgroup at B=64, one at B=3)
+    hg3 = HeatmapGenerator(_gpu_model(net), u64(), LRP_NAME_MAP_GTZAN, "jazz", num_concepts=4, layer_idx=7)
+    hg3.generate_subspace_heatmaps(x[:3], to_host=False)
+    for k, v in hg3.info_device.items():
+        assert torch.equal(v, a[k][:3]), k
+
+
+def test_large_batch_bit_exact_vs_oracle_sample(net):
+    """B=96: two samples (first and last) of a large batch vs the exact oracle run on them alone."""
+    x = logmel(96, seed=41)
+    hg = HeatmapGenerator(_gpu_model(net), u64(), LRP_NAME_MAP_GTZAN, "metal", num_concepts=4, layer_idx=7)
+    hg.generate_subspace_heatmaps(x.to(DEV))
+    pm = ProjectionModel(net, 7, u64(), 4).eval()
+    idx = [0, 95]
+    ref = lrp_ref.subspace_heatmaps(pm, spec(LRP_NAME_MAP_GTZAN), 4, x[idx], class_idx=1, mode="exact")
+    for k in ("standard_heatmaps", "subspace_heatmaps", "subspace_relevances", "mask"):
+        assert np.array_equal(hg.info[k][idx], ref[k]), k
