@@ -152,6 +152,38 @@ def drsa_bench(device, steps=200):
             "objective_max_rel_err_vs_oracle_10_steps": rel, "objective_final": float(traj[-1])}
 
 
+def frontend_bench(device, n_songs=64, iters=20):
+    """R17 log-mel front end: n_songs synthetic 29.5 s songs x 8 chunks -> [512, 1, 128, 128] in one
+    launch (get_slice + peak_normalizer + STFT + mel + log10 + clamp).  HBM roofline: the chunk's
+    48 000 samples read once + the 128x128 log-mel written once = 257 KB per chunk."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import logmel_ref
+    from drsa_audio_amd.utils.dataloading import Loader
+    songs = torch.from_numpy(logmel_ref.synthetic_songs(n_songs, seed=3)).to(device)
+    ld = Loader("gtzan", device=device)
+    out = ld.load_songs(songs)
+    ref = logmel_ref.load_songs(songs[:1].cpu().numpy(), "gtzan", mode="f64")
+    err = float(np.abs(out[:8].cpu().numpy() - ref).max())
+    s = torch.cuda.current_stream(device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(3):
+        ld.load_songs(songs)
+    e0.record(s)
+    for _ in range(iters):
+        ld.load_songs(songs)
+    e1.record(s)
+    torch.cuda.synchronize(device)
+    ms = e0.elapsed_time(e1) / iters
+    chunks = n_songs * 8
+    byts = chunks * 4.0 * (48000 + 128 * 128)
+    gbs = byts / (ms * 1e-3) / 1e9
+    return {"config": f"GTZAN front end: {n_songs} songs x 8 chunks of 3 s @16 kHz -> 128x128 log-mel",
+            "chunks_per_s": chunks / (ms * 1e-3), "ms_per_launch": ms, "algorithmic_bytes_per_launch": byts,
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs / HBM_PEAK_GBS},
+            "max_abs_logmel_err_vs_f64_oracle_song0": err}
+
+
 def drsa_sharded_bench(device, world, rank, steps=100):
     """C4-style row-sharded DRSA: 20000 rows per rank (weak), d=64, K=4; one RCCL all-reduce of the
     [d*d+K] partial per step (drsa_audio_amd/xai/drsa/distributed.py)."""
@@ -294,6 +326,7 @@ def main():
     drsa = None
     if not args.no_drsa and rank == 0:
         drsa = drsa_bench(device)
+    frontend = frontend_bench(device) if rank == 0 else None
     drsa_sharded = None
     if not args.no_drsa and world > 1:
         drsa_sharded = drsa_sharded_bench(device, world, rank)
@@ -327,7 +360,7 @@ def main():
             "kernels": kernels,
             "secondary": {"standard_lrp_c2_bs64_samples_per_s": c2 * world,
                           "explained_samples_per_s_bs64": bs64 * world, "drsa": drsa,
-                          "drsa_sharded": drsa_sharded},
+                          "drsa_sharded": drsa_sharded, "logmel_frontend": frontend},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -1,0 +1,342 @@
+// Log-mel front end: get_slice -> peak_normalizer -> |STFT| -> HTK mel
+// -> log10(+eps) -> clamp -> frames frame0..frame0+width-1, fused into one launch.
+//
+// Reference: cxai/utils/dataloading.py:62-74 (torchaudio Spectrogram(n_fft, hop, power=None) +
+// MelScale), :138-176 (transform_wav); cxai/utils/sound.py:8-44 (get_slice), :67-70
+// (peak_normalizer).
+//
+// One workgroup per audio chunk, 8 waves.  The chunk's samples stream through LDS in blocks of
+// 8 frames (one frame per wave, reflect padding resolved on the load); each wave runs the
+// n_fft-point real FFT as an n_fft/2-point complex Stockham FFT (radices 4/2/3/5) in its own
+// LDS ping-pong buffers, the real-input split, |X|, and the sparse triangular mel filterbank
+// (each filter is a contiguous band of FFT bins).  Mel columns collect in LDS so the
+// [n_mels][width] output leaves as coalesced rows.  The STFT and the filterbank are
+// linear and |.| is positively homogeneous, so the per-chunk peak division is applied to the
+// mel energies at the end: one read of the waveform (HBM roofline: 4*(L + n_mels*width) B per
+// chunk).
+#include "common.h"
+#include "drsa_amd.h"
+
+namespace {
+
+constexpr int LM_WAVES = 8;
+constexpr int LM_THREADS = LM_WAVES * 64;
+constexpr int LM_MAX_STAGES = 8;
+
+struct LogmelArgs {
+  const float* wav;
+  int64_t song_stride;       // floats between songs
+  int64_t chunk_hop;         // floats between consecutive chunks of a song
+  int chunks_per_song;
+  int n_chunks;
+  int L;                     // chunk length in samples
+  int nfft, hop, n_mels, width, frame0;
+  int n_stages;
+  int radix[LM_MAX_STAGES];
+  const float* window;       // [nfft]
+  const int* band_lo;        // [n_mels] first FFT bin of filter m
+  const int* band_n;         // [n_mels] bins in filter m
+  const int* band_off;       // [n_mels] offset of filter m in band_w
+  const float* band_w;       // [nnz]
+  int nnz;
+  int peak_norm, do_clamp;
+  float clamp_min, log_eps;
+  float* out;                // [n_chunks][n_mels][width]
+  // LDS carve (floats), computed on the host
+  int o_tw, o_ptw, o_win, o_blo, o_bn, o_boff, o_bw, o_samp, o_fft, o_mel, o_red, smem_floats;
+};
+
+struct cf {
+  float x, y;
+};
+__device__ __forceinline__ cf cadd(cf a, cf b) { return {a.x + b.x, a.y + b.y}; }
+__device__ __forceinline__ cf csub(cf a, cf b) { return {a.x - b.x, a.y - b.y}; }
+__device__ __forceinline__ cf cmul(cf a, cf b) { return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
+__device__ __forceinline__ cf cscale(cf a, float s) { return {a.x * s, a.y * s}; }
+__device__ __forceinline__ cf mul_negi(cf a) { return {a.y, -a.x}; }   // -i * a
+
+// Wave-local LDS hand-off: all lanes' LDS writes are visible to the wave's later reads.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// forward DFT butterflies (sign -i), in place on v[0..R)
+__device__ __forceinline__ void bfly2(cf* v) {
+  cf a = v[0], b = v[1];
+  v[0] = cadd(a, b);
+  v[1] = csub(a, b);
+}
+__device__ __forceinline__ void bfly4(cf* v) {
+  cf t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]);
+  cf t2 = cadd(v[1], v[3]), t3 = mul_negi(csub(v[1], v[3]));
+  v[0] = cadd(t0, t2);
+  v[2] = csub(t0, t2);
+  v[1] = cadd(t1, t3);
+  v[3] = csub(t1, t3);
+}
+__device__ __forceinline__ void bfly3(cf* v) {
+  const float s = 0.86602540378443864676f;
+  cf sm = cadd(v[1], v[2]);
+  cf y0 = cadd(v[0], sm);
+  cf t = csub(v[0], cscale(sm, 0.5f));
+  cf u = mul_negi(cscale(csub(v[1], v[2]), s));
+  v[0] = y0;
+  v[1] = cadd(t, u);
+  v[2] = csub(t, u);
+}
+__device__ __forceinline__ void bfly5(cf* v) {
+  const float c1 = 0.30901699437494742410f, c2 = -0.80901699437494742410f;
+  const float s1 = 0.95105651629515357212f, s2 = 0.58778525229247312917f;
+  cf b1 = cadd(v[1], v[4]), b2 = cadd(v[2], v[3]);
+  cf d1 = csub(v[1], v[4]), d2 = csub(v[2], v[3]);
+  cf a0 = v[0];
+  cf r1 = cadd(a0, cadd(cscale(b1, c1), cscale(b2, c2)));
+  cf r2 = cadd(a0, cadd(cscale(b1, c2), cscale(b2, c1)));
+  cf q1 = mul_negi(cadd(cscale(d1, s1), cscale(d2, s2)));   // -i (s1 d1 + s2 d2)
+  cf q2 = mul_negi(csub(cscale(d1, s2), cscale(d2, s1)));   // -i (s2 d1 - s1 d2)
+  v[0] = cadd(a0, cadd(b1, b2));
+  v[1] = cadd(r1, q1);
+  v[4] = csub(r1, q1);
+  v[2] = cadd(r2, q2);
+  v[3] = csub(r2, q2);
+}
+
+// One Stockham pass of radix R over M points (Govindaraju et al. 2008 indexing):
+//   v[r] = in[j + r*M/R] * W_M^{r*k*M/(Ns*R)}, k = j % Ns;  out[(j/Ns)*Ns*R + k + r*Ns] = DFT_R(v)[r]
+template <int R>
+__device__ __forceinline__ void stockham_pass(const cf* __restrict__ in, cf* __restrict__ out, const cf* tw, int M,
+                                              int Ns, int lane) {
+  const int MR = M / R;
+  const int tstep = M / (Ns * R);
+  for (int j = lane; j < MR; j += 64) {
+    const int k = j % Ns;
+    cf v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = in[j + r * MR];
+    if (Ns > 1) {
+#pragma unroll
+      for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw[r * k * tstep]);
+    }
+    if constexpr (R == 2) bfly2(v);
+    if constexpr (R == 3) bfly3(v);
+    if constexpr (R == 4) bfly4(v);
+    if constexpr (R == 5) bfly5(v);
+    const int base = (j / Ns) * Ns * R + k;
+#pragma unroll
+    for (int r = 0; r < R; ++r) out[base + r * Ns] = v[r];
+  }
+}
+
+__global__ __launch_bounds__(LM_THREADS) void logmel_kernel(LogmelArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int chunk = blockIdx.x;
+  const int M = a.nfft >> 1, half = a.nfft >> 1;
+  const float* x = a.wav + (int64_t)(chunk / a.chunks_per_song) * a.song_stride +
+                   (int64_t)(chunk % a.chunks_per_song) * a.chunk_hop;
+  cf* tw = reinterpret_cast<cf*>(sm + a.o_tw);      // W_M^j, j < M
+  cf* ptw = reinterpret_cast<cf*>(sm + a.o_ptw);    // W_N^k, k <= M
+  float* win = sm + a.o_win;
+  int* blo = reinterpret_cast<int*>(sm + a.o_blo);
+  int* bn = reinterpret_cast<int*>(sm + a.o_bn);
+  int* boff = reinterpret_cast<int*>(sm + a.o_boff);
+  float* bw = sm + a.o_bw;
+  float* samp = sm + a.o_samp;
+  cf* fa = reinterpret_cast<cf*>(sm + a.o_fft) + (size_t)w * 2 * M;
+  cf* fb = fa + M;
+  float* mel = sm + a.o_mel;
+  float* red = sm + a.o_red;
+
+  // ---- tables (twiddles from exact fp64 angles rounded once to fp32) ----
+  for (int j = tid; j < M; j += LM_THREADS) {
+    double s, c;
+    sincospi(2.0 * (double)j / (double)M, &s, &c);
+    tw[j] = {(float)c, (float)-s};
+  }
+  for (int k = tid; k <= M; k += LM_THREADS) {
+    double s, c;
+    sincospi((double)k / (double)M, &s, &c);          // 2*pi*k/N, N = 2M
+    ptw[k] = {(float)c, (float)-s};
+  }
+  for (int i = tid; i < a.nfft; i += LM_THREADS) win[i] = a.window[i];
+  for (int m = tid; m < a.n_mels; m += LM_THREADS) {
+    blo[m] = a.band_lo[m];
+    bn[m] = a.band_n[m];
+    boff[m] = a.band_off[m];
+  }
+  for (int i = tid; i < a.nnz; i += LM_THREADS) bw[i] = a.band_w[i];
+
+  float pk = 0.f;   // running max |x| over this thread's loads
+  const int nblk_samp = (LM_WAVES - 1) * a.hop + a.nfft;
+  for (int tb = 0; tb < a.width; tb += LM_WAVES) {
+    const int nw = min(LM_WAVES, a.width - tb);
+    const int base = (a.frame0 + tb) * a.hop - half;
+    const int cnt = (nw - 1) * a.hop + a.nfft;
+    __syncthreads();   // previous block's frames are done with samp (and the tables are ready)
+    for (int i = tid; i < cnt; i += LM_THREADS) {
+      int j = base + i;
+      j = j < 0 ? -j : j;                                  // reflect (torch pad_mode="reflect")
+      j = j >= a.L ? 2 * (a.L - 1) - j : j;
+      const float v = x[j];
+      samp[i] = v;
+      pk = fmaxf(pk, fabsf(v));
+    }
+    __syncthreads();
+    if (w < nw) {
+      const float* fr = samp + w * a.hop;
+      // pack the windowed real frame as M complex points z[n] = x[2n] + i x[2n+1]
+      for (int n = lane; n < M; n += 64) fa[n] = {fr[2 * n] * win[2 * n], fr[2 * n + 1] * win[2 * n + 1]};
+      wave_lds_sync();
+      cf* src = fa;
+      cf* dst = fb;
+      int Ns = 1;
+      for (int s = 0; s < a.n_stages; ++s) {
+        const int R = a.radix[s];
+        if (R == 4) stockham_pass<4>(src, dst, tw, M, Ns, lane);
+        else if (R == 5) stockham_pass<5>(src, dst, tw, M, Ns, lane);
+        else if (R == 3) stockham_pass<3>(src, dst, tw, M, Ns, lane);
+        else stockham_pass<2>(src, dst, tw, M, Ns, lane);
+        wave_lds_sync();
+        Ns *= R;
+        cf* t = src;
+        src = dst;
+        dst = t;
+      }
+      // real-input split: X[k] = E[k] + W_N^k O[k], E = (Z_k + conj Z_{M-k})/2, O = (Z_k - conj Z_{M-k})/(2i)
+      float* mag = reinterpret_cast<float*>(dst);
+      for (int k = lane; k <= M; k += 64) {
+        const cf zk = src[k == M ? 0 : k];
+        const cf zr = src[k == 0 ? 0 : M - k];
+        const cf zc = {zr.x, -zr.y};
+        const cf e = cscale(cadd(zk, zc), 0.5f);
+        const cf d = csub(zk, zc);
+        const cf o = {0.5f * d.y, -0.5f * d.x};
+        const cf X = cadd(e, cmul(ptw[k], o));
+        mag[k] = sqrtf(X.x * X.x + X.y * X.y);
+      }
+      wave_lds_sync();
+      for (int m = lane; m < a.n_mels; m += 64) {
+        const float* wm = bw + boff[m];
+        const float* mg = mag + blo[m];
+        float acc = 0.f;
+        for (int q = 0; q < bn[m]; ++q) acc += wm[q] * mg[q];
+        mel[m * a.width + tb + w] = acc;
+      }
+    }
+  }
+  // samples of the chunk no frame touched still count for the peak
+  {
+    const int c0 = max(0, a.frame0 * a.hop - half);
+    const int c1 = min(a.L, (a.frame0 + a.width - 1) * a.hop - half + a.nfft);
+    for (int i = tid; i < c0; i += LM_THREADS) pk = fmaxf(pk, fabsf(x[i]));
+    for (int i = c1 + tid; i < a.L; i += LM_THREADS) pk = fmaxf(pk, fabsf(x[i]));
+  }
+  for (int o = 32; o > 0; o >>= 1) pk = fmaxf(pk, shfl_xor(pk, o));
+  if (lane == 0) red[w] = pk;
+  __syncthreads();
+  float p = red[0];
+  for (int i = 1; i < LM_WAVES; ++i) p = fmaxf(p, red[i]);
+  const float inv_scale = a.peak_norm ? p : 1.f;
+  float* o = a.out + (size_t)chunk * a.n_mels * a.width;
+  const int total = a.n_mels * a.width;
+  for (int i = tid; i < total; i += LM_THREADS) {
+    float v = log10f(mel[i] / inv_scale + a.log_eps);
+    if (a.do_clamp) v = (v < a.clamp_min) ? a.clamp_min : v;   // torch.clamp keeps NaN (silent chunk: 0/0)
+    o[i] = v;
+  }
+}
+
+int factor_radices(int M, int* r) {
+  int n = 0;
+  while (M % 4 == 0 && n < LM_MAX_STAGES) { r[n++] = 4; M /= 4; }
+  while (M % 2 == 0 && n < LM_MAX_STAGES) { r[n++] = 2; M /= 2; }
+  while (M % 3 == 0 && n < LM_MAX_STAGES) { r[n++] = 3; M /= 3; }
+  while (M % 5 == 0 && n < LM_MAX_STAGES) { r[n++] = 5; M /= 5; }
+  return M == 1 ? n : -1;
+}
+
+}  // namespace
+
+extern "C" int drsa_amd_logmel_smem_bytes(int n_fft, int hop, int n_mels, int width, int band_nnz) {
+  const int M = n_fft / 2;
+  int off = 0;
+  auto take = [&](int n) { int o = off; off += (n + 3) & ~3; return o; };
+  take(2 * M);
+  take(2 * (M + 1));
+  take(n_fft);
+  take(n_mels);
+  take(n_mels);
+  take(n_mels);
+  take(band_nnz);
+  take((LM_WAVES - 1) * hop + n_fft);
+  take(LM_WAVES * 4 * M);
+  take(n_mels * width);
+  take(LM_WAVES);
+  return off * 4;
+}
+
+extern "C" int drsa_amd_logmel(const float* wav, int64_t n_songs, int64_t song_stride, int chunks_per_song,
+                               int64_t chunk_hop, int chunk_len, int n_fft, int hop, int n_mels, int width,
+                               int frame0, const float* window, const int* band_lo, const int* band_n,
+                               const int* band_off, const float* band_w, int band_nnz, int peak_norm, int clamp,
+                               float clamp_min, float log_eps, float* out, void* stream) {
+  DRSA_REQUIRE(wav && window && band_lo && band_n && band_off && band_w && out, "logmel: null pointer");
+  DRSA_REQUIRE(n_songs >= 0 && chunks_per_song >= 1, "logmel: bad chunk counts");
+  DRSA_REQUIRE(n_fft >= 8 && n_fft % 2 == 0, "logmel: n_fft must be even (got %d)", n_fft);
+  DRSA_REQUIRE(hop >= 1 && n_mels >= 1 && width >= 1 && frame0 >= 0, "logmel: bad hop/n_mels/width/frame0");
+  DRSA_REQUIRE(chunk_len > n_fft / 2, "logmel: reflect padding needs chunk_len > n_fft/2");
+  DRSA_REQUIRE(frame0 + width <= 1 + chunk_len / hop, "logmel: frames %d..%d exceed the %d STFT frames", frame0,
+               frame0 + width - 1, 1 + chunk_len / hop);
+  DRSA_REQUIRE(band_nnz >= 0, "logmel: band_nnz < 0");
+  LogmelArgs a{};
+  a.n_stages = factor_radices(n_fft / 2, a.radix);
+  DRSA_REQUIRE(a.n_stages > 0, "logmel: n_fft/2 = %d must factor into 2, 3, 5", n_fft / 2);
+  if (n_songs == 0) return DRSA_OK;
+  const int64_t n_chunks = n_songs * chunks_per_song;
+  DRSA_REQUIRE(n_chunks < (1 << 30), "logmel: too many chunks");
+  a.wav = wav;
+  a.song_stride = song_stride;
+  a.chunk_hop = chunk_hop;
+  a.chunks_per_song = chunks_per_song;
+  a.n_chunks = (int)n_chunks;
+  a.L = chunk_len;
+  a.nfft = n_fft;
+  a.hop = hop;
+  a.n_mels = n_mels;
+  a.width = width;
+  a.frame0 = frame0;
+  a.window = window;
+  a.band_lo = band_lo;
+  a.band_n = band_n;
+  a.band_off = band_off;
+  a.band_w = band_w;
+  a.nnz = band_nnz;
+  a.peak_norm = peak_norm;
+  a.do_clamp = clamp;
+  a.clamp_min = clamp_min;
+  a.log_eps = log_eps;
+  a.out = out;
+  const int M = n_fft / 2;
+  int off = 0;
+  auto take = [&](int n) { int o = off; off += (n + 3) & ~3; return o; };
+  a.o_tw = take(2 * M);
+  a.o_ptw = take(2 * (M + 1));
+  a.o_win = take(n_fft);
+  a.o_blo = take(n_mels);
+  a.o_bn = take(n_mels);
+  a.o_boff = take(n_mels);
+  a.o_bw = take(band_nnz);
+  a.o_samp = take((LM_WAVES - 1) * hop + n_fft);
+  a.o_fft = take(LM_WAVES * 4 * M);
+  a.o_mel = take(n_mels * width);
+  a.o_red = take(LM_WAVES);
+  a.smem_floats = off;
+  const size_t smem = (size_t)off * 4;
+  DRSA_REQUIRE(smem <= 160 * 1024, "logmel: LDS footprint %zu B exceeds 160 KB (n_mels*width too large)", smem);
+  DRSA_HIP(hipFuncSetAttribute((const void*)logmel_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+  hipLaunchKernelGGL(logmel_kernel, dim3((unsigned)n_chunks), dim3(LM_THREADS), smem, (hipStream_t)stream, a);
+  DRSA_LAUNCH_CHECK();
+  return DRSA_OK;
+}

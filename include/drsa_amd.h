@@ -143,6 +143,27 @@ int drsa_amd_first_layer_den(const float* w2, const float* b2, float* den, int C
 int drsa_amd_heatmap_sort(const float* hm, int B, int K, int HW, float* std_out, float* std_rel, float* sub_out,
                           float* rel, int64_t* mask, void* stream);
 
+/* ------------------------------------------------------------------------- *
+ * Log-mel front end
+ * Replaces cxai/utils/dataloading.py:62-74 + :138-176 (Loader: torchaudio
+ * Spectrogram(n_fft, hop, power=None) -> MelScale(n_mels) -> log10(+log_eps) -> clamp ->
+ * frames [frame0, frame0+width)) fused with cxai/utils/sound.py:8-44 (get_slice chunking)
+ * and :67-70 (peak_normalizer).
+ *   wav: songs [n_songs] at stride song_stride floats; chunk c of a song starts at
+ *        c*chunk_hop and is chunk_len samples long (get_slice's unfold).
+ *   window: [n_fft] analysis window (torch.hann_window(n_fft), periodic).
+ *   band_*: the mel filterbank [n_fft/2+1, n_mels] in band form: filter m covers FFT bins
+ *        band_lo[m] .. band_lo[m]+band_n[m]-1 with weights band_w[band_off[m] ...].
+ *   peak_norm: divide each chunk by its max |x| (peak_normalizer).
+ *   out: [n_songs*chunks_per_song, n_mels, width] fp32.
+ * Needs n_fft/2 = 2^a 3^b 5^c; LDS footprint (drsa_amd_logmel_smem_bytes) <= 160 KB.
+ * ------------------------------------------------------------------------- */
+int drsa_amd_logmel_smem_bytes(int n_fft, int hop, int n_mels, int width, int band_nnz);
+int drsa_amd_logmel(const float* wav, int64_t n_songs, int64_t song_stride, int chunks_per_song, int64_t chunk_hop,
+                    int chunk_len, int n_fft, int hop, int n_mels, int width, int frame0, const float* window,
+                    const int* band_lo, const int* band_n, const int* band_off, const float* band_w, int band_nnz,
+                    int peak_norm, int clamp, float clamp_min, float log_eps, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,119 @@
+"""Log-mel HIP front end (csrc/logmel.hip) vs the CPU oracle (GPU).
+
+Tolerance (written here, floating point): |log-mel(GPU) - log-mel(oracle f64)| <= 1e-3 in
+log10 units (0.23 % in mel energy; the worst bins are the quiet ones, where any fp32 FFT's
+rounding noise relative to the frame's energy shows), and the linear-mel error relative to
+each chunk's maximum <= 2e-5.  torch.stft's own float32 restatement sits at the same distance
+from the f64 oracle (measured: 7.9e-5 vs ours 7.2e-5 on test 1; 2.1e-4 vs 3.7e-4 worst seen).
+Parity vs torchaudio itself is unpinned (not installed; no reference fixture).
+"""
+import numpy as np
+import pytest
+import torch
+
+import logmel_ref as L
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+TOL_LOG = 1e-3
+
+
+def _loader(case="gtzan", **kw):
+    from drsa_audio_amd.utils.dataloading import Loader
+    return Loader(case, device=DEV, **kw) if case else Loader(None, device=DEV, **kw)
+
+
+def test_gtzan_songs_fused_slice_peak_logmel():
+    songs = L.synthetic_songs(3, seed=11)
+    ref = L.load_songs(songs, "gtzan", mode="f64")
+    out = _loader().load_songs(torch.from_numpy(songs).to(DEV)).cpu().numpy()
+    assert out.shape == ref.shape == (24, 1, 128, 128)
+    err = np.abs(out - ref).max()
+    t32 = L.load_songs(songs, "gtzan", mode="torch32")
+    print("max |dlogmel| gpu vs f64:", err, " torch32 vs f64:", np.abs(t32 - ref).max())
+    assert err <= TOL_LOG
+
+
+def test_transform_wav_toy_matches_oracle():
+    rng = np.random.default_rng(3)
+    wav = L.peak_normalizer(rng.standard_normal((5, 16000)).astype(np.float32))
+    ref = L.transform_wav(wav.astype(np.float64), "toy", mode="f64")
+    out = _loader("toy").transform_wav(torch.from_numpy(wav).to(DEV)).cpu().numpy()
+    assert out.shape == (5, 1, 64, 64)
+    assert np.abs(out - ref).max() <= TOL_LOG
+
+
+def test_linear_mel_error_relative_to_chunk_max():
+    songs = L.synthetic_songs(2, seed=4)
+    ld = _loader()
+    w = L.peak_normalizer(L.get_slice(songs[:1].astype(np.float64), 3, 0, 8, 16000))
+    mel_ref = L.mel_spectrogram(w, 800, 360, 128, 16000)[..., 1:129].reshape(8, 128, 128)
+    out = ld.load_songs(torch.from_numpy(songs[:1]).to(DEV), peak_norm=True)
+    # no clamp: recover the linear mel from the log (all synthetic bins are far above 1e-7)
+    mel = 10.0 ** out.cpu().numpy().astype(np.float64).reshape(8, 128, 128) - 1e-7
+    rel = np.abs(mel - mel_ref) / mel_ref.max(axis=(1, 2), keepdims=True)
+    assert rel.max() <= 2e-5
+
+
+def test_right_reflect_edge_and_all_frames():
+    # frames 1..66 of a 16000-sample chunk with hop 240: the last frame reads past the end
+    ld = _loader(None, sample_rate=16000, n_fft=480, hop_length=240, n_mels=64, slice_length=0, width=66)
+    rng = np.random.default_rng(9)
+    wav = rng.uniform(-1, 1, (2, 16000)).astype(np.float32)
+    out = ld.transform_wav(torch.from_numpy(wav).to(DEV), clamp=False).cpu().numpy()
+    mel = L.mel_spectrogram(wav.astype(np.float64), 480, 240, 64, 16000)
+    ref = np.log10(mel + 1e-7)[..., 1:67].reshape(2, 1, 64, 66)
+    assert np.abs(out - ref).max() <= TOL_LOG
+
+
+def test_clamp_and_quiet_input():
+    t = np.arange(48000) / 16000
+    wav = (1e-3 * np.sin(2 * np.pi * 440 * t))[None].astype(np.float32)
+    ld = _loader()
+    out = ld.transform_wav(torch.from_numpy(wav).to(DEV)).cpu().numpy()
+    ref = L.transform_wav(wav.astype(np.float64), "gtzan", mode="f64")
+    assert (ref == -4).mean() > 0.2                  # the clamp is exercised
+    assert np.array_equal(out == -4, ref == -4) or np.abs(out - ref).max() <= TOL_LOG
+    assert np.abs(out - ref).max() <= TOL_LOG
+
+
+def test_silent_chunk_is_nan_like_reference():
+    songs = np.zeros((1, 30 * 16000), dtype=np.float32)
+    out = _loader().load_songs(torch.from_numpy(songs).to(DEV)).cpu().numpy()
+    assert np.isnan(out).all()                       # reference: wav / 0 -> NaN survives clamp
+
+
+def test_peak_norm_scale_invariance_bit_exact():
+    songs = torch.from_numpy(L.synthetic_songs(2, seed=8)).to(DEV)
+    ld = _loader()
+    a = ld.load_songs(songs)
+    b = ld.load_songs(songs * 0.25)                  # power-of-two scaling is exact in fp32
+    assert torch.equal(a, b)
+
+
+def test_batch_independence_large_batch():
+    songs = L.synthetic_songs(24, seed=21)
+    ld = _loader()
+    big = ld.load_songs(torch.from_numpy(songs).to(DEV))
+    for i in (0, 13, 23):
+        one = ld.load_songs(torch.from_numpy(songs[i:i + 1]).to(DEV))
+        assert torch.equal(big[8 * i:8 * i + 8], one)
+    ref = L.load_songs(songs[[5]], "gtzan", mode="f64")
+    assert np.abs(big[40:48].cpu().numpy() - ref).max() <= TOL_LOG
+
+
+def test_feeds_the_explainer_end_to_end():
+    """songs -> log-mel (HIP) -> GTZAN-128 HeatmapGenerator (HIP): the front end's output is a
+    valid explainer input and the whole chain stays on device."""
+    from drsa_audio_amd.model.create_model import VGGType
+    from drsa_audio_amd.utils.constants import LRP_NAME_MAP_GTZAN
+    from drsa_audio_amd.xai.explain.explainer import HeatmapGenerator
+    torch.manual_seed(0)
+    m = VGGType(n_filters=(32, 32, 64, 64, 128), n_dense=128, pool_kernels=((2, 2),) * 5, dropout=0.4,
+                input_size=(128, 128), conv_bn=False, dense_bn=False, block_depth=1).eval().to(DEV)
+    U = torch.from_numpy(np.linalg.qr(np.random.default_rng(0).standard_normal((64, 64)))[0].astype(np.float32))
+    x = _loader().load_songs(torch.from_numpy(L.synthetic_songs(1, seed=1)).to(DEV))
+    hg = HeatmapGenerator(m, U, LRP_NAME_MAP_GTZAN, "blues", num_concepts=4, layer_idx=7, device=DEV)
+    hg.generate_subspace_heatmaps(x)
+    assert hg.info["subspace_heatmaps"].shape == (8, 4, 128, 128)
+    assert np.isfinite(hg.info["subspace_relevances"]).all()
