@@ -80,6 +80,8 @@ class ConvStage:
     xmode_bwd: int = XM_NONE
     w2_first: Optional[torch.Tensor] = None
     den_maps: Dict[Tuple[int, int], torch.Tensor] = field(default_factory=dict)
+    relu_name: Optional[str] = None      # features.<i> of the ReLU after the conv
+    pool_name: Optional[str] = None      # features.<i> of the MaxPool2d (None: no pool)
 
 
 @dataclass
@@ -152,6 +154,7 @@ class LRPEngine:
             if j >= n or not isinstance(feats[j][1], nn.ReLU):
                 raise EngineError(f"engine: conv features.{name} must be followed by ReLU")
             self._rule_ok_on_activation(rules.get(f"features.{feats[j][0]}"))
+            relu_name = f"features.{feats[j][0]}"
             j += 1
             proj = None
             if j < n and type(feats[j][1]).__name__ == "Projection":
@@ -173,10 +176,12 @@ class LRPEngine:
                     raise EngineError("engine: SubspaceHook num_concepts differs from the projection")
                 j += 3
             pool = False
+            pool_name = None
             if j < n and isinstance(feats[j][1], nn.MaxPool2d):
                 self._check_pool(feats[j][1])
                 self._rule_ok_on_activation(rules.get(f"features.{feats[j][0]}"))
                 pool = True
+                pool_name = f"features.{feats[j][0]}"
                 j += 1
             if proj is not None:
                 proj.pool_after = pool
@@ -187,7 +192,8 @@ class LRPEngine:
             eps = {None: 0.0, "epsilon": getattr(rule, "epsilon", 0.0), "gamma": getattr(rule, "stabilizer", 0.0),
                    "wsquare": getattr(rule, "stabilizer", 0.0), "flat": getattr(rule, "stabilizer", 0.0)}[kind]
             st = ConvStage(name=f"features.{name}", cin=m.in_channels, cout=m.out_channels, rule_kind=kind,
-                           eps=float(eps), pool=pool, proj=proj, input_nonneg=prev_nonneg, W=W, b=b, rule=rule)
+                           eps=float(eps), pool=pool, proj=proj, input_nonneg=prev_nonneg, W=W, b=b, rule=rule,
+                           relu_name=relu_name, pool_name=pool_name)
             self.stages.append(st)
             prev_nonneg = proj is None      # outputs are post-ReLU (pooled) unless a' follows
             i = j
@@ -327,8 +333,10 @@ class LRPEngine:
 
     # ---------------------------------------------------------------- forward
     @torch.no_grad()
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        """Model forward with all LRP state (argmax, denominators) kept on device."""
+    def forward(self, x: torch.Tensor, capture: Optional[int] = None) -> torch.Tensor:
+        """Model forward with all LRP state (argmax, denominators) kept on device.  ``capture``:
+        index of a conv stage whose full-resolution ReLU output is kept even though a max-pool
+        follows (the reference's store_hook, preprocessing.py:92-103)."""
         _capi.require_gpu(x, "input", dtype=None)
         x = x.detach().to(torch.float32).contiguous()
         if x.dim() != 4 or x.size(1) != self.stages[0].cin:
@@ -344,7 +352,20 @@ class LRPEngine:
             rec = {"in": cur, "H": h, "W": w}
             den_map = self._den_map(st, h, w) if st.den_kind == "map" else None
             need_den = st.den_kind is not None
-            if st.proj is None and st.pool:
+            if st.proj is None and st.pool and li == capture:
+                a = self._buf((li, "a"), (B, st.cout, h, w))
+                den_full = self._buf((li, "den_full"), (B, st.cout, h, w)) if need_den else None
+                self._call(f"conv_fwd:{st.name}", "drsa_amd_conv_fwd", cur.data_ptr(), st.wts_fwd.data_ptr(),
+                           st.bias3.data_ptr(), _capi.ptr(den_map), a.data_ptr(), None, _capi.ptr(den_full), B, st.cin,
+                           st.cout, h, w, st.ng_fwd, 0, s)
+                out = self._buf((li, "y"), (B, st.cout, h // 2, w // 2))
+                amax = self._buf((li, "amax"), (B, st.cout, h // 2, w // 2), torch.uint8)
+                den = self._buf((li, "den"), (B, st.cout, h // 2, w // 2)) if need_den else None
+                self._call("maxpool_capture", "drsa_amd_maxpool_capture", a.data_ptr(), _capi.ptr(den_full),
+                           out.data_ptr(), amax.data_ptr(), _capi.ptr(den), B, st.cout, h, w, s)
+                rec.update(a=a, y=out, amax=amax, den=den, Hout=h // 2, Wout=w // 2)
+                cur, h, w = out, h // 2, w // 2
+            elif st.proj is None and st.pool:
                 out = self._buf((li, "y"), (B, st.cout, h // 2, w // 2))
                 amax = self._buf((li, "amax"), (B, st.cout, h // 2, w // 2), torch.uint8)
                 den = self._buf((li, "den"), (B, st.cout, h // 2, w // 2)) if need_den else None
@@ -413,11 +434,12 @@ class LRPEngine:
 
     @torch.no_grad()
     def backward(self, seed: Optional[torch.Tensor] = None, cls: Optional[torch.Tensor] = None,
-                 one_hot: bool = False, fanout: bool = False) -> torch.Tensor:
+                 one_hot: bool = False, fanout: bool = False, stop_after: Optional[int] = None) -> torch.Tensor:
         """Relevance at the input.  ``seed`` [B, n_out] (output relevance) or ``cls`` [B] int32
         (lrp_output_modifier semantics).  ``fanout``: the projection stage emits K+1 clones per
         sample (HeatmapGenerator path); otherwise rows are treated as the reference's
-        replicated batch."""
+        replicated batch.  ``stop_after``: stop once the relevance at the OUTPUT of conv stage
+        ``stop_after`` is known and return it (pool resolution when that stage pools)."""
         st0 = self.last
         if st0 is None:
             raise RuntimeError("backward() before forward()")
@@ -434,6 +456,8 @@ class LRPEngine:
             post, den, eps_post = POST_NONE, None, 0.0
             if di == 0:
                 post, den, eps_post = self._post_for(L - 1)
+                if stop_after == L - 1:
+                    post, den, eps_post = POST_NONE, None, 0.0
                 x_mask = rec["x"]
             else:
                 x_mask = rec["x"]
@@ -456,6 +480,8 @@ class LRPEngine:
         g = R.reshape(B, self.stages[-1].cout, st0["stages"][-1]["Hout"], st0["stages"][-1]["Wout"])
         clones, Bq = 1, B
         for li in range(L - 1, -1, -1):
+            if stop_after is not None and li == stop_after:
+                return g
             st, rec = self.stages[li], st0["stages"][li]
             h, w = rec["H"], rec["W"]
             amax_in = None
@@ -479,6 +505,8 @@ class LRPEngine:
             x_in = rec["in"]
             if li > 0:
                 post, den, eps = self._post_for(li - 1)
+                if stop_after == li - 1:
+                    post, den, eps = POST_NONE, None, 0.0
             else:
                 post, den, eps = POST_NONE, None, 0.0
             if li == 0 and st.w2_first is not None:
@@ -493,6 +521,39 @@ class LRPEngine:
                            st.xmode_bwd, post, float(eps), s)
             g = out
         return g
+
+    # ------------------------------------------------------------ DRSA data
+    def capture_stage(self, layer_name: str) -> Tuple[int, str]:
+        """(stage index, "relu" | "pool") of a trunk module name (features.<layer_idx>)."""
+        for li, st in enumerate(self.stages):
+            if st.relu_name == layer_name:
+                if st.proj is not None:
+                    raise EngineError("engine: capture inside a ProjectionModel layer is not supported")
+                return li, "relu"
+            if st.pool_name == layer_name and st.proj is None:
+                return li, "pool"
+        raise EngineError(f"engine: {layer_name} is not a ReLU or MaxPool2d output of the conv trunk "
+                          "(DRSA data is captured at ReLU/pool outputs, preprocessing.py:60)")
+
+    @torch.no_grad()
+    def capture(self, x: torch.Tensor, layer_name: str, cls: Optional[torch.Tensor] = None, one_hot: bool = False,
+                seed_fn=None) -> dict:
+        """get_intermediate (preprocessing.py:106-176) for one batch: forward, LRP backward
+        down to layer ``layer_name`` only, and that layer's activation and relevance.  The
+        relevance of a pooled ReLU output is returned pooled with its argmax (``amax``); the
+        activation is the full map."""
+        li, where = self.capture_stage(layer_name)
+        st = self.stages[li]
+        out = self.forward(x, capture=li if (where == "relu" and st.pool) else None)
+        rec = self.last["stages"][li]
+        if seed_fn is not None:
+            R = self.backward(seed=seed_fn(out).contiguous(), stop_after=li)
+        else:
+            R = self.backward(cls=cls, one_hot=one_hot, stop_after=li)
+        if where == "pool":
+            return {"act": rec["y"], "rel": R, "amax": None, "H": rec["Hout"], "W": rec["Wout"], "C": st.cout}
+        return {"act": rec["a"], "rel": R, "amax": rec["amax"] if st.pool else None, "H": rec["H"], "W": rec["W"],
+                "C": st.cout}
 
     # -------------------------------------------------------------- heatmaps
     @torch.no_grad()

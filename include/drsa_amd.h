@@ -164,6 +164,37 @@ int drsa_amd_logmel(const float* wav, int64_t n_songs, int64_t song_stride, int 
                     const int* band_lo, const int* band_n, const int* band_off, const float* band_w, int band_nnz,
                     int peak_norm, int clamp, float clamp_min, float log_eps, float* out, void* stream);
 
+/* ------------------------------------------------------------------------- *
+ * DRSA training data: cxai/xai/drsa/preprocessing.py:18-256 and
+ * cxai/xai/drsa/cluster/getdrsadata.py:47-59.
+ * ------------------------------------------------------------------------- */
+
+/* 2x2 max-pool of a full-resolution ReLU output with the engine's argmax byte and the rule
+ * denominator gathered at the argmax (den may be NULL).  Lets the LRP forward keep the layer-j
+ * activation map (the reference's store_hook, preprocessing.py:92-103). */
+int drsa_amd_maxpool_capture(const float* a, const float* den, float* y, uint8_t* amax, float* den_pooled, int B,
+                             int C, int H, int W, void* stream);
+
+/* Relevance map at full resolution from its pooled form + argmax: layer.output.grad of
+ * get_intermediate (preprocessing.py:156-158). out [B, C, H, W]. */
+int drsa_amd_relevance_unpool(const float* rel, const uint8_t* amax, int B, int C, int H, int W, float* out,
+                              void* stream);
+
+/* Activation vectors and context vectors C = R / (A + 1e-7) at sampled locations
+ * (get_vectors_from_maps + compute_context_vectors, preprocessing.py:179-193, 234-256).
+ *   act [B, C, H, W]; rel full [B, C, H, W] (rel_amax NULL) or pooled [B, C, H/2, W/2] + argmax.
+ *   idx [B, L] int32 flat locations (sample_spatial_locations), or NULL = every location
+ *   (L = H*W, inference branch, [B, H*W, C]).
+ *   layout 0 = the reference's get_vectors_from_maps row order (transpose-then-reshape),
+ *   layout 1 = one row per (sample, location).  A_out, C_out [B*L, C]. */
+int drsa_amd_drsa_vectors(const float* act, const float* rel, const uint8_t* rel_amax, const int* idx, int B, int C,
+                          int H, int W, int L, int layout, float* A_out, float* C_out, void* stream);
+
+/* normalize_vectors (preprocessing.py:219-231): out = v / sqrt(mean(v^2)) / d^(1/4) over all
+ * n elements (deterministic fp64 reduction).  out may alias v. */
+size_t drsa_amd_normalize_workspace_bytes(void);
+int drsa_amd_normalize_vectors(const float* v, int64_t n, int d, float* out, void* ws, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

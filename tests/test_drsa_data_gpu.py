@@ -1,0 +1,121 @@
+"""DRSA training-data extraction (R16) on the HIP engine vs the oracle (GPU).
+
+Parity: activation and context vectors are bit-identical to the exact-order oracle
+(lrp_ref mode="exact" capturing (a, R) at the layer, then the reference's
+get_vectors_from_maps / compute_context_vectors restated in drsa_ref); the same global numpy
+RNG stream draws the locations.  normalize_vectors within 2e-6 relative (fp64 reduction vs
+torch's float32 mean).
+"""
+import numpy as np
+import pytest
+import torch
+
+import drsa_ref
+import lrp_ref
+from lrp_common import gtzan128, logmel, spec, toy
+from drsa_audio_amd.utils.constants import LRP_NAME_MAP_GTZAN, LRP_NAME_MAP_TOY
+from drsa_audio_amd.zennit.composites import NameMapComposite
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _gpu(m):
+    import copy
+    return copy.deepcopy(m).to(DEV)
+
+
+def _oracle_maps(m, nm, x, layer, class_idx):
+    _, _, (act, rel) = lrp_ref.lrp(m, spec(nm), x, class_idx=class_idx, mode="exact", capture=layer)
+    return act, rel
+
+
+@pytest.mark.parametrize("layer_idx", [7, 4, 8, 13])
+def test_get_intermediate_maps_bit_exact(layer_idx):
+    from drsa_audio_amd.xai.drsa.preprocessing import get_intermediate
+    net = gtzan128()
+    x = logmel(3, seed=layer_idx)
+    act, rel = _oracle_maps(net, LRP_NAME_MAP_GTZAN, x, f"features.{layer_idx}", 3)
+    a, r = get_intermediate(_gpu(net), x.to(DEV), NameMapComposite(LRP_NAME_MAP_GTZAN), layer_idx, 3,
+                            attr_batch_size=2)
+    assert torch.equal(a.cpu(), act)
+    assert torch.equal(r.cpu(), rel)
+
+
+@pytest.mark.parametrize("layout", [0, 1])
+def test_preprocess_data_sampled_bit_exact(layout):
+    from drsa_audio_amd.xai.drsa.preprocessing import preprocess_data
+    net = gtzan128()
+    x = logmel(5, seed=2)
+    act, rel = _oracle_maps(net, LRP_NAME_MAP_GTZAN, x, "features.7", 6)
+    np.random.seed(123)
+    idx = drsa_ref.sample_spatial_locations(5, act.shape[-2:], 20)
+    if layout == 0:
+        va = drsa_ref.get_vectors_from_maps(act, idx)
+        vr = drsa_ref.get_vectors_from_maps(rel, idx)
+    else:
+        b, d = act.shape[:2]
+        am, rm = act.reshape(b, d, -1), rel.reshape(b, d, -1)
+        va = torch.stack([am[i][:, idx[i]].T for i in range(b)]).reshape(-1, d)
+        vr = torch.stack([rm[i][:, idx[i]].T for i in range(b)]).reshape(-1, d)
+    ctx = drsa_ref.compute_context_vectors(va, vr)
+    np.random.seed(123)
+    A, C = preprocess_data(_gpu(net), x.to(DEV), NameMapComposite(LRP_NAME_MAP_GTZAN), 7, 6, num_locations=20,
+                           attr_batch_size=3, layout=layout)
+    assert A.shape == (100, 64)
+    assert torch.equal(A.cpu(), va)
+    assert torch.equal(C.cpu(), ctx)
+
+
+def test_preprocess_data_all_locations_inference_branch():
+    from drsa_audio_amd.xai.drsa.preprocessing import preprocess_data
+    net = toy()
+    x = logmel(2, 64, 64, seed=3)
+    act, rel = _oracle_maps(net, LRP_NAME_MAP_TOY, x, "features.4", 1)
+    A, C = preprocess_data(_gpu(net), x.to(DEV), NameMapComposite(LRP_NAME_MAP_TOY), 4, 1)
+    b, d = act.shape[:2]
+    va = act.reshape(b, d, -1).transpose(-2, -1)              # intended D3 semantics
+    vr = rel.reshape(b, d, -1).transpose(-2, -1)
+    assert A.shape == va.shape
+    assert torch.equal(A.cpu(), va)
+    assert torch.equal(C.cpu(), drsa_ref.compute_context_vectors(va, vr))
+
+
+def test_get_vectors_and_normalize_vs_reference_fixture(golden_dir):
+    from drsa_audio_amd.xai.drsa.preprocessing import get_vectors_from_maps, normalize_vectors
+    fx = np.load(f"{golden_dir}/preprocessing_fixture.npz")
+    va = get_vectors_from_maps(torch.from_numpy(fx["maps_a"]).to(DEV), fx["idx"])
+    assert np.array_equal(va.cpu().numpy(), fx["vec_a"])
+    na = normalize_vectors(torch.from_numpy(fx["vec_a"]).to(DEV)).cpu().numpy()
+    nc = normalize_vectors(torch.from_numpy(fx["ctx"]).to(DEV)).cpu().numpy()
+    np.testing.assert_allclose(na, fx["norm_a"], rtol=2e-6, atol=1e-7)
+    np.testing.assert_allclose(nc, fx["norm_ctx"], rtol=2e-6, atol=1e-7)
+
+
+def test_training_data_feeds_drsa_and_matches_oracle_objective(tmp_path):
+    """C3 pipeline on device: LRP capture at j=7 -> 20 locations -> normalise -> DRSA step; the
+    objective on the extracted data matches the oracle's on the oracle-extracted data."""
+    from drsa_audio_amd.xai.drsa.preprocessing import drsa_training_data
+    from drsa_audio_amd.xai.drsa.drsa import drsa_step
+    from drsa_audio_amd.xai.drsa.cluster.getdrsadata import load_and_normalize_data, save_data
+    net = gtzan128()
+    x = logmel(8, seed=5)
+    np.random.seed(7)
+    A, C = drsa_training_data(_gpu(net), x.to(DEV), NameMapComposite(LRP_NAME_MAP_GTZAN), 7, 3, num_locations=20)
+    act, rel = _oracle_maps(net, LRP_NAME_MAP_GTZAN, x, "features.7", 3)
+    np.random.seed(7)
+    idx = drsa_ref.sample_spatial_locations(8, act.shape[-2:], 20)
+    va = drsa_ref.get_vectors_from_maps(act, idx)
+    ctx = drsa_ref.compute_context_vectors(va, drsa_ref.get_vectors_from_maps(rel, idx))
+    Ar, Cr = drsa_ref.normalize_vectors(va), drsa_ref.normalize_vectors(ctx)
+    np.testing.assert_allclose(A.cpu().numpy(), Ar.numpy(), rtol=2e-6, atol=1e-7)
+    np.testing.assert_allclose(C.cpu().numpy(), Cr.numpy(), rtol=2e-6, atol=1e-7)
+    U0 = torch.from_numpy(np.linalg.qr(np.random.default_rng(0).standard_normal((64, 64)))[0].astype(np.float32))
+    _, f = drsa_step(A, C, U0.to(DEV), 4)
+    _, f_ref, _ = drsa_ref.step(Ar, Cr, U0, 4)
+    assert abs(float(f) - f_ref) <= 1e-4 * abs(f_ref)
+    # pickle round trip in the reference's dataset format
+    p = save_data(va, ctx, layer=7, sample_class="blues", output_path=str(tmp_path))
+    a2, c2 = load_and_normalize_data(p, DEV)
+    np.testing.assert_allclose(a2.cpu().numpy(), Ar.numpy(), rtol=2e-6, atol=1e-7)
+    np.testing.assert_allclose(c2.cpu().numpy(), Cr.numpy(), rtol=2e-6, atol=1e-7)
