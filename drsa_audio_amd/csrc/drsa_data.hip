@@ -18,13 +18,15 @@
 namespace {
 
 // relevance at flat location p of channel map (b, c) from a full map or a pooled map + argmax
+// (ph x pw max-pool; argmax byte = dy * pw + dx, the first maximum in row-major window order)
 __device__ __forceinline__ float rel_at(const float* __restrict__ rel, const uint8_t* __restrict__ amax, size_t bc,
-                                        int p, int H, int W) {
+                                        size_t bc_amax, int p, int H, int W, int ph, int pw) {
   if (!amax) return rel[bc * (size_t)(H * W) + p];
   const int y = p / W, x = p % W;
-  const int W2 = W >> 1, H2 = H >> 1;
-  const size_t q = bc * (size_t)(H2 * W2) + (size_t)(y >> 1) * W2 + (x >> 1);
-  return ((int)amax[q] == ((y & 1) << 1 | (x & 1))) ? rel[q] : 0.f;
+  const int W2 = W / pw, H2 = H / ph;
+  const size_t cell = (size_t)(y / ph) * W2 + (x / pw);
+  return ((int)amax[bc_amax * (size_t)(H2 * W2) + cell] == (y % ph) * pw + (x % pw)) ? rel[bc * (size_t)(H2 * W2) + cell]
+                                                                                     : 0.f;
 }
 
 // layout 0: get_vectors_from_maps exactly as the reference (preprocessing.py:251-255): the
@@ -34,7 +36,7 @@ __device__ __forceinline__ float rel_at(const float* __restrict__ rel, const uin
 __global__ __launch_bounds__(256) void drsa_vectors_kernel(const float* __restrict__ act, const float* __restrict__ rel,
                                                            const uint8_t* __restrict__ amax,
                                                            const int* __restrict__ idx, int B, int C, int H, int W,
-                                                           int L, int layout, float* __restrict__ A_out,
+                                                           int ph, int pw, int L, int layout, float* __restrict__ A_out,
                                                            float* __restrict__ C_out) {
   const int64_t total = (int64_t)B * L * C;
   for (int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x; o < total; o += (int64_t)gridDim.x * 256) {
@@ -51,49 +53,55 @@ __global__ __launch_bounds__(256) void drsa_vectors_kernel(const float* __restri
     const int p = idx ? idx[(size_t)b * L + l] : l;
     const size_t bc = (size_t)b * C + ch;
     const float a = act[bc * (size_t)(H * W) + p];
-    const float r = rel_at(rel, amax, bc, p, H, W);
+    const float r = rel_at(rel, amax, bc, bc, p, H, W, ph, pw);
     A_out[o] = a;
     C_out[o] = r / (a + 1e-7f);      // compute_context_vectors
   }
 }
 
-// relevance map at full resolution from the pooled form (get_intermediate's layer.output.grad)
+// relevance (or rule-divided g) at full resolution from the pooled form: get_intermediate's
+// layer.output.grad, and the engine's max-pool backward for pools other than 2x2.  Rows of rel
+// are sample*clones + clone; amax is per sample.
 __global__ __launch_bounds__(256) void unpool_kernel(const float* __restrict__ rel, const uint8_t* __restrict__ amax,
-                                                     int64_t BC, int H, int W, float* __restrict__ out) {
+                                                     int64_t BC, int C, int clones, int H, int W, int ph, int pw,
+                                                     float* __restrict__ out) {
   const int64_t total = BC * H * W;
   for (int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x; o < total; o += (int64_t)gridDim.x * 256) {
     const size_t bc = (size_t)(o / (H * W));
-    out[o] = rel_at(rel, amax, bc, (int)(o % (H * W)), H, W);
+    const size_t bca = (bc / C) / clones * C + bc % C;
+    out[o] = rel_at(rel, amax, bc, bca, (int)(o % (H * W)), H, W, ph, pw);
   }
 }
 
-// 2x2 max-pool of a full-resolution activation with the engine's argmax byte (first maximum in
-// row-major window order, NaN wins: torch max_pool2d) and the rule denominator gathered at the
-// argmax — the same tensors the fused conv+pool forward epilogue writes.
+// ph x pw max-pool (stride = kernel) of a full-resolution activation with the engine's argmax
+// byte (first maximum in row-major window order, NaN wins: torch max_pool2d) and the rule
+// denominator gathered at the argmax — the tensors the fused conv+2x2-pool epilogue writes.
 __global__ __launch_bounds__(256) void maxpool_capture_kernel(const float* __restrict__ a, const float* __restrict__ den,
-                                                              int64_t BC, int H, int W, float* __restrict__ y,
-                                                              uint8_t* __restrict__ amax, float* __restrict__ den_p) {
-  const int H2 = H >> 1, W2 = W >> 1;
+                                                              int64_t BC, int H, int W, int ph, int pw,
+                                                              float* __restrict__ y, uint8_t* __restrict__ amax,
+                                                              float* __restrict__ den_p) {
+  const int H2 = H / ph, W2 = W / pw;
   const int64_t total = BC * H2 * W2;
   for (int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x; o < total; o += (int64_t)gridDim.x * 256) {
     const size_t bc = (size_t)(o / (H2 * W2));
     const int rem = (int)(o % (H2 * W2));
     const int qy = rem / W2, qx = rem % W2;
-    const size_t base = bc * (size_t)(H * W) + (size_t)(2 * qy) * W + 2 * qx;
-    const size_t off[4] = {0, 1, (size_t)W, (size_t)W + 1};
+    const size_t base = bc * (size_t)(H * W) + (size_t)(ph * qy) * W + pw * qx;
     int am = 0;
+    size_t amoff = 0;
     float m = a[base];
-#pragma unroll
-    for (int s = 1; s < 4; ++s) {
-      const float v = a[base + off[s]];
+    for (int s = 1; s < ph * pw; ++s) {
+      const size_t off = (size_t)(s / pw) * W + (s % pw);
+      const float v = a[base + off];
       if (v > m || (v != v && m == m)) {
         m = v;
         am = s;
+        amoff = off;
       }
     }
     y[o] = m;
     amax[o] = (uint8_t)am;
-    if (den) den_p[o] = den[base + off[am]];
+    if (den) den_p[o] = den[base + amoff];
   }
 }
 
@@ -136,36 +144,40 @@ int grid_for(int64_t total) {
 }  // namespace
 
 extern "C" int drsa_amd_maxpool_capture(const float* a, const float* den, float* y, uint8_t* amax, float* den_pooled,
-                                        int B, int C, int H, int W, void* stream) {
+                                        int B, int C, int H, int W, int ph, int pw, void* stream) {
   DRSA_REQUIRE(a && y && amax, "maxpool_capture: null pointer");
   DRSA_REQUIRE(!den || den_pooled, "maxpool_capture: den needs den_pooled");
-  DRSA_REQUIRE(B >= 0 && C > 0 && H % 2 == 0 && W % 2 == 0 && H > 0 && W > 0, "maxpool_capture: bad shape");
+  DRSA_REQUIRE(ph >= 1 && pw >= 1 && ph * pw <= 256, "maxpool_capture: bad pool kernel %dx%d", ph, pw);
+  DRSA_REQUIRE(B >= 0 && C > 0 && H > 0 && W > 0 && H % ph == 0 && W % pw == 0, "maxpool_capture: bad shape");
   if (B == 0) return DRSA_OK;
   const int64_t BC = (int64_t)B * C;
-  hipLaunchKernelGGL(maxpool_capture_kernel, dim3(grid_for(BC * (H / 2) * (W / 2))), dim3(256), 0,
-                     (hipStream_t)stream, a, den, BC, H, W, y, amax, den_pooled);
+  hipLaunchKernelGGL(maxpool_capture_kernel, dim3(grid_for(BC * (H / ph) * (W / pw))), dim3(256), 0,
+                     (hipStream_t)stream, a, den, BC, H, W, ph, pw, y, amax, den_pooled);
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;
 }
 
-extern "C" int drsa_amd_relevance_unpool(const float* rel, const uint8_t* amax, int B, int C, int H, int W, float* out,
-                                         void* stream) {
+extern "C" int drsa_amd_relevance_unpool(const float* rel, const uint8_t* amax, int Bq, int clones, int C, int H, int W,
+                                         int ph, int pw, float* out, void* stream) {
   DRSA_REQUIRE(rel && amax && out, "relevance_unpool: null pointer");
-  DRSA_REQUIRE(B >= 0 && C > 0 && H % 2 == 0 && W % 2 == 0, "relevance_unpool: bad shape");
-  if (B == 0) return DRSA_OK;
-  const int64_t BC = (int64_t)B * C;
-  hipLaunchKernelGGL(unpool_kernel, dim3(grid_for(BC * H * W)), dim3(256), 0, (hipStream_t)stream, rel, amax, BC, H,
-                     W, out);
+  DRSA_REQUIRE(clones >= 1 && Bq % clones == 0, "relevance_unpool: bad clones");
+  DRSA_REQUIRE(ph >= 1 && pw >= 1 && ph * pw <= 256, "relevance_unpool: bad pool kernel");
+  DRSA_REQUIRE(Bq >= 0 && C > 0 && H % ph == 0 && W % pw == 0, "relevance_unpool: bad shape");
+  if (Bq == 0) return DRSA_OK;
+  const int64_t BC = (int64_t)Bq * C;
+  hipLaunchKernelGGL(unpool_kernel, dim3(grid_for(BC * H * W)), dim3(256), 0, (hipStream_t)stream, rel, amax, BC, C,
+                     clones, H, W, ph, pw, out);
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;
 }
 
 extern "C" int drsa_amd_drsa_vectors(const float* act, const float* rel, const uint8_t* rel_amax, const int* idx,
-                                     int B, int C, int H, int W, int L, int layout, float* A_out, float* C_out,
-                                     void* stream) {
+                                     int B, int C, int H, int W, int ph, int pw, int L, int layout, float* A_out,
+                                     float* C_out, void* stream) {
   DRSA_REQUIRE(act && rel && A_out && C_out, "drsa_vectors: null pointer");
   DRSA_REQUIRE(B >= 0 && C > 0 && H > 0 && W > 0, "drsa_vectors: bad shape");
-  DRSA_REQUIRE(!rel_amax || (H % 2 == 0 && W % 2 == 0), "drsa_vectors: pooled relevance needs even H, W");
+  DRSA_REQUIRE(!rel_amax || (ph >= 1 && pw >= 1 && H % ph == 0 && W % pw == 0),
+               "drsa_vectors: pooled relevance needs H, W divisible by the pool kernel");
   DRSA_REQUIRE(layout == 0 || layout == 1, "drsa_vectors: layout must be 0 (reference) or 1 (rows)");
   if (!idx) {
     DRSA_REQUIRE(L == H * W, "drsa_vectors: idx == NULL takes every location (L must be H*W)");
@@ -175,7 +187,7 @@ extern "C" int drsa_amd_drsa_vectors(const float* act, const float* rel, const u
   }
   if (B == 0) return DRSA_OK;
   hipLaunchKernelGGL(drsa_vectors_kernel, dim3(grid_for((int64_t)B * L * C)), dim3(256), 0, (hipStream_t)stream, act,
-                     rel, rel_amax, idx, B, C, H, W, L, layout, A_out, C_out);
+                     rel, rel_amax, idx, B, C, H, W, ph, pw, L, layout, A_out, C_out);
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;
 }

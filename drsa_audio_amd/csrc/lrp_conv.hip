@@ -9,7 +9,7 @@
 // dispatch table
 // ---------------------------------------------------------------------------
 namespace drsa_conv {
-extern const Table kTableFwdA, kTableFwdB, kTableFwdC, kTableBwdA, kTableBwdB;
+extern const Table kTableFwdA, kTableFwdB, kTableFwdC, kTableFwdD, kTableFwdE, kTableBwdA, kTableBwdB, kTableBwdC;
 }
 
 namespace {
@@ -17,7 +17,8 @@ using drsa_conv::Entry;
 using namespace drsa_conv;
 
 const drsa_conv::Table* kTables[] = {&drsa_conv::kTableFwdA, &drsa_conv::kTableFwdB, &drsa_conv::kTableFwdC,
-                                     &drsa_conv::kTableBwdA, &drsa_conv::kTableBwdB};
+                                     &drsa_conv::kTableFwdD, &drsa_conv::kTableFwdE, &drsa_conv::kTableBwdA,
+                                     &drsa_conv::kTableBwdB, &drsa_conv::kTableBwdC};
 
 int pad32(int c) { return (c + 31) / 32 * 32; }
 
@@ -74,6 +75,7 @@ int drsa_amd_conv_fwd(const float* in, const float* wts, const float* bias, cons
   DRSA_REQUIRE(ng >= 1 && ng <= 3, "conv_fwd: ng must be 1..3");
   DRSA_REQUIRE(H % 2 == 0 && W % 2 == 0, "conv_fwd: H and W must be even (got %dx%d)", H, W);
   DRSA_REQUIRE(!pool || out_amax, "conv_fwd: pool needs out_amax");
+  DRSA_REQUIRE(pool || W % 4 == 0, "conv_fwd: an unpooled output needs W %% 4 == 0 (float4 epilogue; got W=%d)", W);
   const int cin_p = cin_pad(cin), cout_p = pad32(cout);
   const Entry* e = find(cin_p, cout_p, W, ng, A_DENSE, pool ? EPI_FWD_POOL : EPI_FWD_RELU);
   if (!e) {
@@ -91,7 +93,7 @@ int drsa_amd_conv_bwd(const float* g, const uint8_t* g_amax, const float* wts, c
                       int post, float eps, void* stream) {
   DRSA_REQUIRE(Bq > 0 && clones > 0 && Bq % clones == 0, "conv_bwd: bad batch/clones");
   DRSA_REQUIRE(ng >= 1 && ng <= 2, "conv_bwd: ng must be 1..2");
-  DRSA_REQUIRE(H % 2 == 0 && W % 2 == 0, "conv_bwd: H and W must be even");
+  DRSA_REQUIRE(H % 2 == 0 && W % 4 == 0, "conv_bwd: H must be even and W %% 4 == 0 (got %dx%d)", H, W);
   DRSA_REQUIRE(xmode == XM_NONE || x, "conv_bwd: xmode needs x");
   DRSA_REQUIRE(post == POST_NONE || (x && (den || post == POST_MASK)), "conv_bwd: POST_DIV needs x and den");
   const int cin_p = pad32(cin), cout_p = pad32(cout);

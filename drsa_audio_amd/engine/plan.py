@@ -82,6 +82,7 @@ class ConvStage:
     den_maps: Dict[Tuple[int, int], torch.Tensor] = field(default_factory=dict)
     relu_name: Optional[str] = None      # features.<i> of the ReLU after the conv
     pool_name: Optional[str] = None      # features.<i> of the MaxPool2d (None: no pool)
+    pool_k: Tuple[int, int] = (2, 2)     # max-pool kernel (= stride); 2x2 is fused into the conv
 
 
 @dataclass
@@ -142,15 +143,18 @@ class LRPEngine:
             if not isinstance(m, nn.Conv2d):
                 raise EngineError(f"engine: unexpected feature layer features.{name} ({type(m).__name__})")
             self._check_conv(m, name)
-            W = m.weight.detach().to(self.device, torch.float32)
-            b = (m.bias.detach().to(self.device, torch.float32) if m.bias is not None
-                 else torch.zeros(m.out_channels, device=self.device))
+            # weights are prepared on the host in fp32 (the BN merge there is the same IEEE
+            # arithmetic as zennit's canonizer on CPU) and then moved to the device once
+            W = m.weight.detach().cpu().to(torch.float32)
+            b = (m.bias.detach().cpu().to(torch.float32) if m.bias is not None
+                 else torch.zeros(m.out_channels))
             j = i + 1
             if j < n and isinstance(feats[j][1], nn.BatchNorm2d):
                 if not merge_bn:
                     raise EngineError("BatchNorm2d in the trunk needs the SequentialMergeBatchNorm canonizer")
-                W, b = SequentialMergeBatchNorm.fold(W, b, _bn_to(feats[j][1], self.device))
+                W, b = SequentialMergeBatchNorm.fold(W, b, _bn_to(feats[j][1], torch.device("cpu")))
                 j += 1
+            W, b = W.to(self.device), b.to(self.device)
             if j >= n or not isinstance(feats[j][1], nn.ReLU):
                 raise EngineError(f"engine: conv features.{name} must be followed by ReLU")
             self._rule_ok_on_activation(rules.get(f"features.{feats[j][0]}"))
@@ -177,14 +181,17 @@ class LRPEngine:
                 j += 3
             pool = False
             pool_name = None
+            pool_k = (2, 2)
             if j < n and isinstance(feats[j][1], nn.MaxPool2d):
-                self._check_pool(feats[j][1])
+                pool_k = self._check_pool(feats[j][1])
                 self._rule_ok_on_activation(rules.get(f"features.{feats[j][0]}"))
                 pool = True
                 pool_name = f"features.{feats[j][0]}"
                 j += 1
             if proj is not None:
                 proj.pool_after = pool
+                if pool and pool_k != (2, 2):
+                    raise EngineError("engine: a ProjectionModel layer must be followed by MaxPool2d(2) or no pool")
             rule = rules.get(f"features.{name}")
             kind = _kind(rule)
             if kind not in (None, "epsilon", "gamma", "wsquare", "flat"):
@@ -193,7 +200,7 @@ class LRPEngine:
                    "wsquare": getattr(rule, "stabilizer", 0.0), "flat": getattr(rule, "stabilizer", 0.0)}[kind]
             st = ConvStage(name=f"features.{name}", cin=m.in_channels, cout=m.out_channels, rule_kind=kind,
                            eps=float(eps), pool=pool, proj=proj, input_nonneg=prev_nonneg, W=W, b=b, rule=rule,
-                           relu_name=relu_name, pool_name=pool_name)
+                           relu_name=relu_name, pool_name=pool_name, pool_k=pool_k)
             self.stages.append(st)
             prev_nonneg = proj is None      # outputs are post-ReLU (pooled) unless a' follows
             i = j
@@ -207,14 +214,16 @@ class LRPEngine:
                 continue
             if not isinstance(m, nn.Linear):
                 raise EngineError(f"engine: unexpected classifier layer classifier.{name} ({type(m).__name__})")
-            W = m.weight.detach().to(self.device, torch.float32)
-            b = m.bias.detach().to(self.device, torch.float32) if m.bias is not None else None
+            W = m.weight.detach().cpu().to(torch.float32)
+            b = m.bias.detach().cpu().to(torch.float32) if m.bias is not None else None
             j = i + 1
             if j < n and isinstance(cl[j][1], nn.BatchNorm1d):
                 if not merge_bn:
                     raise EngineError("BatchNorm1d in the head needs the SequentialMergeBatchNorm canonizer")
-                W, b = SequentialMergeBatchNorm.fold(W, b, _bn_to(cl[j][1], self.device))
+                W, b = SequentialMergeBatchNorm.fold(W, b, _bn_to(cl[j][1], torch.device("cpu")))
                 j += 1
+            W = W.to(self.device)
+            b = None if b is None else b.to(self.device)
             relu = False
             while j < n and isinstance(cl[j][1], (nn.ReLU, nn.Dropout)):
                 if isinstance(cl[j][1], nn.ReLU):
@@ -248,8 +257,10 @@ class LRPEngine:
         st = m.stride if isinstance(m.stride, tuple) else (m.stride, m.stride)
         pd = m.padding if isinstance(m.padding, tuple) else (m.padding, m.padding)
         dl = m.dilation if isinstance(m.dilation, tuple) else (m.dilation, m.dilation)
-        if tuple(ks) != (2, 2) or tuple(st) != (2, 2) or tuple(pd) != (0, 0) or tuple(dl) != (1, 1) or m.ceil_mode:
-            raise EngineError(f"engine: only MaxPool2d(2) is supported yet (got kernel {ks})")
+        if tuple(ks) != tuple(st) or tuple(pd) != (0, 0) or tuple(dl) != (1, 1) or m.ceil_mode or ks[0] * ks[1] > 256:
+            raise EngineError(f"engine: MaxPool2d must have stride = kernel, no padding/dilation (got kernel {ks}, "
+                              f"stride {st})")
+        return (int(ks[0]), int(ks[1]))
 
     @staticmethod
     def _rule_ok_on_activation(rule):
@@ -347,24 +358,25 @@ class LRPEngine:
         state = {"B": B, "input": x, "stages": []}
         cur, h, w = x, H, W
         for li, st in enumerate(self.stages):
-            if h % 2 or w % 2:
-                raise ValueError(f"{st.name}: feature map {h}x{w} must have even sides")
+            ph, pw = st.pool_k if st.pool else (1, 1)
+            if h % 2 or w % 2 or h % ph or w % pw:
+                raise ValueError(f"{st.name}: feature map {h}x{w} must have even sides divisible by the pool")
             rec = {"in": cur, "H": h, "W": w}
             den_map = self._den_map(st, h, w) if st.den_kind == "map" else None
             need_den = st.den_kind is not None
-            if st.proj is None and st.pool and li == capture:
+            if st.proj is None and st.pool and (li == capture or st.pool_k != (2, 2)):
                 a = self._buf((li, "a"), (B, st.cout, h, w))
                 den_full = self._buf((li, "den_full"), (B, st.cout, h, w)) if need_den else None
                 self._call(f"conv_fwd:{st.name}", "drsa_amd_conv_fwd", cur.data_ptr(), st.wts_fwd.data_ptr(),
                            st.bias3.data_ptr(), _capi.ptr(den_map), a.data_ptr(), None, _capi.ptr(den_full), B, st.cin,
                            st.cout, h, w, st.ng_fwd, 0, s)
-                out = self._buf((li, "y"), (B, st.cout, h // 2, w // 2))
-                amax = self._buf((li, "amax"), (B, st.cout, h // 2, w // 2), torch.uint8)
-                den = self._buf((li, "den"), (B, st.cout, h // 2, w // 2)) if need_den else None
-                self._call("maxpool_capture", "drsa_amd_maxpool_capture", a.data_ptr(), _capi.ptr(den_full),
-                           out.data_ptr(), amax.data_ptr(), _capi.ptr(den), B, st.cout, h, w, s)
-                rec.update(a=a, y=out, amax=amax, den=den, Hout=h // 2, Wout=w // 2)
-                cur, h, w = out, h // 2, w // 2
+                out = self._buf((li, "y"), (B, st.cout, h // ph, w // pw))
+                amax = self._buf((li, "amax"), (B, st.cout, h // ph, w // pw), torch.uint8)
+                den = self._buf((li, "den"), (B, st.cout, h // ph, w // pw)) if need_den else None
+                self._call(f"maxpool:{st.pool_name}", "drsa_amd_maxpool_capture", a.data_ptr(), _capi.ptr(den_full),
+                           out.data_ptr(), amax.data_ptr(), _capi.ptr(den), B, st.cout, h, w, ph, pw, s)
+                rec.update(a=a, y=out, amax=amax, den=den, Hout=h // ph, Wout=w // pw)
+                cur, h, w = out, h // ph, w // pw
             elif st.proj is None and st.pool:
                 out = self._buf((li, "y"), (B, st.cout, h // 2, w // 2))
                 amax = self._buf((li, "amax"), (B, st.cout, h // 2, w // 2), torch.uint8)
@@ -499,8 +511,14 @@ class LRPEngine:
                            _capi.ptr(den if post == POST_DIV else None), P.U.data_ptr(), G.data_ptr(), B, st.cout,
                            h, w, K, P.eps_inv, eps, 1 if fan else 0, s)
                 g, clones, Bq = G, nq, B * nq
-            elif st.pool:
+            elif st.pool and st.pool_k == (2, 2):
                 amax_in = rec["amax"]
+            elif st.pool:
+                ph, pw = st.pool_k
+                gf = self._buf((li, "g_unpool"), (Bq, st.cout, h, w))
+                self._call(f"maxpool_bwd:{st.pool_name}", "drsa_amd_relevance_unpool", g.data_ptr(),
+                           rec["amax"].data_ptr(), Bq, clones, st.cout, h, w, ph, pw, gf.data_ptr(), s)
+                g = gf
             # rule backward of conv li
             x_in = rec["in"]
             if li > 0:
@@ -550,10 +568,12 @@ class LRPEngine:
             R = self.backward(seed=seed_fn(out).contiguous(), stop_after=li)
         else:
             R = self.backward(cls=cls, one_hot=one_hot, stop_after=li)
+        ph, pw = st.pool_k
         if where == "pool":
-            return {"act": rec["y"], "rel": R, "amax": None, "H": rec["Hout"], "W": rec["Wout"], "C": st.cout}
+            return {"act": rec["y"], "rel": R, "amax": None, "H": rec["Hout"], "W": rec["Wout"], "C": st.cout,
+                    "ph": 1, "pw": 1}
         return {"act": rec["a"], "rel": R, "amax": rec["amax"] if st.pool else None, "H": rec["H"], "W": rec["W"],
-                "C": st.cout}
+                "C": st.cout, "ph": ph, "pw": pw}
 
     # -------------------------------------------------------------- heatmaps
     @torch.no_grad()

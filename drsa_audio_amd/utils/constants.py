@@ -35,3 +35,27 @@ LRP_NAME_MAP_TOY = [
     (["classifier.2"], Epsilon(epsilon=1e-7)),
     (["classifier.4"], Epsilon(epsilon=1e-7)),
 ]
+
+
+def lrp_name_map_vggish(gamma: float = 0.3, stab: float = 1e-7, dense_eps: float = 1e-7):
+    """VGGish-BN name map of the reference's DRSA data script (getdrsadata.py:87-108): WSquare on
+    the first conv, Gamma(gamma) on blocks 1-2, gamma/2 on blocks 3-4, gamma/4 on block 5,
+    Epsilon on the dense layers (the model is used with SequentialMergeBatchNorm)."""
+    return [
+        (["features.0"], WSquare(stabilizer=stab)),
+        (["features.3"], Gamma(gamma=gamma, stabilizer=stab)),
+        (["features.7"], Gamma(gamma=gamma, stabilizer=stab)),
+        (["features.10"], Gamma(gamma=gamma, stabilizer=stab)),
+        (["features.14"], Gamma(gamma=gamma / 2, stabilizer=stab)),
+        (["features.17"], Gamma(gamma=gamma / 2, stabilizer=stab)),
+        (["features.21"], Gamma(gamma=gamma / 2, stabilizer=stab)),
+        (["features.24"], Gamma(gamma=gamma / 2, stabilizer=stab)),
+        (["features.28"], Gamma(gamma=gamma / 4, stabilizer=stab)),
+        (["features.31"], Gamma(gamma=gamma / 4, stabilizer=stab)),
+        (["classifier.0"], Epsilon(epsilon=dense_eps)),
+        (["classifier.4"], Epsilon(epsilon=dense_eps)),
+        (["classifier.8"], Epsilon(epsilon=dense_eps)),
+    ]
+
+
+LRP_NAME_MAP_VGGISH = lrp_name_map_vggish()

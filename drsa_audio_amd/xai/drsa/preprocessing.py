@@ -78,8 +78,8 @@ def get_intermediate(model: nn.Module, input_batch: torch.Tensor, composite, lay
         acts.append(cap["act"].clone())
         if cap["amax"] is not None:
             full = torch.empty_like(cap["act"])
-            _capi.call("drsa_amd_relevance_unpool", cap["rel"].data_ptr(), cap["amax"].data_ptr(), xb.size(0),
-                       cap["C"], cap["H"], cap["W"], full.data_ptr(), _capi.stream_ptr(x.device))
+            _capi.call("drsa_amd_relevance_unpool", cap["rel"].data_ptr(), cap["amax"].data_ptr(), xb.size(0), 1,
+                       cap["C"], cap["H"], cap["W"], cap["ph"], cap["pw"], full.data_ptr(), _capi.stream_ptr(x.device))
             rels.append(full)
         else:
             rels.append(cap["rel"].clone())
@@ -100,7 +100,8 @@ def _layer_name(model, layer) -> str:
 def _vectors(cap: dict, idx: Optional[torch.Tensor], L: int, layout: int, A_out: torch.Tensor,
              C_out: torch.Tensor, B: int, device) -> None:
     _capi.call("drsa_amd_drsa_vectors", cap["act"].data_ptr(), cap["rel"].data_ptr(), _capi.ptr(cap["amax"]),
-               _capi.ptr(idx), B, cap["C"], cap["H"], cap["W"], L, layout, A_out.data_ptr(), C_out.data_ptr(),
+               _capi.ptr(idx), B, cap["C"], cap["H"], cap["W"], cap["ph"], cap["pw"], L, layout, A_out.data_ptr(),
+               C_out.data_ptr(),
                _capi.stream_ptr(device))
 
 
@@ -162,7 +163,7 @@ def get_vectors_from_maps(maps: torch.Tensor, idcs_batch: np.ndarray) -> torch.T
     L = idx.size(1)
     A = torch.empty(B * L, d, device=maps.device)
     Cc = torch.empty_like(A)
-    _capi.call("drsa_amd_drsa_vectors", maps.data_ptr(), maps.data_ptr(), None, idx.data_ptr(), B, d, H, W, L,
+    _capi.call("drsa_amd_drsa_vectors", maps.data_ptr(), maps.data_ptr(), None, idx.data_ptr(), B, d, H, W, 1, 1, L,
                LAYOUT_REFERENCE, A.data_ptr(), Cc.data_ptr(), _capi.stream_ptr(maps.device))
     return A
 

@@ -169,26 +169,29 @@ int drsa_amd_logmel(const float* wav, int64_t n_songs, int64_t song_stride, int 
  * cxai/xai/drsa/cluster/getdrsadata.py:47-59.
  * ------------------------------------------------------------------------- */
 
-/* 2x2 max-pool of a full-resolution ReLU output with the engine's argmax byte and the rule
- * denominator gathered at the argmax (den may be NULL).  Lets the LRP forward keep the layer-j
- * activation map (the reference's store_hook, preprocessing.py:92-103). */
+/* ph x pw max-pool (stride = kernel) of a full-resolution ReLU output with the engine's argmax
+ * byte (dy*pw + dx of the first maximum) and the rule denominator gathered at the argmax (den
+ * may be NULL).  Keeps the layer-j activation map for DRSA data (the reference's store_hook,
+ * preprocessing.py:92-103) and runs the pools the fused conv epilogue does not (VGGish (2,4),
+ * create_model.py:61 pool_kernels). */
 int drsa_amd_maxpool_capture(const float* a, const float* den, float* y, uint8_t* amax, float* den_pooled, int B,
-                             int C, int H, int W, void* stream);
+                             int C, int H, int W, int ph, int pw, void* stream);
 
-/* Relevance map at full resolution from its pooled form + argmax: layer.output.grad of
- * get_intermediate (preprocessing.py:156-158). out [B, C, H, W]. */
-int drsa_amd_relevance_unpool(const float* rel, const uint8_t* amax, int B, int C, int H, int W, float* out,
-                              void* stream);
+/* Full-resolution map from its pooled form + argmax (ph x pw pool): layer.output.grad of
+ * get_intermediate (preprocessing.py:156-158), and the max-pool backward of pools other than
+ * 2x2.  rel rows are sample*clones + clone, amax rows are samples.  out [Bq, C, H, W]. */
+int drsa_amd_relevance_unpool(const float* rel, const uint8_t* amax, int Bq, int clones, int C, int H, int W, int ph,
+                              int pw, float* out, void* stream);
 
 /* Activation vectors and context vectors C = R / (A + 1e-7) at sampled locations
  * (get_vectors_from_maps + compute_context_vectors, preprocessing.py:179-193, 234-256).
- *   act [B, C, H, W]; rel full [B, C, H, W] (rel_amax NULL) or pooled [B, C, H/2, W/2] + argmax.
+ *   act [B, C, H, W]; rel full [B, C, H, W] (rel_amax NULL) or pooled [B, C, H/ph, W/pw] + argmax.
  *   idx [B, L] int32 flat locations (sample_spatial_locations), or NULL = every location
  *   (L = H*W, inference branch, [B, H*W, C]).
  *   layout 0 = the reference's get_vectors_from_maps row order (transpose-then-reshape),
  *   layout 1 = one row per (sample, location).  A_out, C_out [B*L, C]. */
 int drsa_amd_drsa_vectors(const float* act, const float* rel, const uint8_t* rel_amax, const int* idx, int B, int C,
-                          int H, int W, int L, int layout, float* A_out, float* C_out, void* stream);
+                          int H, int W, int ph, int pw, int L, int layout, float* A_out, float* C_out, void* stream);
 
 /* normalize_vectors (preprocessing.py:219-231): out = v / sqrt(mean(v^2)) / d^(1/4) over all
  * n elements (deterministic fp64 reduction).  out may alias v. */

@@ -84,7 +84,7 @@ def _kind(m: nn.Module) -> str:
         return "relu"
     if isinstance(m, nn.MaxPool2d):
         return "maxpool"
-    if isinstance(m, nn.Dropout):
+    if isinstance(m, (nn.Dropout, nn.Identity)):
         return "dropout"
     if isinstance(m, nn.BatchNorm2d):
         return "bn2d"
@@ -97,6 +97,33 @@ def _kind(m: nn.Module) -> str:
     if cname == "InvProjection":
         return "invproj"
     raise TypeError(f"oracle: unsupported module {cname}")
+
+
+@torch.no_grad()
+def merge_batch_norm(model: nn.Module) -> nn.Module:
+    """zennit 0.5.1 ``SequentialMergeBatchNorm`` (canonizers.py; used at getdrsadata.py:81,113):
+    every BatchNorm directly after a Conv2d/Linear is merged into it,
+    w' = w * (gamma / (var + eps) ** .5), b' = (b - mean) * (gamma / (var + eps) ** .5) + beta,
+    and the BatchNorm becomes the identity.  Returns a merged deep copy (CPU)."""
+    import copy
+    m = copy.deepcopy(model).cpu()
+    for seq in (m.features, m.classifier):
+        kids = list(seq.children())
+        for a, b in zip(kids[:-1], kids[1:]):
+            if isinstance(b, (nn.BatchNorm1d, nn.BatchNorm2d)) and isinstance(a, (nn.Conv2d, nn.Linear)):
+                scale = b.weight / (b.running_var + b.eps) ** .5
+                shape = (-1,) + (1,) * (a.weight.dim() - 1)
+                a.weight.data = a.weight.data * scale.reshape(shape)
+                b0 = a.bias.data if a.bias is not None else torch.zeros_like(b.running_mean)
+                if a.bias is None:
+                    a.bias = nn.Parameter(b0.clone())
+                a.bias.data = (b0 - b.running_mean) * scale + b.bias
+        # the merged BatchNorm is the identity (zennit sets mean 0, var 1, eps 0; torch >= 2.x
+        # rejects eps = 0, so the module is replaced by nn.Identity instead)
+        for name, b in list(seq.named_children()):
+            if isinstance(b, (nn.BatchNorm1d, nn.BatchNorm2d)):
+                setattr(seq, name, nn.Identity())
+    return m
 
 
 def sequential_layers(model: nn.Module) -> List[Layer]:

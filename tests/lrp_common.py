@@ -60,3 +60,23 @@ def maxnorm_err(a, b):
     a = torch.as_tensor(a).reshape(a.shape[0], -1).double()
     b = torch.as_tensor(b).reshape(b.shape[0], -1).double()
     return float(((a - b).abs().amax(1) / b.abs().amax(1).clamp_min(1e-30)).max())
+
+
+def vggish(seed=0, input_size=(128, 256), randomize_bn=True):
+    """VGGish-BN of the reference's DRSA scripts (getdrsadata.py:68-73): filters (64,64,100,128,128),
+    n_dense 100, pools ((2,4),(2,2),(2,2),(2,2),(2,2)), block_depth 2, BN in trunk and head.
+    BN running statistics / affine parameters are randomised so that merging is not a no-op."""
+    torch.manual_seed(seed)
+    m = VGGType(n_filters=(64, 64, 100, 128, 128), n_dense=100,
+                pool_kernels=((2, 4), (2, 2), (2, 2), (2, 2), (2, 2)), dropout=0.3, input_size=input_size,
+                conv_bn=True, dense_bn=True).eval()
+    if randomize_bn:
+        g = torch.Generator().manual_seed(seed + 100)
+        for mod in m.modules():
+            if isinstance(mod, (torch.nn.BatchNorm1d, torch.nn.BatchNorm2d)):
+                n = mod.num_features
+                mod.running_mean.copy_(0.1 * torch.randn(n, generator=g))
+                mod.running_var.copy_(0.5 + torch.rand(n, generator=g))
+                mod.weight.data.copy_(0.8 + 0.4 * torch.rand(n, generator=g))
+                mod.bias.data.copy_(0.05 * torch.randn(n, generator=g))
+    return m

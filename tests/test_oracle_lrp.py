@@ -191,3 +191,27 @@ def test_preprocessing_helpers_match_reference_fixture(golden_dir):
     ctx = drsa_ref.compute_context_vectors(va, vr)
     assert np.array_equal(ctx.numpy(), fx["ctx"])
     assert np.array_equal(drsa_ref.normalize_vectors(va).numpy(), fx["norm_a"])
+
+
+def test_merge_batch_norm_preserves_forward():
+    """oracle.merge_batch_norm (zennit SequentialMergeBatchNorm restated): the merged network
+    computes the same function as the BN network in eval mode."""
+    from lrp_common import vggish
+    net = vggish(input_size=(64, 128))
+    merged = lrp_ref.merge_batch_norm(net)
+    x = logmel(2, 64, 128, seed=1)
+    with torch.no_grad():
+        a = net.classifier(net.features(x).reshape(2, -1))
+        b = merged.classifier(merged.features(x).reshape(2, -1))
+    assert torch.allclose(a, b, rtol=1e-4, atol=1e-6)
+    assert not any(isinstance(m, (torch.nn.BatchNorm1d, torch.nn.BatchNorm2d)) for m in merged.modules())
+
+
+def test_product_bn_fold_matches_oracle_merge():
+    from lrp_common import vggish
+    from drsa_audio_amd.zennit.canonizers import SequentialMergeBatchNorm
+    net = vggish(input_size=(64, 128))
+    merged = lrp_ref.merge_batch_norm(net)
+    w, b = SequentialMergeBatchNorm.fold(net.features[3].weight.detach(), net.features[3].bias.detach(),
+                                         net.features[4])
+    assert torch.equal(w, merged.features[3].weight) and torch.equal(b, merged.features[3].bias)
