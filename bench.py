@@ -184,14 +184,69 @@ def frontend_bench(device, n_songs=64, iters=20):
             "max_abs_logmel_err_vs_f64_oracle_song0": err}
 
 
+def drsa_joint_bench(device, steps=200):
+    """C5 DRSA: layers j=26 and j=33 of VGGish (d=128, K=16 each, 20000 rows each) optimised
+    together in one hipGraph (drsa_amd_drsa_run_multi)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from gen_fixtures import drsa_inputs
+    from drsa_audio_amd.xai.drsa.drsa import drsa_run, drsa_run_joint
+    N, d, K = 20000, 128, 16
+    probs = []
+    for seed in (26, 33):
+        A, C = drsa_inputs(N, d, seed)
+        U0 = np.linalg.qr(np.random.default_rng(seed).standard_normal((d, d)))[0].astype(np.float32)
+        probs.append(tuple(torch.from_numpy(v).to(device) for v in (A, C, U0)) + (K,))
+    s = torch.cuda.Stream(device)
+    with torch.cuda.stream(s):
+        drsa_run_joint(probs, 4)
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        out = drsa_run_joint(probs, steps)
+        torch.cuda.synchronize(device)
+        dt = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        for A, C, U0, K_ in probs:
+            drsa_run(A, C, U0, K_, steps)
+        torch.cuda.synchronize(device)
+        dt_seq = time.perf_counter() - t0
+    flop = 2 * 8.0 * N * d * d
+    return {"config": "C5 joint: 2 problems (VGGish j=26, j=33) x N=20000, d=128, K=16, one graph",
+            "ms_per_joint_step": dt / steps * 1e3, "ms_per_step_sequential_runs": dt_seq / steps * 1e3,
+            "vector_steps_per_s": 2 * N * steps / dt, "tflops_algorithmic": flop * steps / dt / 1e12,
+            "objective_final": [float(t[-1]) for _, t in out]}
+
+
+def vggish_lrp_bench(device, B=32, iters=5):
+    """C5 model: standard LRP (compute_relevances) on VGGish-BN, 128x256 log-mel, fp32."""
+    from drsa_audio_amd.model.create_model import VGGType
+    from drsa_audio_amd.utils.constants import LRP_NAME_MAP_VGGISH
+    from drsa_audio_amd.zennit.canonizers import SequentialMergeBatchNorm
+    from drsa_audio_amd.zennit.composites import NameMapComposite
+    from drsa_audio_amd.xai.explain.attribute import compute_relevances
+    torch.manual_seed(0)
+    m = VGGType(n_filters=(64, 64, 100, 128, 128), n_dense=100, pool_kernels=((2, 4),) + ((2, 2),) * 4, dropout=0.3,
+                input_size=(128, 256), conv_bn=True, dense_bn=True).eval().to(device)
+    comp = NameMapComposite(LRP_NAME_MAP_VGGISH, canonizers=[SequentialMergeBatchNorm()])
+    x = synthetic_logmel(B, 128, 256, seed=5, device=device)
+    for _ in range(2):
+        compute_relevances(m, x, comp, class_idx=1)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        compute_relevances(m, x, comp, class_idx=1)
+    torch.cuda.synchronize(device)
+    return {"config": f"VGGish-BN (64,64,100,128,128), block_depth 2, 128x256, B={B}, standard LRP fp32",
+            "samples_per_s": B * iters / (time.perf_counter() - t0)}
+
+
 def drsa_sharded_bench(device, world, rank, steps=100):
-    """C4-style row-sharded DRSA: 20000 rows per rank (weak), d=64, K=4; one RCCL all-reduce of the
-    [d*d+K] partial per step (drsa_audio_amd/xai/drsa/distributed.py)."""
+    """C4 row-sharded DRSA: 20000 rows per rank (weak; 160000 at 8 ranks), d=64, K=8; one RCCL
+    all-reduce of the [d*d+K] partial per step (drsa_audio_amd/xai/drsa/distributed.py)."""
     import torch.distributed as dist
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from gen_fixtures import drsa_inputs
     from drsa_audio_amd.xai.drsa.distributed import sharded_run
-    n, d, K = 20000, 64, 4
+    n, d, K = 20000, 64, 8
     A, C = drsa_inputs(n, d, 100 + rank)
     U0 = np.load(os.path.join(ROOT, "tests", "golden", "u64_seed42.npy"))
     Ag, Cg, Ug = (torch.from_numpy(v).to(device) for v in (A, C, U0))
@@ -327,6 +382,8 @@ def main():
     if not args.no_drsa and rank == 0:
         drsa = drsa_bench(device)
     frontend = frontend_bench(device) if rank == 0 else None
+    joint = drsa_joint_bench(device) if (rank == 0 and not args.no_drsa) else None
+    vgg = vggish_lrp_bench(device) if (rank == 0 and not args.no_drsa) else None
     drsa_sharded = None
     if not args.no_drsa and world > 1:
         drsa_sharded = drsa_sharded_bench(device, world, rank)
@@ -360,7 +417,8 @@ def main():
             "kernels": kernels,
             "secondary": {"standard_lrp_c2_bs64_samples_per_s": c2 * world,
                           "explained_samples_per_s_bs64": bs64 * world, "drsa": drsa,
-                          "drsa_sharded": drsa_sharded, "logmel_frontend": frontend},
+                          "drsa_sharded": drsa_sharded, "drsa_joint_c5": joint, "vggish_lrp": vgg,
+                          "logmel_frontend": frontend},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -29,6 +29,7 @@ SIGNATURES = {
     "drsa_amd_drsa_step": (_i32, [_fp, _fp, _i64, _i32, _i32, _fp, _fp, _fp, _vp, _sz, _vp]),
     "drsa_amd_drsa_objective": (_i32, [_fp, _fp, _i64, _i32, _i32, _fp, _fp, _vp, _sz, _vp]),
     "drsa_amd_drsa_run": (_i32, [_fp, _fp, _i64, _i32, _i32, _fp, _fp, _i32, _fp, _ip, _vp, _sz, _i32, _vp]),
+    "drsa_amd_drsa_run_multi": (_i32, [_i32, _vp, _i32, _i32, _vp]),
     "drsa_amd_polar": (_i32, [_fp, _i32, _fp, _ip, _vp]),
     "drsa_amd_subspace_relevances": (_i32, [_fp, _fp, _i64, _i64, _i32, _i32, _fp, _fp, _vp]),
     "drsa_amd_conv_weight_floats": (_sz, [_i32, _i32, _i32]),
@@ -54,6 +55,12 @@ SIGNATURES = {
     "drsa_amd_logmel": (_i32, [_fp, _i64, _i64, _i32, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _fp, _ip, _ip, _ip,
                                _fp, _i32, _i32, _i32, _f32, _f32, _fp, _vp]),
 }
+
+class DrsaProblem(C.Structure):
+    """drsa_amd_problem_t (include/drsa_amd.h)."""
+    _fields_ = [("A", _vp), ("C", _vp), ("N", _i64), ("d", _i32), ("K", _i32), ("U_io", _vp), ("U_tmp", _vp),
+                ("f_traj", _vp), ("counter", _vp), ("ws", _vp), ("ws_size", _sz)]
+
 
 XM_NONE, XM_MUL, XM_SPLIT = 0, 1, 2
 POST_NONE, POST_DIV, POST_MASK = 0, 1, 2

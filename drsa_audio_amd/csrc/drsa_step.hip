@@ -16,6 +16,7 @@
 //                        polar(V) by Newton-Schulz on fp32 MFMA in one workgroup; writes f, U_new
 // The closed-form gradient equals autograd's (checked in float64 in tests/test_oracle_drsa.py).
 #include "common.h"
+#include "drsa_amd.h"
 
 #include <stdarg.h>
 #include <vector>
@@ -718,6 +719,126 @@ int drsa_amd_drsa_run(const float* A, const float* C, int64_t N, int d, int K, f
   if (rc) return rc;
   return dispatch_finish(gs, (double)N, d, K, U_io, nullptr, f_traj, counter, 1, 1, kPolarTol,
                          kPolarMaxIter, nullptr, s);
+}
+
+// P independent problems (e.g. the C5 joint optimisation of two layers, optsubspaces.py:18-23
+// run one after the other in the reference) advanced together: per step every problem's
+// partial/reduce/finish chain runs on its own forked stream inside ONE captured hipGraph, so
+// the latency-bound single-workgroup finish kernels of different problems overlap and the
+// whole S-step joint loop is one graph launch per two steps.
+int drsa_amd_drsa_run_multi(int P, const drsa_amd_problem_t* probs, int steps, int use_graph, void* stream) {
+  DRSA_REQUIRE(P >= 1 && P <= 64 && probs, "drsa_run_multi: P must be in [1, 64]");
+  DRSA_REQUIRE(steps >= 0, "drsa_run_multi: steps < 0");
+  for (int p = 0; p < P; ++p) {
+    const drsa_amd_problem_t& q = probs[p];
+    DRSA_REQUIRE(supported_dims(q.d, q.K), "drsa_run_multi: problem %d unsupported d=%d K=%d", p, q.d, q.K);
+    DRSA_REQUIRE(q.N > 0 && q.A && q.C && q.U_io && q.U_tmp && q.f_traj && q.counter && q.ws,
+                 "drsa_run_multi: problem %d has null pointers or N <= 0", p);
+    DRSA_REQUIRE(q.ws_size >= ws_bytes(q.N, q.d, q.K), "drsa_run_multi: problem %d workspace too small", p);
+  }
+  if (P == 1 || !use_graph || steps < 2) {
+    for (int p = 0; p < P; ++p) {
+      const drsa_amd_problem_t& q = probs[p];
+      int rc = drsa_amd_drsa_run(q.A, q.C, q.N, q.d, q.K, q.U_io, q.U_tmp, steps, q.f_traj, q.counter, q.ws,
+                                 q.ws_size, use_graph, stream);
+      if (rc) return rc;
+    }
+    return DRSA_OK;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  hipStream_t side[64] = {nullptr};
+  hipEvent_t ev_fork = nullptr, ev_join[64] = {nullptr};
+  int rc = DRSA_OK;
+  auto cleanup = [&]() {
+    for (int p = 0; p < P; ++p) {
+      if (side[p]) (void)hipStreamDestroy(side[p]);
+      if (ev_join[p]) (void)hipEventDestroy(ev_join[p]);
+    }
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+  };
+  auto hip_ok = [&](hipError_t e, const char* what) -> bool {
+    if (e == hipSuccess) return true;
+    drsa::set_error("drsa_run_multi: %s: %s", what, hipGetErrorString(e));
+    rc = (int)e;
+    return false;
+  };
+  if (!hip_ok(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming), "event")) { cleanup(); return rc; }
+  for (int p = 0; p < P; ++p) {
+    if (!hip_ok(hipStreamCreateWithFlags(&side[p], hipStreamNonBlocking), "stream") ||
+        !hip_ok(hipEventCreateWithFlags(&ev_join[p], hipEventDisableTiming), "event")) {
+      cleanup();
+      return rc;
+    }
+    const drsa_amd_problem_t& q = probs[p];
+    if (!hip_ok(hipMemsetAsync(q.counter, 0, sizeof(int), s), "memset")) { cleanup(); return rc; }
+  }
+  // one step of problem p on stream st: U_in -> U_out, f -> f_traj[counter++]
+  auto one = [&](int p, hipStream_t st, const float* Uin, float* Uout) -> int {
+    const drsa_amd_problem_t& q = probs[p];
+    const PartialPlan pl = plan_partial(q.N, q.d);
+    float* gs = (float*)q.ws + (size_t)pl.grid * ((size_t)q.d * q.d + q.K);
+    int r = drsa_amd_drsa_partial(q.A, q.C, q.N, q.d, q.K, Uin, gs, q.ws, q.ws_size, st);
+    if (r) return r;
+    return dispatch_finish(gs, (double)q.N, q.d, q.K, Uin, Uout, q.f_traj, q.counter, 1, Uout ? 0 : 1, kPolarTol,
+                           kPolarMaxIter, nullptr, st);
+  };
+  // fork -> per-problem body -> join, captured from stream s
+  auto forked = [&](int nsteps_body, bool final_objective) -> int {
+    if (!hip_ok(hipEventRecord(ev_fork, s), "record")) return rc;
+    for (int p = 0; p < P; ++p) {
+      if (!hip_ok(hipStreamWaitEvent(side[p], ev_fork, 0), "wait")) return rc;
+      const drsa_amd_problem_t& q = probs[p];
+      for (int k = 0; k < nsteps_body; ++k) {
+        int r = (k % 2 == 0) ? one(p, side[p], q.U_io, q.U_tmp) : one(p, side[p], q.U_tmp, q.U_io);
+        if (r) return r;
+      }
+      if (final_objective) {
+        int r = one(p, side[p], q.U_io, nullptr);
+        if (r) return r;
+      }
+      if (!hip_ok(hipEventRecord(ev_join[p], side[p]), "record")) return rc;
+      if (!hip_ok(hipStreamWaitEvent(s, ev_join[p], 0), "wait")) return rc;
+    }
+    return DRSA_OK;
+  };
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  if (!hip_ok(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal), "capture")) { cleanup(); return rc; }
+  int rbody = forked(2, false);
+  hipError_t ce = hipStreamEndCapture(s, &graph);
+  if (rbody || !hip_ok(ce, "end capture") || !hip_ok(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0), "instantiate")) {
+    if (graph) (void)hipGraphDestroy(graph);
+    cleanup();
+    return rbody ? rbody : rc;
+  }
+  int done = 0;
+  for (; done + 2 <= steps; done += 2)
+    if (!hip_ok(hipGraphLaunch(exec, s), "graph launch")) break;
+  (void)hipGraphExecDestroy(exec);
+  (void)hipGraphDestroy(graph);
+  if (rc) { cleanup(); return rc; }
+  // odd tail step + final objective, eager on the forked streams
+  if (done < steps) {
+    if (!hip_ok(hipEventRecord(ev_fork, s), "record")) { cleanup(); return rc; }
+    for (int p = 0; p < P; ++p) {
+      const drsa_amd_problem_t& q = probs[p];
+      if (!hip_ok(hipStreamWaitEvent(side[p], ev_fork, 0), "wait")) { cleanup(); return rc; }
+      int r = one(p, side[p], q.U_io, q.U_tmp);
+      if (r) { cleanup(); return r; }
+      if (!hip_ok(hipMemcpyAsync(q.U_io, q.U_tmp, (size_t)q.d * q.d * sizeof(float), hipMemcpyDeviceToDevice,
+                                 side[p]), "copy")) { cleanup(); return rc; }
+      if (!hip_ok(hipEventRecord(ev_join[p], side[p]), "record") || !hip_ok(hipStreamWaitEvent(s, ev_join[p], 0), "wait")) {
+        cleanup();
+        return rc;
+      }
+    }
+  }
+  int r = forked(0, true);
+  if (r) { cleanup(); return r; }
+  // make sure nothing is pending on the side streams before they are destroyed
+  for (int p = 0; p < P; ++p) (void)hipStreamSynchronize(side[p]);
+  cleanup();
+  return DRSA_OK;
 }
 
 int drsa_amd_polar(const float* V, int d, float* U_out, int* iters_out, void* stream) {

@@ -77,6 +77,45 @@ def sharded_run(A_local: torch.Tensor, C_local: torch.Tensor, U0: torch.Tensor, 
     return U, torch.cat([t.reshape(1) for t in traj]).cpu().numpy()
 
 
+def sharded_run_joint(problems, steps: int, group=None, backends=None):
+    """Several DRSA problems (C5: layers j=26 and j=33 of one model, K=16 each) row-sharded over
+    the process group and advanced together with ONE all-reduce per step: the P partials
+    [d_p*d_p + K_p] are packed into one buffer (64.1 KB per d=128 problem), reduced, and each
+    problem finishes from its slice.  ``problems``: list of (A_local, C_local, U0, K).
+    Returns [(U_S, trajectory [S+1])] on every rank."""
+    P = len(problems)
+    if backends is None:
+        backends = [HipBackend(A.contiguous(), C.contiguous(), U0.size(0), K) for A, C, U0, K in problems]
+    dev = problems[0][2].device
+    n = torch.tensor([A.size(0) for A, _, _, _ in problems], dtype=torch.int64, device=dev)
+    if dist.is_initialized():
+        dist.all_reduce(n, op=dist.ReduceOp.SUM, group=group)
+    N_tot = [int(v) for v in n.tolist()]
+    sizes = [U0.size(0) ** 2 + K for _, _, U0, K in problems]
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(int)
+    Us = [U0.detach().clone().contiguous() for _, _, U0, _ in problems]
+    trajs: List[List[torch.Tensor]] = [[] for _ in range(P)]
+
+    def reduced():
+        parts = [backends[p].partial(Us[p]) for p in range(P)]
+        buf = torch.cat([t.reshape(-1) for t in parts])
+        if dist.is_initialized():
+            dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+        return [buf[offs[p]:offs[p + 1]].contiguous() for p in range(P)]
+
+    for _ in range(steps):
+        gss = reduced()
+        for p in range(P):
+            Us[p], f = backends[p].finish(gss[p], N_tot[p], Us[p])
+            trajs[p].append(f)
+    gss = reduced()
+    out = []
+    for p in range(P):
+        trajs[p].append(backends[p].objective(gss[p], N_tot[p], Us[p]))
+        out.append((Us[p], torch.cat([t.reshape(1) for t in trajs[p]]).cpu().numpy()))
+    return out
+
+
 def shard_rows(N: int, world: int, rank: int) -> slice:
     """Contiguous, balanced row range of ``rank``."""
     base, rem = divmod(N, world)

@@ -113,6 +113,38 @@ def drsa_run(A, C, U0, K: int, steps: int, ws: Optional[DrsaWorkspace] = None,
     return U, traj
 
 
+def drsa_run_joint(problems, steps: int, use_graph: bool = True):
+    """Several independent DRSA problems advanced together (C5: the same model's layers j=26 and
+    j=33, K=16 each; the reference optimises them one after another, optsubspaces.py:18-23).
+
+    ``problems``: list of (A, C, U0, K) on one device.  One hipGraph holds every problem's step
+    on its own forked stream (drsa_amd_drsa_run_multi).  Returns [(U_S, trajectory [S+1])]."""
+    import ctypes
+    if not problems:
+        return []
+    dev = problems[0][0].device
+    keep, structs, outs = [], [], []
+    for A, C, U0, K in problems:
+        _check_problem(A, C, U0, K)
+        if A.device != dev:
+            raise ValueError("drsa_run_joint: all problems must live on one device")
+        N, d = A.shape
+        ws = DrsaWorkspace(N, d, K, dev)
+        U = U0.detach().clone().contiguous()
+        U_tmp = torch.empty_like(U)
+        traj = torch.empty(steps + 1, dtype=torch.float32, device=dev)
+        keep += [ws, U_tmp, A, C]
+        outs.append((U, traj))
+        structs.append(_capi.DrsaProblem(A.data_ptr(), C.data_ptr(), N, d, int(K), U.data_ptr(), U_tmp.data_ptr(),
+                                         traj.data_ptr(), ws.counter.data_ptr(), ws.ptr, ws.nbytes))
+    arr = (_capi.DrsaProblem * len(structs))(*structs)
+    stream = torch.cuda.current_stream(dev)
+    graph = bool(use_graph) and stream.cuda_stream != 0
+    _capi.call("drsa_amd_drsa_run_multi", len(structs), ctypes.addressof(arr), int(steps), 1 if graph else 0,
+               stream.cuda_stream)
+    return outs
+
+
 class SubspaceOptimizer:
     """Trains U by gradient ascent + polar retraction (reference drsa.py:15-168)."""
 

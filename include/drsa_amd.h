@@ -143,6 +143,26 @@ int drsa_amd_first_layer_den(const float* w2, const float* b2, float* den, int C
 int drsa_amd_heatmap_sort(const float* hm, int B, int K, int HW, float* std_out, float* std_rel, float* sub_out,
                           float* rel, int64_t* mask, void* stream);
 
+/* One DRSA problem for drsa_amd_drsa_run_multi (all pointers device memory; the fields mean what
+ * the same-named arguments of drsa_amd_drsa_run mean). */
+typedef struct drsa_amd_problem {
+  const float* A;
+  const float* C;
+  int64_t N;
+  int d;
+  int K;
+  float* U_io;
+  float* U_tmp;
+  float* f_traj; /* [steps + 1] */
+  int* counter;
+  void* ws;
+  size_t ws_size;
+} drsa_amd_problem_t;
+
+/* P independent problems advanced S steps together (C5: two layers, K=16 each, one graph).
+ * Replaces the sequential per-layer loop of optsubspaces.py:18-23 / drsa.main. */
+int drsa_amd_drsa_run_multi(int P, const drsa_amd_problem_t* probs, int steps, int use_graph, void* stream);
+
 /* ------------------------------------------------------------------------- *
  * Log-mel front end
  * Replaces cxai/utils/dataloading.py:62-74 + :138-176 (Loader: torchaudio

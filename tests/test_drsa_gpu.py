@@ -190,3 +190,24 @@ def test_sharded_run_two_ranks_gloo_matches_single():
     traj1 = traj1.cpu().numpy()
     assert np.max(np.abs(res[0][1] - traj1) / np.abs(traj1)) < 1e-5
     assert np.abs(res[0][0] - U1.cpu().numpy()).max() < 1e-4
+
+
+def test_joint_run_equals_separate_runs_bitwise():
+    """drsa_amd_drsa_run_multi (C5: two d=128 K=16 problems in one graph) gives exactly what two
+    separate drsa_run calls give."""
+    from drsa_audio_amd.xai.drsa.drsa import drsa_run, drsa_run_joint
+    probs = []
+    for N, seed in ((3000, 1), (2048, 2)):
+        A, C = drsa_inputs(N, 128, seed)
+        probs.append((*_gpu(A, C, _u0(128, seed)), 16))
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        joint = drsa_run_joint(probs, 7)
+        sep = [drsa_run(A, C, U0, K, 7) for A, C, U0, K in probs]
+    torch.cuda.synchronize()
+    for (Uj, tj), (Us, ts) in zip(joint, sep):
+        assert torch.equal(Uj, Us) and torch.equal(tj, ts)
+    # and against the oracle's trajectory
+    A, C, U0, K = probs[0]
+    Ur, ref = drsa_ref.run(A.cpu(), C.cpu(), U0.cpu(), K, 7)
+    np.testing.assert_allclose(joint[0][1].cpu().numpy(), np.array(ref), rtol=1e-4)
