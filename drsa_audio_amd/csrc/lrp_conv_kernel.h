@@ -75,6 +75,8 @@ struct ConvCfg {
   static constexpr size_t staging_floats = (size_t)CIC * PLANE + (size_t)NG * KCP * COUT;
   static constexpr size_t epi_floats = (size_t)TCH * TH * TWP;
   static constexpr size_t lds_floats = staging_floats > epi_floats ? staging_floats : epi_floats;
+  // minimum waves per SIMD the register allocation must allow (1 block = 1 wave per SIMD)
+  static constexpr int WPE = (EPI == EPI_BWD && NG == 1) ? 3 : 1;
   static_assert(TH % MTH == 0 && TW % MTW == 0, "tile must be a multiple of the M-tile");
   static_assert(COUT % 32 == 0, "COUT must be padded to 32");
   static_assert(CIN % CIC == 0, "CIN must be a multiple of the chunk");
@@ -338,7 +340,7 @@ __device__ __forceinline__ void mfma_chunk(const float* halo, const float* wl, c
 
 
 template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI>
-__global__ __launch_bounds__(kThreads) void conv3x3_kernel(ConvArgs a) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AMODE, EPI>::WPE))) void conv3x3_kernel(ConvArgs a) {
   using Cfg = ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AMODE, EPI>;
   constexpr int HY = Cfg::HY, HX = Cfg::HX, RS = Cfg::RS, PLANE = Cfg::PLANE;
   constexpr int MTH = Cfg::MTH, MTW = Cfg::MTW, MTX = Cfg::MTX;
