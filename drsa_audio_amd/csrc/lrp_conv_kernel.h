@@ -26,6 +26,10 @@
 #include "common.h"
 #include "lrp_conv.h"
 
+#ifndef DRSA_CONV_PD_BWD
+#define DRSA_CONV_PD_BWD 2
+#endif
+
 namespace drsa_conv {
 
 constexpr int kThreads = 256;
@@ -77,6 +81,8 @@ struct ConvCfg {
   static constexpr size_t lds_floats = staging_floats > epi_floats ? staging_floats : epi_floats;
   // minimum waves per SIMD the register allocation must allow (1 block = 1 wave per SIMD)
   static constexpr int WPE = (EPI == EPI_BWD && NG == 1) ? 3 : 1;
+  // operand prefetch distance of the MFMA loop (k-steps)
+  static constexpr int PD = DRSA_CONV_PD_BWD > 0 && EPI == EPI_BWD ? DRSA_CONV_PD_BWD : 1;
   static_assert(TH % MTH == 0 && TW % MTW == 0, "tile must be a multiple of the M-tile");
   static_assert(COUT % 32 == 0, "COUT must be padded to 32");
   static_assert(CIN % CIC == 0, "CIN must be a multiple of the chunk");
@@ -395,7 +401,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
     __syncthreads();
     if (chunk + 1 < Cfg::NCHUNK) stg.load(a, (chunk + 1) * CIC, tid, ty0, tx0, bq, bs);
     if (!active || (a.dbg & 4)) continue;
-    mfma_chunk<Cfg>(halo, wl, pix_off, lane, wn, acc);
+    mfma_chunk<Cfg, Cfg::PD>(halo, wl, pix_off, lane, wn, acc);
   }
 
   // ---- epilogue, staged through LDS so global I/O is coalesced float4 rows ----
