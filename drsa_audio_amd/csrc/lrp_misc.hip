@@ -387,22 +387,27 @@ __global__ __launch_bounds__(256) void first_layer_bwd_kernel(const float* __res
 // Pool-sparse variant (the VGG case: conv0 -> ReLU -> MaxPool2d(2)).  A workgroup covers
 // 16 x 64 pool cells (32 x 128 output pixels); each thread owns 2 x 2 cells = a 4 x 4 pixel
 // block.  Per group of FQ_C channels the cells of the tile (+1 halo) are expanded to pixels
-// while staging (value at the argmax position, zeros elsewhere; two 8-byte LDS writes per
-// cell) into an image with origin pixel (2qy0-2, 2qx0-2); the next group's cells are
-// prefetched into registers while the current group is consumed.  Every thread reads its
-// 6 x 6 patch per channel and runs 9 fmas per pixel in the dense chain order
-// (channel, dy, dx) — the chain of the dense kernel above and of oracle/lrp_exact.c (the
-// zero terms included: fma(0, w, acc) == acc).
+// while staging (value at the argmax position, zeros elsewhere) into an image with origin
+// pixel (2qy0-2, 2qx0-2) at column 1 (so that even pixel pairs of a thread's patch are 8-byte
+// aligned); the next group's cells are prefetched (branch-free, clamped addresses) into
+// registers while the current group is consumed.  Every thread reads its 6 x 6 patch per
+// channel as five pixel pairs per row and runs packed fmas (v_pk_fma_f32: two output pixels
+// per instruction) in the dense chain order (channel, dy, dx) — the chain of the dense kernel
+// above and of oracle/lrp_exact.c (the zero terms included: fma(0, w, acc) == acc).
 constexpr int FQ_Y = 16, FQ_X = 64, FQ_C = 2;
 constexpr int FQ_RY = FQ_Y + 2, FQ_RX = FQ_X + 2;            // cells incl. halo
 constexpr int FQ_PY = 2 * FQ_RY, FQ_PX = 2 * FQ_RX + 4;      // pixel image (row pad 4)
 constexpr int FQ_KR = (FQ_RY + 3) / 4;                       // row passes of 4 waves
 constexpr int FQ_NS = FQ_C * FQ_KR + 1;                      // staged cells per thread
 
+typedef float fq2 __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ void fq_put(float* img, int ci, int ry, int rx, float v, int sb) {
-  float* d = img + (ci * FQ_PY + 2 * ry) * FQ_PX + 2 * rx;
-  *reinterpret_cast<float2*>(d) = make_float2(sb == 0 ? v : 0.f, sb == 1 ? v : 0.f);
-  *reinterpret_cast<float2*>(d + FQ_PX) = make_float2(sb == 2 ? v : 0.f, sb == 3 ? v : 0.f);
+  float* d = img + (ci * FQ_PY + 2 * ry) * FQ_PX + 2 * rx + 1;
+  d[0] = sb == 0 ? v : 0.f;
+  d[1] = sb == 1 ? v : 0.f;
+  d[FQ_PX] = sb == 2 ? v : 0.f;
+  d[FQ_PX + 1] = sb == 3 ? v : 0.f;
 }
 
 __global__ __launch_bounds__(256) void first_layer_bwd_pooled_kernel(const float* __restrict__ g,
@@ -427,6 +432,7 @@ __global__ __launch_bounds__(256) void first_layer_bwd_pooled_kernel(const float
   const bool hact = tid < 2 * FQ_RY * FQ_C;
   float v[FQ_NS];
   int sb[FQ_NS];
+  // loads are unconditional from a clamped (always valid) address and masked afterwards
   auto fetch = [&](int c0) {
     const int cx = qx0 + lane;
 #pragma unroll
@@ -435,16 +441,20 @@ __global__ __launch_bounds__(256) void first_layer_bwd_pooled_kernel(const float
       for (int k = 0; k < FQ_KR; ++k) {
         const int ry = wv4 + 4 * k, cy = qy0 - 1 + ry, c = c0 + ci;
         const bool ok = ry < FQ_RY && c < C && cy >= 0 && cy < H2 && cx < W2;
-        const size_t o = c * plane + (size_t)cy * W2 + cx;
-        v[ci * FQ_KR + k] = ok ? gb[o] : 0.f;
-        sb[ci * FQ_KR + k] = ok ? (int)ab[o] : 4;
+        const size_t o = ok ? c * plane + (size_t)cy * W2 + cx : 0;
+        const float gv = gb[o];
+        const int av = (int)ab[o];
+        v[ci * FQ_KR + k] = ok ? gv : 0.f;
+        sb[ci * FQ_KR + k] = ok ? av : 4;
       }
     {
       const int c = c0 + hci, cy = qy0 - 1 + hry, cxh = qx0 - 1 + hrx;
       const bool ok = hact && c < C && cy >= 0 && cy < H2 && cxh >= 0 && cxh < W2;
-      const size_t o = c * plane + (size_t)cy * W2 + cxh;
-      v[FQ_NS - 1] = ok ? gb[o] : 0.f;
-      sb[FQ_NS - 1] = ok ? (int)ab[o] : 4;
+      const size_t o = ok ? c * plane + (size_t)cy * W2 + cxh : 0;
+      const float gv = gb[o];
+      const int av = (int)ab[o];
+      v[FQ_NS - 1] = ok ? gv : 0.f;
+      sb[FQ_NS - 1] = ok ? av : 4;
     }
   };
   auto stage = [&]() {
@@ -457,34 +467,33 @@ __global__ __launch_bounds__(256) void first_layer_bwd_pooled_kernel(const float
       }
     if (hact) fq_put(img, hci, hry, hrx, v[FQ_NS - 1], sb[FQ_NS - 1]);
   };
-  float acc[4][4];
+  fq2 acc[4][2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = fq2{0.f, 0.f};
   fetch(0);
   for (int c0 = 0; c0 < C; c0 += FQ_C) {
     __syncthreads();
     stage();
     __syncthreads();
     if (c0 + FQ_C < C) fetch(c0 + FQ_C);
-#pragma unroll 1
+#pragma unroll
     for (int ci = 0; ci < FQ_C; ++ci) {
       const int c = c0 + ci;
       float wv[9];
 #pragma unroll
       for (int t = 0; t < 9; ++t) wv[t] = (c < C) ? w2[c * 9 + t] : 0.f;
-      // patch P[i][j] = pixel (2qy0 + 4ty - 1 + i, 2qx0 + 4tx - 1 + j) = img[4ty + 1 + i][4tx + 1 + j]
-      float P[6][6];
-      const float* base = img + (ci * FQ_PY + 4 * ty + 1) * FQ_PX + 4 * tx;
+      // patch P[i][j] = pixel (2qy0 + 4ty - 1 + i, 2qx0 + 4tx - 1 + j) = img[4ty + 1 + i][4tx + 2 + j];
+      // pair q (q = 0..4) = (P[i][q], P[i][q + 1])
+      fq2 pr[6][5];
+      const float* base = img + (ci * FQ_PY + 4 * ty + 1) * FQ_PX + 4 * tx + 2;
 #pragma unroll
       for (int i = 0; i < 6; ++i) {
         const float* r = base + i * FQ_PX;
-        const float2 a0 = *reinterpret_cast<const float2*>(r);
-        const float2 a1 = *reinterpret_cast<const float2*>(r + 2);
-        const float2 a2 = *reinterpret_cast<const float2*>(r + 4);
-        const float2 a3 = *reinterpret_cast<const float2*>(r + 6);
-        P[i][0] = a0.y; P[i][1] = a1.x; P[i][2] = a1.y; P[i][3] = a2.x; P[i][4] = a2.y; P[i][5] = a3.x;
+        pr[i][0] = *reinterpret_cast<const fq2*>(r);
+        pr[i][2] = *reinterpret_cast<const fq2*>(r + 2);
+        pr[i][4] = *reinterpret_cast<const fq2*>(r + 4);
+        pr[i][1] = fq2{r[1], r[2]};
+        pr[i][3] = fq2{r[3], r[4]};
       }
 #pragma unroll
       for (int py = 0; py < 4; ++py)
@@ -493,8 +502,9 @@ __global__ __launch_bounds__(256) void first_layer_bwd_pooled_kernel(const float
 #pragma unroll
           for (int dx = -1; dx <= 1; ++dx) {
             const float w = wv[(1 - dy) * 3 + (1 - dx)];
-#pragma unroll
-            for (int px = 0; px < 4; ++px) acc[py][px] = fmaf(P[py + 1 + dy][px + 1 + dx], w, acc[py][px]);
+            const fq2 ww = fq2{w, w};
+            acc[py][0] = __builtin_elementwise_fma(pr[py + 1 + dy][1 + dx], ww, acc[py][0]);
+            acc[py][1] = __builtin_elementwise_fma(pr[py + 1 + dy][3 + dx], ww, acc[py][1]);
           }
     }
   }
@@ -504,7 +514,7 @@ __global__ __launch_bounds__(256) void first_layer_bwd_pooled_kernel(const float
     for (int py = 0; py < 4; ++py) {
       if (oy + py < H)
         *reinterpret_cast<float4*>(out + ((size_t)bq * H + oy + py) * W + ox) =
-            make_float4(acc[py][0], acc[py][1], acc[py][2], acc[py][3]);
+            make_float4(acc[py][0].x, acc[py][0].y, acc[py][1].x, acc[py][1].y);
     }
   }
 }
