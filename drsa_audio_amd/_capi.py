@@ -12,7 +12,7 @@ from typing import Optional
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libdrsa_amd.so")
+LIB_PATH = os.environ.get("DRSA_AMD_LIB") or os.path.join(_HERE, "lib", "libdrsa_amd.so")
 
 _lib: Optional[C.CDLL] = None
 

@@ -394,7 +394,10 @@ __global__ __launch_bounds__(256) void first_layer_bwd_kernel(const float* __res
 // channel as five pixel pairs per row and runs packed fmas (v_pk_fma_f32: two output pixels
 // per instruction) in the dense chain order (channel, dy, dx) — the chain of the dense kernel
 // above and of oracle/lrp_exact.c (the zero terms included: fma(0, w, acc) == acc).
-constexpr int FQ_Y = 16, FQ_X = 64, FQ_C = 2;
+#ifndef DRSA_FQ_C
+#define DRSA_FQ_C 1
+#endif
+constexpr int FQ_Y = 16, FQ_X = 64, FQ_C = DRSA_FQ_C;
 constexpr int FQ_RY = FQ_Y + 2, FQ_RX = FQ_X + 2;            // cells incl. halo
 constexpr int FQ_PY = 2 * FQ_RY, FQ_PX = 2 * FQ_RX + 4;      // pixel image (row pad 4)
 constexpr int FQ_KR = (FQ_RY + 3) / 4;                       // row passes of 4 waves
