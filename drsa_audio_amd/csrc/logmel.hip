@@ -17,6 +17,8 @@
 #include "common.h"
 #include "drsa_amd.h"
 
+#include <stdlib.h>
+
 namespace {
 
 constexpr int LM_WAVES = 8;
@@ -248,6 +250,233 @@ __global__ __launch_bounds__(LM_THREADS) void logmel_kernel(LogmelArgs a) {
   }
 }
 
+// ===========================================================================
+// Fast path for n_fft = 800 (GTZAN, AUDIO_PARAMS['gtzan']): the 400-point complex FFT of a
+// frame as 20 x 20 (n = 20 n1 + n2, k = k1 + 20 k2), each 20-point DFT in registers (4 x 5).
+// Three frames per wave, one lane per (frame, n2) in pass A and per (frame, k1) in pass B
+// (60 of 64 lanes busy): two LDS hand-offs per frame instead of the generic kernel's
+// Stockham stages.  Samples come straight from global memory (frames overlap 55 %, served by
+// L1/L2); one workgroup per chunk keeps the peak division and the coalesced output rows.
+// ===========================================================================
+constexpr int LF_M = 400, LF_R = 20, LF_FPW = 3;   // complex points, radix, frames per wave
+// T layout: pass-A rows k1 at stride LF_RS = 21 (pass-B lanes k1 read a row each: 42-bank
+// stride, conflict-free); frames at LF_FS = 421 complex
+constexpr int LF_RS = 21, LF_FS = 421;
+#ifndef LF_UNROLL_MEL
+#define LF_UNROLL_MEL 0
+#endif
+#ifndef LF_VEC_LOADS
+#define LF_VEC_LOADS 0
+#endif
+constexpr int LF_MAXB = 20;                          // unrolled mel band width (wider: loop)
+
+__device__ __constant__ cf kW20[13] = {
+    {1.0f, 0.0f},
+    {9.51056516295153531e-01f, -3.09016994374947396e-01f},
+    {8.09016994374947451e-01f, -5.87785252292473137e-01f},
+    {5.87785252292473137e-01f, -8.09016994374947451e-01f},
+    {3.09016994374947451e-01f, -9.51056516295153531e-01f},
+    {0.0f, -1.0f},
+    {-3.09016994374947340e-01f, -9.51056516295153642e-01f},
+    {-5.87785252292473026e-01f, -8.09016994374947451e-01f},
+    {-8.09016994374947340e-01f, -5.87785252292473248e-01f},
+    {-9.51056516295153531e-01f, -3.09016994374947507e-01f},
+    {-1.0f, 0.0f},
+    {-9.51056516295153753e-01f, 3.09016994374946896e-01f},
+    {-8.09016994374947562e-01f, 5.87785252292473026e-01f}};
+
+// forward 20-point DFT in place: v[n] -> v[k] (4 x 5: n = 5 n1 + n2, k = k1 + 4 k2)
+__device__ __forceinline__ void dft20(cf* v) {
+  cf y[4][5];
+#pragma unroll
+  for (int n2 = 0; n2 < 5; ++n2) {
+    cf t[4] = {v[n2], v[5 + n2], v[10 + n2], v[15 + n2]};
+    bfly4(t);
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) y[k1][n2] = (n2 * k1 == 0) ? t[k1] : cmul(t[k1], kW20[n2 * k1]);
+  }
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) {
+    bfly5(y[k1]);
+#pragma unroll
+    for (int k2 = 0; k2 < 5; ++k2) v[k1 + 4 * k2] = y[k1][k2];
+  }
+}
+
+__global__ __launch_bounds__(LM_THREADS) void logmel800_kernel(LogmelArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int chunk = blockIdx.x;
+  const float* x = a.wav + (int64_t)(chunk / a.chunks_per_song) * a.song_stride +
+                   (int64_t)(chunk % a.chunks_per_song) * a.chunk_hop;
+  cf* tw = reinterpret_cast<cf*>(sm + a.o_tw);      // [k1][n2] = W_400^{n2 k1} (lanes n2 adjacent)
+  cf* ptw = reinterpret_cast<cf*>(sm + a.o_ptw);    // W_800^k, k <= 400
+  float* win = sm + a.o_win;
+  int* blo = reinterpret_cast<int*>(sm + a.o_blo);
+  int* bn = reinterpret_cast<int*>(sm + a.o_bn);
+  int* boff = reinterpret_cast<int*>(sm + a.o_boff);
+  float* bw = sm + a.o_bw;
+  cf* T = reinterpret_cast<cf*>(sm + a.o_fft) + (size_t)w * LF_FPW * LF_FS;  // [3][LF_FS] per wave
+  float* mel = sm + a.o_mel;
+  float* red = sm + a.o_red;
+
+  for (int j = tid; j < LF_M; j += LM_THREADS) {
+    double s, c;
+    const int e = ((j / LF_R) * (j % LF_R)) % LF_M;
+    sincospi(2.0 * (double)e / (double)LF_M, &s, &c);
+    tw[j] = {(float)c, (float)-s};
+  }
+  for (int k = tid; k <= LF_M; k += LM_THREADS) {
+    double s, c;
+    sincospi((double)k / (double)LF_M, &s, &c);
+    ptw[k] = {(float)c, (float)-s};
+  }
+  for (int i = tid; i < 800; i += LM_THREADS) win[i] = a.window[i];
+  for (int m = tid; m < a.n_mels; m += LM_THREADS) {
+    blo[m] = a.band_lo[m];
+    bn[m] = a.band_n[m];
+    boff[m] = a.band_off[m];
+  }
+  for (int i = tid; i < a.nnz; i += LM_THREADS) bw[i] = a.band_w[i];
+  __syncthreads();
+
+  const int fl = lane / LF_R, q = lane % LF_R;       // frame slot in the wave, n2 / k1
+  const bool lact = lane < LF_FPW * LF_R;
+  float pk = 0.f;
+  constexpr int FPR = LM_WAVES * LF_FPW;             // frames per workgroup round
+  for (int tb = 0; tb < a.width; tb += FPR) {
+    const int fi = tb + w * LF_FPW + fl;             // frame slot index in [0, width)
+    const bool fok = lact && fi < a.width;
+    cf v[LF_R];
+    // ---- pass A: lane (frame, n2) loads z[20 n1 + n2] = x[2n] w[2n] + i x[2n+1] w[2n+1] ----
+    {
+      const int base = (a.frame0 + (fok ? fi : 0)) * a.hop - 400;
+      if (LF_VEC_LOADS && base >= 0 && base + 800 <= a.L && ((base + (int)((uintptr_t)x >> 2)) & 1) == 0) {
+        // interior frame, 8-byte aligned pairs: one float2 load per n1
+        const float2* xp = reinterpret_cast<const float2*>(x + base) + q;
+#pragma unroll
+        for (int n1 = 0; n1 < LF_R; ++n1) {
+          const float2 xv = xp[20 * n1];
+          const int s0 = 40 * n1 + 2 * q;
+          pk = fok ? fmaxf(pk, fmaxf(fabsf(xv.x), fabsf(xv.y))) : pk;
+          v[n1] = {xv.x * win[s0], xv.y * win[s0 + 1]};
+        }
+      } else {
+#pragma unroll
+        for (int n1 = 0; n1 < LF_R; ++n1) {
+          const int s0 = 40 * n1 + 2 * q;
+          int j0 = base + s0, j1 = base + s0 + 1;
+          j0 = j0 < 0 ? -j0 : j0;
+          j0 = j0 >= a.L ? 2 * (a.L - 1) - j0 : j0;
+          j1 = j1 < 0 ? -j1 : j1;
+          j1 = j1 >= a.L ? 2 * (a.L - 1) - j1 : j1;
+          const float x0 = x[j0], x1 = x[j1];
+          pk = fok ? fmaxf(pk, fmaxf(fabsf(x0), fabsf(x1))) : pk;
+          v[n1] = {x0 * win[s0], x1 * win[s0 + 1]};
+        }
+      }
+      dft20(v);
+      // twiddle W_400^{n2 k1}, store T[k1][n2]
+#pragma unroll
+      for (int k1 = 0; k1 < LF_R; ++k1) {
+        const cf t = (k1 == 0) ? v[0] : cmul(v[k1], tw[k1 * LF_R + q]);
+        if (lact) T[fl * LF_FS + k1 * LF_RS + q] = t;
+      }
+    }
+    wave_lds_sync();
+    // ---- pass B: lane (frame, k1) reads T[k1][n2], DFT over n2 -> Z[k1 + 20 k2] ----
+    if (lact) {
+#pragma unroll
+      for (int n2 = 0; n2 < LF_R; ++n2) v[n2] = T[fl * LF_FS + q * LF_RS + n2];
+    }
+    dft20(v);
+    wave_lds_sync();
+    if (lact) {
+#pragma unroll
+      for (int k2 = 0; k2 < LF_R; ++k2) T[fl * LF_FS + q + LF_R * k2] = v[k2];
+    }
+    wave_lds_sync();
+    // ---- real split + |X|: 3 x 401 bins over the wave; magnitudes held in registers until
+    //      every lane has read its Z pairs, then written over T (as floats) ----
+    constexpr int NB = LF_FPW * (LF_M + 1);
+    constexpr int NIT = (NB + 63) / 64;
+    float mg[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int i = lane + 64 * it;
+      const int f = i / (LF_M + 1), k = i % (LF_M + 1);
+      float m = 0.f;
+      if (i < NB) {
+        const cf* Z = T + f * LF_FS;
+        const cf zk = Z[k == LF_M ? 0 : k];
+        const cf zr = Z[k == 0 ? 0 : LF_M - k];
+        const cf zc = {zr.x, -zr.y};
+        const cf e = cscale(cadd(zk, zc), 0.5f);
+        const cf d = csub(zk, zc);
+        const cf o = {0.5f * d.y, -0.5f * d.x};
+        const cf X = cadd(e, cmul(ptw[k], o));
+        m = sqrtf(X.x * X.x + X.y * X.y);
+      }
+      mg[it] = m;
+    }
+    wave_lds_sync();
+    float* magb = reinterpret_cast<float*>(T);      // [3][401] floats
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int i = lane + 64 * it;
+      if (i < NB) magb[i] = mg[it];
+    }
+    wave_lds_sync();
+    // ---- banded mel filters, lanes over (frame, mel) ----
+    for (int i = lane; i < LF_FPW * a.n_mels; i += 64) {
+      const int f = i / a.n_mels, m = i % a.n_mels;
+      const int t = tb + w * LF_FPW + f;
+      if (t < a.width) {
+        const float* wm = bw + boff[m];
+        const float* mgp = magb + f * (LF_M + 1) + blo[m];
+        const int nb = bn[m];
+        float acc = 0.f;
+        if (LF_UNROLL_MEL && nb <= LF_MAXB) {
+          // all band reads issued together (masked, clamped), then the ordered chain
+          float wv[LF_MAXB], mv[LF_MAXB];
+#pragma unroll
+          for (int qq = 0; qq < LF_MAXB; ++qq) {
+            const int qc = qq < nb ? qq : 0;
+            wv[qq] = wm[qc];
+            mv[qq] = mgp[qc];
+          }
+#pragma unroll
+          for (int qq = 0; qq < LF_MAXB; ++qq)
+            if (qq < nb) acc += wv[qq] * mv[qq];
+        } else {
+          for (int qq = 0; qq < nb; ++qq) acc += wm[qq] * mgp[qq];
+        }
+        mel[m * a.width + t] = acc;
+      }
+    }
+    wave_lds_sync();
+  }
+  {
+    const int c0 = max(0, a.frame0 * a.hop - 400);
+    const int c1 = min(a.L, (a.frame0 + a.width - 1) * a.hop + 400);
+    for (int i = tid; i < c0; i += LM_THREADS) pk = fmaxf(pk, fabsf(x[i]));
+    for (int i = c1 + tid; i < a.L; i += LM_THREADS) pk = fmaxf(pk, fabsf(x[i]));
+  }
+  for (int o = 32; o > 0; o >>= 1) pk = fmaxf(pk, shfl_xor(pk, o));
+  if (lane == 0) red[w] = pk;
+  __syncthreads();
+  float p = red[0];
+  for (int i = 1; i < LM_WAVES; ++i) p = fmaxf(p, red[i]);
+  const float inv_scale = a.peak_norm ? p : 1.f;
+  float* o = a.out + (size_t)chunk * a.n_mels * a.width;
+  const int total = a.n_mels * a.width;
+  for (int i = tid; i < total; i += LM_THREADS) {
+    float vv = log10f(mel[i] / inv_scale + a.log_eps);
+    if (a.do_clamp) vv = (vv < a.clamp_min) ? a.clamp_min : vv;
+    o[i] = vv;
+  }
+}
+
 int factor_radices(int M, int* r) {
   int n = 0;
   while (M % 4 == 0 && n < LM_MAX_STAGES) { r[n++] = 4; M /= 4; }
@@ -319,6 +548,8 @@ extern "C" int drsa_amd_logmel(const float* wav, int64_t n_songs, int64_t song_s
   a.log_eps = log_eps;
   a.out = out;
   const int M = n_fft / 2;
+  static const int no_fast = getenv("DRSA_AMD_LOGMEL_GENERIC") ? atoi(getenv("DRSA_AMD_LOGMEL_GENERIC")) : 0;
+  const bool fast = n_fft == 800 && !no_fast;
   int off = 0;
   auto take = [&](int n) { int o = off; off += (n + 3) & ~3; return o; };
   a.o_tw = take(2 * M);
@@ -328,15 +559,19 @@ extern "C" int drsa_amd_logmel(const float* wav, int64_t n_songs, int64_t song_s
   a.o_bn = take(n_mels);
   a.o_boff = take(n_mels);
   a.o_bw = take(band_nnz);
-  a.o_samp = take((LM_WAVES - 1) * hop + n_fft);
-  a.o_fft = take(LM_WAVES * 4 * M);
+  a.o_samp = take(fast ? 0 : (LM_WAVES - 1) * hop + n_fft);
+  a.o_fft = take(fast ? LM_WAVES * LF_FPW * 2 * LF_FS : LM_WAVES * 4 * M);
   a.o_mel = take(n_mels * width);
   a.o_red = take(LM_WAVES);
   a.smem_floats = off;
   const size_t smem = (size_t)off * 4;
   DRSA_REQUIRE(smem <= 160 * 1024, "logmel: LDS footprint %zu B exceeds 160 KB (n_mels*width too large)", smem);
-  DRSA_HIP(hipFuncSetAttribute((const void*)logmel_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
-  hipLaunchKernelGGL(logmel_kernel, dim3((unsigned)n_chunks), dim3(LM_THREADS), smem, (hipStream_t)stream, a);
+  const void* fn = fast ? (const void*)logmel800_kernel : (const void*)logmel_kernel;
+  DRSA_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+  if (fast)
+    hipLaunchKernelGGL(logmel800_kernel, dim3((unsigned)n_chunks), dim3(LM_THREADS), smem, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(logmel_kernel, dim3((unsigned)n_chunks), dim3(LM_THREADS), smem, (hipStream_t)stream, a);
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;
 }
