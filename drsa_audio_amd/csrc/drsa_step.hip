@@ -249,16 +249,21 @@ __global__ __launch_bounds__(256) void drsa_reduce_kernel(const float* __restric
 // ---------------------------------------------------------------------------
 // finish: objective, scaled gradient, V = U + G, polar(V) via Newton-Schulz
 //   X0 = a V; X <- X (1.5 I - 0.5 X^T X) until max|X^T X - I| < tol.
-//   One workgroup of 256 threads; matrices in LDS [D][D+1].
+//   One workgroup of polar_waves<D>() waves (enough to keep every SIMD's MFMA pipe fed from
+//   LDS); matrices in LDS [D][D+1].
 // ---------------------------------------------------------------------------
+template <int D>
+constexpr int polar_waves() { return D >= 128 ? 16 : (D >= 64 ? 8 : 4); }
+
 template <int D>
 __device__ void lds_matmul_tn(const float* X, const float* Y, float* Z, int ld) {
   // Z = X^T Y  (all D x D, row-major with leading dim ld), fp32 MFMA 16x16x4
-  constexpr int NB = D / 16;
+  constexpr int NB = D / 16, NW = polar_waves<D>();
   const int lane = lane_id(), w = wave_id();
-  for (int t = w; t < NB * NB; t += 4) {
+  for (int t = w; t < NB * NB; t += NW) {
     const int ib = t / NB, jb = t % NB;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
     for (int k0 = 0; k0 < D; k0 += 4) {
       const int kk = k0 + (lane >> 4);
       acc = mfma16(X[kk * ld + 16 * ib + (lane & 15)], Y[kk * ld + 16 * jb + (lane & 15)], acc);
@@ -271,16 +276,17 @@ template <int D>
 __device__ void lds_matmul_nn_inplace(float* X, const float* Y, int ld) {
   // X <- X Y.  Each wave keeps its output tiles in registers until every wave has
   // finished reading X, then overwrites X (saves a third D x D LDS matrix).
-  constexpr int NB = D / 16;
-  constexpr int NT = (NB * NB + 3) / 4;
+  constexpr int NB = D / 16, NW = polar_waves<D>();
+  constexpr int NT = (NB * NB + NW - 1) / NW;
   const int lane = lane_id(), w = wave_id();
   f32x4 acc[NT];
 #pragma unroll
   for (int q = 0; q < NT; ++q) {
     acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int t = w + 4 * q;
+    const int t = w + NW * q;
     if (t >= NB * NB) break;
     const int ib = t / NB, jb = t % NB;
+#pragma unroll 8
     for (int k0 = 0; k0 < D; k0 += 4) {
       const int kk = k0 + (lane >> 4);
       acc[q] = mfma16(X[(16 * ib + (lane & 15)) * ld + kk], Y[kk * ld + 16 * jb + (lane & 15)], acc[q]);
@@ -289,7 +295,7 @@ __device__ void lds_matmul_nn_inplace(float* X, const float* Y, int ld) {
   __syncthreads();
 #pragma unroll
   for (int q = 0; q < NT; ++q) {
-    const int t = w + 4 * q;
+    const int t = w + NW * q;
     if (t >= NB * NB) break;
     const int ib = t / NB, jb = t % NB;
     for (int r = 0; r < 4; ++r) X[(16 * ib + (lane >> 4) * 4 + r) * ld + 16 * jb + (lane & 15)] = acc[q][r];
@@ -363,7 +369,7 @@ __device__ void polar_ns(float* X, float* P, float* scratch, float tol, int max_
 
 // mode 0: full step (f, U_out = polar(U + G)); mode 1: objective only
 template <int D>
-__global__ __launch_bounds__(256) void drsa_finish_kernel(
+__global__ __launch_bounds__(polar_waves<D>() * 64) void drsa_finish_kernel(
     const float* __restrict__ gs, double n_total, int K, const float* __restrict__ U,
     float* __restrict__ U_out, float* __restrict__ f_out, int* __restrict__ step_counter,
     int f_stride_by_counter, int mode, float tol, int max_iter, int* __restrict__ iters_out) {
@@ -408,7 +414,7 @@ __global__ __launch_bounds__(256) void drsa_finish_kernel(
 
 // polar only (orthogonalize API)
 template <int D>
-__global__ __launch_bounds__(256) void polar_kernel(const float* __restrict__ V, float* __restrict__ U_out,
+__global__ __launch_bounds__(polar_waves<D>() * 64) void polar_kernel(const float* __restrict__ V, float* __restrict__ U_out,
                                                     float tol, int max_iter, int* iters_out) {
   constexpr int ld = D + 1;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -561,7 +567,7 @@ int launch_finish(const float* gs, double n_total, int K, const float* U, float*
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr_set = true;
   }
-  hipLaunchKernelGGL(drsa_finish_kernel<D>, dim3(1), dim3(256), lds, s, gs, n_total, K, U, U_out, f_out,
+  hipLaunchKernelGGL(drsa_finish_kernel<D>, dim3(1), dim3(polar_waves<D>() * 64), lds, s, gs, n_total, K, U, U_out, f_out,
                      counter, by_counter, mode, tol, max_iter, iters);
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;
@@ -853,7 +859,7 @@ int drsa_amd_polar(const float* V, int d, float* U_out, int* iters_out, void* st
                                    (int)lds));
       set = true;
     }
-    hipLaunchKernelGGL(polar_kernel<D>, dim3(1), dim3(256), lds, s, V, U_out, kPolarTol, kPolarMaxIter,
+    hipLaunchKernelGGL(polar_kernel<D>, dim3(1), dim3(polar_waves<D>() * 64), lds, s, V, U_out, kPolarTol, kPolarMaxIter,
                        iters_out);
     DRSA_LAUNCH_CHECK();
     return DRSA_OK;
