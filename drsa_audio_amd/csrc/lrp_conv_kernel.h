@@ -29,6 +29,15 @@
 #ifndef DRSA_CONV_PD_BWD
 #define DRSA_CONV_PD_BWD 2
 #endif
+#ifndef DRSA_CONV_BWD_ES
+#define DRSA_CONV_BWD_ES 1
+#endif
+#ifndef DRSA_CONV_BWD_WPE
+#define DRSA_CONV_BWD_WPE 3
+#endif
+#ifndef DRSA_CONV_FWD_WPE
+#define DRSA_CONV_FWD_WPE 1
+#endif
 
 namespace drsa_conv {
 
@@ -75,12 +84,18 @@ struct ConvCfg {
   static constexpr int KCP = round_up<KC, 2>();
   static constexpr int NCHUNK = CIN / CIC;
   static constexpr int TWP = (TW == 32) ? 48 : TW;          // epilogue tile row stride (conflict-free writes)
-  static constexpr int TCH = WN * 32;                          // channels staged per epilogue pass
+  // backward epilogue in ES channel passes (halves the epilogue LDS and registers; WN == 1 only)
+  // small-chunk rule backward (CIC <= 8, 32 output channels): 24.6 KB LDS and <= 128 VGPRs, so
+  // 4 workgroups (16 waves) per CU
+  static constexpr bool SMALL_BWD = EPI == EPI_BWD && NG == 1 && CIC <= 8 && COUT <= 32;
+  static constexpr int ES = (EPI == EPI_BWD && WN == 1) ? (SMALL_BWD ? 2 : DRSA_CONV_BWD_ES) : 1;
+  static constexpr int TCH = WN * 32 / ES;                     // channels staged per epilogue pass
   static constexpr size_t staging_floats = (size_t)CIC * PLANE + (size_t)NG * KCP * COUT;
   static constexpr size_t epi_floats = (size_t)TCH * TH * TWP;
   static constexpr size_t lds_floats = staging_floats > epi_floats ? staging_floats : epi_floats;
   // minimum waves per SIMD the register allocation must allow (1 block = 1 wave per SIMD)
-  static constexpr int WPE = (EPI == EPI_BWD && NG == 1) ? 3 : 1;
+  static constexpr int WPE = (EPI == EPI_BWD && NG == 1) ? (SMALL_BWD ? 4 : DRSA_CONV_BWD_WPE)
+                             : (EPI != EPI_BWD && CIC <= 8 ? DRSA_CONV_FWD_WPE : 1);
   // operand prefetch distance of the MFMA loop (k-steps)
   static constexpr int PD = DRSA_CONV_PD_BWD > 0 && EPI == EPI_BWD ? DRSA_CONV_PD_BWD : 1;
   static_assert(TH % MTH == 0 && TW % MTW == 0, "tile must be a multiple of the M-tile");
@@ -414,20 +429,30 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
   constexpr int NCELL = TCH * (TH / 2) * (TW / 2);
   constexpr int CT = (NCELL + kThreads - 1) / kThreads;
   float* T = smem;
-  auto stage = [&](int v, auto valfn) {
+  constexpr int ES = Cfg::ES;
+  static_assert(ES == 1 || ES == 2, "epilogue split must be 1 or 2");
+  // pass `sub` of ES stages the registers whose channel lies in [sub*TCH, (sub+1)*TCH)
+  // (ES = 2: r >> 3 == sub, since channel = (r&3) + 8(r>>2) + 4h)
+  auto stage = [&](int v, auto valfn, int sub = 0) {
     __syncthreads();
     if (active) {
 #pragma unroll
       for (int u = 0; u < MPW; ++u)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int cl = wn * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          T[(cl * TH + pix_y[u]) * TWP + pix_x[u]] = valfn(u, r);
+          const int cf = (r & 3) + 8 * (r >> 2) + 4 * h;
+          if constexpr (ES == 1) {
+            T[((wn * 32 + cf) * TH + pix_y[u]) * TWP + pix_x[u]] = valfn(u, r);
+          } else {
+            if ((r >> 3) == sub) T[((cf - TCH * sub) * TH + pix_y[u]) * TWP + pix_x[u]] = valfn(u, r);
+          }
         }
     }
     __syncthreads();
   };
   auto gch = [&](int cl, int v) { return ((cl >> 5) * NPW + v) * 32 + (cl & 31); };   // global channel
+  // global channel of staged row cl in pass sub (ES = 2 implies WN = 1)
+  auto gchs = [&](int cl, int v, int sub) { return ES == 1 ? gch(cl, v) : v * 32 + sub * TCH + cl; };
 #pragma unroll
   for (int v = 0; v < NPW; ++v) {
     if constexpr (EPI == EPI_FWD_POOL || EPI == EPI_FWD_RELU) {
@@ -563,8 +588,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
         }
       }
     } else {   // EPI_BWD: R = xmode(acc, x) -> post -> out
+     for (int sub = 0; sub < ES; ++sub) {
       float4 Rk[V4T];
-      stage(v, [&](int u, int r) { return acc[0][u][v][r]; });
+      stage(v, [&](int u, int r) { return acc[0][u][v][r]; }, sub);
 #pragma unroll
       for (int it = 0; it < V4T; ++it) {
         const int i = tid + it * kThreads;
@@ -572,7 +598,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
         if (i < NV4) {
           const int cl = i / (TH * TW / 4), rem = i % (TH * TW / 4);
           const int py = rem / (TW / 4), px = (rem % (TW / 4)) * 4;
-          const int co = gch(cl, v);
+          const int co = gchs(cl, v, sub);
           if (co < a.cout && ty0 + py < H && tx0 + px < W) {
             const float4 t = *reinterpret_cast<const float4*>(T + (cl * TH + py) * TWP + px);
             if (a.xmode == XM_NONE || (a.dbg & 2)) {
@@ -591,14 +617,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
       }
       if constexpr (NG >= 2) {
         if (a.xmode == XM_SPLIT) {
-          stage(v, [&](int u, int r) { return acc[1][u][v][r]; });
+          stage(v, [&](int u, int r) { return acc[1][u][v][r]; }, sub);
 #pragma unroll
           for (int it = 0; it < V4T; ++it) {
             const int i = tid + it * kThreads;
             if (i < NV4) {
               const int cl = i / (TH * TW / 4), rem = i % (TH * TW / 4);
               const int py = rem / (TW / 4), px = (rem % (TW / 4)) * 4;
-              const int co = gch(cl, v);
+              const int co = gchs(cl, v, sub);
               if (co < a.cout && ty0 + py < H && tx0 + px < W) {
                 const float4 t = *reinterpret_cast<const float4*>(T + (cl * TH + py) * TWP + px);
                 const float4 x = *reinterpret_cast<const float4*>(a.x + (((size_t)bs * a.cout + co) * H + ty0 + py) * W + tx0 + px);
@@ -617,7 +643,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
         if (i < NV4) {
           const int cl = i / (TH * TW / 4), rem = i % (TH * TW / 4);
           const int py = rem / (TW / 4), px = (rem % (TW / 4)) * 4;
-          const int co = gch(cl, v);
+          const int co = gchs(cl, v, sub);
           if (co < a.cout && ty0 + py < H && tx0 + px < W) {
             const size_t os = (((size_t)bs * a.cout + co) * H + ty0 + py) * W + tx0 + px;
             const size_t oq = (((size_t)bq * a.cout + co) * H + ty0 + py) * W + tx0 + px;
@@ -644,6 +670,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
           }
         }
       }
+     }
     }
   }
 }

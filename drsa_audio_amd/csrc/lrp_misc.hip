@@ -202,6 +202,12 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
 // Tiles of 64 pixels (RPT rows x TW cols), lanes = pixels; one tile per workgroup.
 // ===========================================================================
 constexpr int PT_BWD = 1;   // tiles per workgroup (backward): one tile, many workgroups
+#ifndef PROJ_STAGE_UNROLL
+#define PROJ_STAGE_UNROLL 1
+#endif
+#ifndef PROJ_CLONE_UNROLL
+#define PROJ_CLONE_UNROLL 1
+#endif
 
 template <int D>
 __global__ __launch_bounds__(256) void projection_bwd_kernel(
@@ -247,6 +253,7 @@ __global__ __launch_bounds__(256) void projection_bwd_kernel(
     __syncthreads();
     if (t == 0)
       for (int i = tid; i < D * D; i += 256) Us[(i / D) * LD + i % D] = U[i];
+#pragma unroll PROJ_STAGE_UNROLL
     for (int i = tid; i < D * P; i += 256) {
       const int c = i / P, p = i % P;
       const int y = y0 + p / TW, x = x0 + p % TW;
@@ -290,6 +297,7 @@ __global__ __launch_bounds__(256) void projection_bwd_kernel(
       for (int i = 0; i < QW; ++i) {
         const int cb = i, pb = w;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll PROJ_CLONE_UNROLL
         for (int k0 = j0; k0 < j1; k0 += 4) {
           const int j = k0 + (lane >> 4);
           const bool ok = j < j1;
