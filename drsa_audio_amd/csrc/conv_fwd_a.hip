@@ -3,7 +3,7 @@
 #include "lrp_conv_kernel.h"
 
 #ifndef DRSA_CONV_CIC_FWD32
-#define DRSA_CONV_CIC_FWD32 16
+#define DRSA_CONV_CIC_FWD32 8
 #endif
 
 namespace drsa_conv {
