@@ -95,7 +95,7 @@ struct ConvCfg {
   static constexpr size_t lds_floats = staging_floats > epi_floats ? staging_floats : epi_floats;
   // minimum waves per SIMD the register allocation must allow (1 block = 1 wave per SIMD)
   static constexpr int WPE = (EPI == EPI_BWD && NG == 1) ? (SMALL_BWD ? 4 : DRSA_CONV_BWD_WPE)
-                             : (EPI != EPI_BWD && CIC <= 8 && COUT <= 32 ? DRSA_CONV_FWD_WPE : 1);
+                             : (EPI != EPI_BWD && CIC <= 8 && COUT <= 32 && NG <= 2 ? DRSA_CONV_FWD_WPE : 1);
   // operand prefetch distance of the MFMA loop (k-steps)
   static constexpr int PD = DRSA_CONV_PD_BWD > 0 && EPI == EPI_BWD ? DRSA_CONV_PD_BWD : 1;
   static_assert(TH % MTH == 0 && TW % MTW == 0, "tile must be a multiple of the M-tile");
