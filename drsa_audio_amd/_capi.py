@@ -30,6 +30,7 @@ SIGNATURES = {
     "drsa_amd_drsa_objective": (_i32, [_fp, _fp, _i64, _i32, _i32, _fp, _fp, _vp, _sz, _vp]),
     "drsa_amd_drsa_run": (_i32, [_fp, _fp, _i64, _i32, _i32, _fp, _fp, _i32, _fp, _ip, _vp, _sz, _i32, _vp]),
     "drsa_amd_drsa_run_multi": (_i32, [_i32, _vp, _i32, _i32, _vp]),
+    "drsa_amd_drsa_partial_bf16": (_i32, [_vp, _vp, _i64, _i32, _i32, _fp, _fp, _vp, _sz, _vp]),
     "drsa_amd_polar": (_i32, [_fp, _i32, _fp, _ip, _vp]),
     "drsa_amd_subspace_relevances": (_i32, [_fp, _fp, _i64, _i64, _i32, _i32, _fp, _fp, _vp]),
     "drsa_amd_conv_weight_floats": (_sz, [_i32, _i32, _i32]),
@@ -59,7 +60,7 @@ SIGNATURES = {
 class DrsaProblem(C.Structure):
     """drsa_amd_problem_t (include/drsa_amd.h)."""
     _fields_ = [("A", _vp), ("C", _vp), ("N", _i64), ("d", _i32), ("K", _i32), ("U_io", _vp), ("U_tmp", _vp),
-                ("f_traj", _vp), ("counter", _vp), ("ws", _vp), ("ws_size", _sz)]
+                ("f_traj", _vp), ("counter", _vp), ("ws", _vp), ("ws_size", _sz), ("dtype", _i32)]
 
 
 XM_NONE, XM_MUL, XM_SPLIT = 0, 1, 2

@@ -60,6 +60,17 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
+// bf16-input MFMA, 16x16x32 (gfx950), fp32 accumulate.
+//   A operand: lane l holds A[i = l&15][k = 8(l>>4) + j], j < 8 (bf16 bit patterns)
+//   B operand: lane l holds B[k = 8(l>>4) + j][col = l&15]
+//   C/D:       as mfma16
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x4 mfma16_bf16(u16x8 a, u16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
+                                                 0, 0, 0);
+}
+
 // zennit Stabilizer: t + eps * (sign(t) + [t == 0])
 __device__ __forceinline__ float stab(float t, float eps) {
   float sgn = (t > 0.f) ? 1.f : ((t < 0.f) ? -1.f : 0.f);

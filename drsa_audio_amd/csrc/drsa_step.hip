@@ -56,15 +56,23 @@ struct PartialCfg {
   static constexpr size_t lds_floats = (size_t)D * D + 4 * (size_t)RT * LDA;
 };
 
-template <int D, int DK>
+// BF: A and C are bf16 in HBM (C5: "bf16 MFMA projection with fp32 accumulate"); GEMM1
+// (XA = A U, XC = C U) runs on v_mfma_f32_16x16x32_bf16 with U rounded to bf16 (RNE) once per
+// step; everything after it (relu, S, P/Q, GEMM2 on the exactly widened A/C, slab) is fp32.
+template <int D, int DK, bool BF>
 __global__ __launch_bounds__(kThreads) void drsa_partial_kernel(
-    const float* __restrict__ A, const float* __restrict__ C, int64_t N,
+    const void* __restrict__ A_, const void* __restrict__ C_, int64_t N,
     const float* __restrict__ U, float* __restrict__ partials, int64_t tiles_per_wg) {
   using Cfg = PartialCfg<D>;
   constexpr int RT = Cfg::RT, NB = Cfg::NB, WR = Cfg::WR, NBW = Cfg::NBW, LDA = Cfg::LDA, IB = Cfg::IB;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* Us = smem;
-  float* As = Us + D * D;
+  const float* A = reinterpret_cast<const float*>(A_);
+  const float* C = reinterpret_cast<const float*>(C_);
+  const uint16_t* Ab = reinterpret_cast<const uint16_t*>(A_);
+  const uint16_t* Cb = reinterpret_cast<const uint16_t*>(C_);
+  float* Us = smem;                                            // fp32 U [D][D]  (BF: bf16 U^T [D][D])
+  uint16_t* Ubt = reinterpret_cast<uint16_t*>(smem);
+  float* As = Us + (BF ? D * D / 2 : D * D);
   float* Cs = As + RT * LDA;
   float* Ps = Cs + RT * LDA;
   float* Qs = Ps + RT * LDA;
@@ -73,7 +81,15 @@ __global__ __launch_bounds__(kThreads) void drsa_partial_kernel(
   const int rb = w % WR, cg = w / WR;
   constexpr int K = D / DK;
 
-  for (int i = tid; i < D * D; i += kThreads) Us[i] = U[i];
+  if constexpr (BF) {
+    for (int i = tid; i < D * D; i += kThreads) {     // Ubt[c][k] = bf16_rne(U[k][c])
+      const int c = i / D, k = i % D;
+      const uint32_t u = __float_as_uint(U[k * D + c]);
+      Ubt[i] = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+    }
+  } else {
+    for (int i = tid; i < D * D; i += kThreads) Us[i] = U[i];
+  }
 
   f32x4 g[IB][NB];
 #pragma unroll
@@ -97,8 +113,17 @@ __global__ __launch_bounds__(kThreads) void drsa_partial_kernel(
       const int row = (i * 4) / D, col = (i * 4) % D;
       float4 a = make_float4(0.f, 0.f, 0.f, 0.f), c = a;
       if (r0 + row < N) {
-        a = *reinterpret_cast<const float4*>(A + (r0 + row) * D + col);
-        c = *reinterpret_cast<const float4*>(C + (r0 + row) * D + col);
+        if constexpr (BF) {   // 4 bf16 -> 4 fp32 (exact)
+          const uint2 ua = *reinterpret_cast<const uint2*>(Ab + (r0 + row) * D + col);
+          const uint2 uc = *reinterpret_cast<const uint2*>(Cb + (r0 + row) * D + col);
+          a = make_float4(__uint_as_float(ua.x << 16), __uint_as_float(ua.x & 0xffff0000u),
+                          __uint_as_float(ua.y << 16), __uint_as_float(ua.y & 0xffff0000u));
+          c = make_float4(__uint_as_float(uc.x << 16), __uint_as_float(uc.x & 0xffff0000u),
+                          __uint_as_float(uc.y << 16), __uint_as_float(uc.y & 0xffff0000u));
+        } else {
+          a = *reinterpret_cast<const float4*>(A + (r0 + row) * D + col);
+          c = *reinterpret_cast<const float4*>(C + (r0 + row) * D + col);
+        }
       }
       float* pa = As + row * LDA + col;
       float* pc = Cs + row * LDA + col;
@@ -111,16 +136,36 @@ __global__ __launch_bounds__(kThreads) void drsa_partial_kernel(
 #pragma unroll
     for (int q = 0; q < NBW; ++q) { xa[q] = f32x4{0.f, 0.f, 0.f, 0.f}; xc[q] = xa[q]; }
     const int arow = 16 * rb + (lane & 15);
-#pragma unroll 4
-    for (int k0 = 0; k0 < D; k0 += 4) {
-      const int kk = k0 + (lane >> 4);
-      const float av = As[arow * LDA + kk];
-      const float cv = Cs[arow * LDA + kk];
+    if constexpr (BF) {
+      // lane: A[row][k0 + 8(lane>>4) + j], U^T[col][k0 + 8(lane>>4) + j], j < 8
 #pragma unroll
-      for (int q = 0; q < NBW; ++q) {
-        const float bv = Us[kk * D + 16 * (cg * NBW + q) + (lane & 15)];
-        xa[q] = mfma16(av, bv, xa[q]);
-        xc[q] = mfma16(cv, bv, xc[q]);
+      for (int k0 = 0; k0 < D; k0 += 32) {
+        const int kb = k0 + 8 * (lane >> 4);
+        u16x8 ab, cb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {   // widened bf16 values: the top 16 bits are exact
+          ab[j] = (uint16_t)(__float_as_uint(As[arow * LDA + kb + j]) >> 16);
+          cb[j] = (uint16_t)(__float_as_uint(Cs[arow * LDA + kb + j]) >> 16);
+        }
+#pragma unroll
+        for (int q = 0; q < NBW; ++q) {
+          const u16x8 ub = *reinterpret_cast<const u16x8*>(Ubt + (16 * (cg * NBW + q) + (lane & 15)) * D + kb);
+          xa[q] = mfma16_bf16(ab, ub, xa[q]);
+          xc[q] = mfma16_bf16(cb, ub, xc[q]);
+        }
+      }
+    } else {
+#pragma unroll 4
+      for (int k0 = 0; k0 < D; k0 += 4) {
+        const int kk = k0 + (lane >> 4);
+        const float av = As[arow * LDA + kk];
+        const float cv = Cs[arow * LDA + kk];
+#pragma unroll
+        for (int q = 0; q < NBW; ++q) {
+          const float bv = Us[kk * D + 16 * (cg * NBW + q) + (lane & 15)];
+          xa[q] = mfma16(av, bv, xa[q]);
+          xc[q] = mfma16(cv, bv, xc[q]);
+        }
       }
     }
     // ---- s = sum over the concept block of XA (.) XC, r = relu(s) ----
@@ -509,46 +554,49 @@ PartialPlan plan_partial(int64_t N, int d) {
   return {grid, per};
 }
 
-template <int D, int DK>
-int launch_partial(const float* A, const float* C, int64_t N, const float* U, float* partials,
+template <int D, int DK, bool BF>
+int launch_partial(const void* A, const void* C, int64_t N, const float* U, float* partials,
                    const PartialPlan& pl, hipStream_t s) {
-  const size_t lds = PartialCfg<D>::lds_floats * sizeof(float);
+  const size_t lds = (PartialCfg<D>::lds_floats - (BF ? (size_t)D * D / 2 : 0)) * sizeof(float);
   static bool attr_set = false;
   if (!attr_set) {
-    DRSA_HIP(hipFuncSetAttribute((const void*)drsa_partial_kernel<D, DK>,
+    DRSA_HIP(hipFuncSetAttribute((const void*)drsa_partial_kernel<D, DK, BF>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr_set = true;
   }
-  hipLaunchKernelGGL((drsa_partial_kernel<D, DK>), dim3(pl.grid), dim3(kThreads), lds, s, A, C, N, U,
+  hipLaunchKernelGGL((drsa_partial_kernel<D, DK, BF>), dim3(pl.grid), dim3(kThreads), lds, s, A, C, N, U,
                      partials, pl.tiles_per_wg);
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;
 }
 
-template <int D>
-int dispatch_partial_d(const float* A, const float* C, int64_t N, int K, const float* U, float* partials,
+template <int D, bool BF>
+int dispatch_partial_d(const void* A, const void* C, int64_t N, int K, const float* U, float* partials,
                        const PartialPlan& pl, hipStream_t s) {
   switch (D / K) {
-    case 1: if constexpr (D / 1 <= 128) return launch_partial<D, 1>(A, C, N, U, partials, pl, s); break;
-    case 2: return launch_partial<D, 2>(A, C, N, U, partials, pl, s);
-    case 4: return launch_partial<D, 4>(A, C, N, U, partials, pl, s);
-    case 8: return launch_partial<D, 8>(A, C, N, U, partials, pl, s);
-    case 16: return launch_partial<D, 16>(A, C, N, U, partials, pl, s);
-    case 32: if constexpr (D >= 32) return launch_partial<D, 32>(A, C, N, U, partials, pl, s); break;
-    case 64: if constexpr (D >= 64) return launch_partial<D, 64>(A, C, N, U, partials, pl, s); break;
+    case 1: if constexpr (D / 1 <= 128) return launch_partial<D, 1, BF>(A, C, N, U, partials, pl, s); break;
+    case 2: return launch_partial<D, 2, BF>(A, C, N, U, partials, pl, s);
+    case 4: return launch_partial<D, 4, BF>(A, C, N, U, partials, pl, s);
+    case 8: return launch_partial<D, 8, BF>(A, C, N, U, partials, pl, s);
+    case 16: return launch_partial<D, 16, BF>(A, C, N, U, partials, pl, s);
+    case 32: if constexpr (D >= 32) return launch_partial<D, 32, BF>(A, C, N, U, partials, pl, s); break;
+    case 64: if constexpr (D >= 64) return launch_partial<D, 64, BF>(A, C, N, U, partials, pl, s); break;
     default: break;
   }
   drsa::set_error("drsa_partial: unsupported d=%d K=%d", D, K);
   return DRSA_EUNSUPPORTED;
 }
 
-int dispatch_partial(const float* A, const float* C, int64_t N, int d, int K, const float* U,
-                     float* partials, const PartialPlan& pl, hipStream_t s) {
+int dispatch_partial(const void* A, const void* C, int64_t N, int d, int K, const float* U,
+                     float* partials, const PartialPlan& pl, hipStream_t s, bool bf = false) {
   switch (d) {
-    case 16: return dispatch_partial_d<16>(A, C, N, K, U, partials, pl, s);
-    case 32: return dispatch_partial_d<32>(A, C, N, K, U, partials, pl, s);
-    case 64: return dispatch_partial_d<64>(A, C, N, K, U, partials, pl, s);
-    case 128: return dispatch_partial_d<128>(A, C, N, K, U, partials, pl, s);
+    case 16: return bf ? DRSA_EUNSUPPORTED : dispatch_partial_d<16, false>(A, C, N, K, U, partials, pl, s);
+    case 32: return bf ? dispatch_partial_d<32, true>(A, C, N, K, U, partials, pl, s)
+                       : dispatch_partial_d<32, false>(A, C, N, K, U, partials, pl, s);
+    case 64: return bf ? dispatch_partial_d<64, true>(A, C, N, K, U, partials, pl, s)
+                       : dispatch_partial_d<64, false>(A, C, N, K, U, partials, pl, s);
+    case 128: return bf ? dispatch_partial_d<128, true>(A, C, N, K, U, partials, pl, s)
+                        : dispatch_partial_d<128, false>(A, C, N, K, U, partials, pl, s);
   }
   return DRSA_EUNSUPPORTED;
 }
@@ -611,10 +659,11 @@ size_t drsa_amd_drsa_workspace_bytes(int64_t N, int d, int K) {
   return ws_bytes(N, d, K);
 }
 
-int drsa_amd_drsa_partial(const float* A, const float* C, int64_t N, int d, int K, const float* U,
-                          float* gs_out, void* ws, size_t ws_size, void* stream) {
+static int partial_impl(const void* A, const void* C, int64_t N, int d, int K, const float* U, float* gs_out,
+                        void* ws, size_t ws_size, void* stream, int dtype) {
   DRSA_REQUIRE(supported_dims(d, K), "drsa_partial: unsupported d=%d K=%d", d, K);
   DRSA_REQUIRE(N >= 0, "drsa_partial: N < 0");
+  DRSA_REQUIRE(dtype == 0 || (dtype == 1 && d >= 32), "drsa_partial: bf16 needs d >= 32");
   hipStream_t s = (hipStream_t)stream;
   const size_t E = (size_t)d * d + K;
   if (N == 0) {
@@ -625,12 +674,22 @@ int drsa_amd_drsa_partial(const float* A, const float* C, int64_t N, int d, int 
   DRSA_REQUIRE(((uintptr_t)A % 16) == 0 && ((uintptr_t)C % 16) == 0, "drsa_partial: A/C must be 16B aligned");
   const PartialPlan pl = plan_partial(N, d);
   float* partials = (float*)ws;
-  int rc = dispatch_partial(A, C, N, d, K, U, partials, pl, s);
+  int rc = dispatch_partial(A, C, N, d, K, U, partials, pl, s, dtype == 1);
   if (rc) return rc;
   hipLaunchKernelGGL(drsa_reduce_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, partials,
                      pl.grid, (int)E, gs_out);
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;
+}
+
+int drsa_amd_drsa_partial(const float* A, const float* C, int64_t N, int d, int K, const float* U,
+                          float* gs_out, void* ws, size_t ws_size, void* stream) {
+  return partial_impl(A, C, N, d, K, U, gs_out, ws, ws_size, stream, 0);
+}
+
+int drsa_amd_drsa_partial_bf16(const uint16_t* A, const uint16_t* C, int64_t N, int d, int K, const float* U,
+                               float* gs_out, void* ws, size_t ws_size, void* stream) {
+  return partial_impl(A, C, N, d, K, U, gs_out, ws, ws_size, stream, 1);
 }
 
 int drsa_amd_drsa_finish(const float* gs, int64_t N_total, int d, int K, const float* U, float* U_out,
@@ -741,8 +800,12 @@ int drsa_amd_drsa_run_multi(int P, const drsa_amd_problem_t* probs, int steps, i
     DRSA_REQUIRE(q.N > 0 && q.A && q.C && q.U_io && q.U_tmp && q.f_traj && q.counter && q.ws,
                  "drsa_run_multi: problem %d has null pointers or N <= 0", p);
     DRSA_REQUIRE(q.ws_size >= ws_bytes(q.N, q.d, q.K), "drsa_run_multi: problem %d workspace too small", p);
+    DRSA_REQUIRE(q.dtype == 0 || (q.dtype == 1 && q.d >= 32), "drsa_run_multi: problem %d: dtype must be 0 (fp32) "
+                 "or 1 (bf16, d >= 32)", p);
   }
-  if (P == 1 || !use_graph || steps < 2) {
+  bool all_f32 = true;
+  for (int p = 0; p < P; ++p) all_f32 = all_f32 && probs[p].dtype == 0;
+  if (all_f32 && (P == 1 || !use_graph || steps < 2)) {
     for (int p = 0; p < P; ++p) {
       const drsa_amd_problem_t& q = probs[p];
       int rc = drsa_amd_drsa_run(q.A, q.C, q.N, q.d, q.K, q.U_io, q.U_tmp, steps, q.f_traj, q.counter, q.ws,
@@ -783,7 +846,7 @@ int drsa_amd_drsa_run_multi(int P, const drsa_amd_problem_t* probs, int steps, i
     const drsa_amd_problem_t& q = probs[p];
     const PartialPlan pl = plan_partial(q.N, q.d);
     float* gs = (float*)q.ws + (size_t)pl.grid * ((size_t)q.d * q.d + q.K);
-    int r = drsa_amd_drsa_partial(q.A, q.C, q.N, q.d, q.K, Uin, gs, q.ws, q.ws_size, st);
+    int r = partial_impl(q.A, q.C, q.N, q.d, q.K, Uin, gs, q.ws, q.ws_size, st, q.dtype);
     if (r) return r;
     return dispatch_finish(gs, (double)q.N, q.d, q.K, Uin, Uout, q.f_traj, q.counter, 1, Uout ? 0 : 1, kPolarTol,
                            kPolarMaxIter, nullptr, st);
@@ -807,22 +870,30 @@ int drsa_amd_drsa_run_multi(int P, const drsa_amd_problem_t* probs, int steps, i
     }
     return DRSA_OK;
   };
-  hipGraph_t graph = nullptr;
-  hipGraphExec_t exec = nullptr;
-  if (!hip_ok(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal), "capture")) { cleanup(); return rc; }
-  int rbody = forked(2, false);
-  hipError_t ce = hipStreamEndCapture(s, &graph);
-  if (rbody || !hip_ok(ce, "end capture") || !hip_ok(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0), "instantiate")) {
-    if (graph) (void)hipGraphDestroy(graph);
-    cleanup();
-    return rbody ? rbody : rc;
-  }
   int done = 0;
-  for (; done + 2 <= steps; done += 2)
-    if (!hip_ok(hipGraphLaunch(exec, s), "graph launch")) break;
-  (void)hipGraphExecDestroy(exec);
-  (void)hipGraphDestroy(graph);
-  if (rc) { cleanup(); return rc; }
+  if (use_graph && steps >= 2) {
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    if (!hip_ok(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal), "capture")) { cleanup(); return rc; }
+    int rbody = forked(2, false);
+    hipError_t ce = hipStreamEndCapture(s, &graph);
+    if (rbody || !hip_ok(ce, "end capture") ||
+        !hip_ok(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0), "instantiate")) {
+      if (graph) (void)hipGraphDestroy(graph);
+      cleanup();
+      return rbody ? rbody : rc;
+    }
+    for (; done + 2 <= steps; done += 2)
+      if (!hip_ok(hipGraphLaunch(exec, s), "graph launch")) break;
+    (void)hipGraphExecDestroy(exec);
+    (void)hipGraphDestroy(graph);
+    if (rc) { cleanup(); return rc; }
+  } else {
+    for (; done + 2 <= steps; done += 2) {
+      int r = forked(2, false);
+      if (r) { cleanup(); return r; }
+    }
+  }
   // odd tail step + final objective, eager on the forked streams
   if (done < steps) {
     if (!hip_ok(hipEventRecord(ev_fork, s), "record")) { cleanup(); return rc; }

@@ -211,3 +211,60 @@ def test_joint_run_equals_separate_runs_bitwise():
     A, C, U0, K = probs[0]
     Ur, ref = drsa_ref.run(A.cpu(), C.cpu(), U0.cpu(), K, 7)
     np.testing.assert_allclose(joint[0][1].cpu().numpy(), np.array(ref), rtol=1e-4)
+
+
+@pytest.mark.parametrize("N,d,K", [(3000, 64, 4), (2048, 128, 16), (777, 32, 2), (20000, 64, 8)])
+def test_bf16_partial_matches_bf16_closed_form(N, d, K):
+    """bf16 path (C5): the kernel against the float64 closed form ON THE SAME bf16 inputs (tight:
+    1e-5 relative) — checks the bf16 MFMA operand layout and the widening, not the rounding."""
+    from drsa_audio_amd.xai.drsa.drsa import DrsaWorkspace
+    from drsa_audio_amd import _capi
+    A, C = drsa_inputs(N, d, 7000 + N)
+    Ab, Cb = drsa_ref.bf16_round(A), drsa_ref.bf16_round(C)
+    U0 = _u0(d, d + K)
+    At = torch.from_numpy(Ab).to(DEV).to(torch.bfloat16)
+    Ct = torch.from_numpy(Cb).to(DEV).to(torch.bfloat16)
+    Ut = torch.from_numpy(U0).to(DEV)
+    ws = DrsaWorkspace(N, d, K, DEV)
+    gs = torch.empty(d * d + K, device=DEV)
+    _capi.call("drsa_amd_drsa_partial_bf16", At.data_ptr(), Ct.data_ptr(), N, d, K, Ut.data_ptr(), gs.data_ptr(),
+               ws.ptr, ws.nbytes, _capi.stream_ptr(DEV))
+    torch.cuda.synchronize()
+    f_ref, G_ref = drsa_ref.closed_form_bf16(Ab, Cb, U0, K)
+    Ud = drsa_ref.bf16_round(U0).astype(np.float64)
+    XA, XC = Ab.astype(np.float64) @ Ud, Cb.astype(np.float64) @ Ud
+    r = np.maximum((XA * XC).reshape(N, K, d // K).sum(-1), 0)
+    S_ref = (r * r).sum(0)
+    S = gs[d * d:].cpu().numpy().astype(np.float64)
+    np.testing.assert_allclose(S, S_ref, rtol=2e-5, atol=1e-6 * S_ref.max())
+    # unscaled gradient = A^T (R (.) XC) + C^T (R (.) XA)
+    R = np.repeat(r, d // K, axis=1)
+    Gt = Ab.astype(np.float64).T @ (R * XC) + Cb.astype(np.float64).T @ (R * XA)
+    Gk = gs[:d * d].cpu().numpy().reshape(d, d).astype(np.float64)
+    assert np.abs(Gk - Gt).max() <= 2e-5 * np.abs(Gt).max()
+
+
+def test_bf16_joint_run_objective_within_loosened_tolerance():
+    """C5 bf16 vs the fp32 path on the same (unrounded) data: the DRSA objective trajectory stays
+    within 1e-2 relative (loosened tolerance for a path the reference does not have)."""
+    from drsa_audio_amd.xai.drsa.drsa import drsa_run, drsa_run_joint
+    probs32, probs16 = [], []
+    for N, seed in ((4000, 26), (3000, 33)):
+        A, C = drsa_inputs(N, 128, seed)
+        U0 = _u0(128, seed)
+        A32, C32, U = _gpu(A, C, U0)
+        probs32.append((A32, C32, U, 16))
+        probs16.append((A32.to(torch.bfloat16), C32.to(torch.bfloat16), U, 16))
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        j16 = drsa_run_joint(probs16, 20)
+        j32 = drsa_run_joint(probs32, 20)
+        one16 = drsa_run(*probs16[0], 20)
+    torch.cuda.synchronize()
+    for (U16, t16), (U32, t32) in zip(j16, j32):
+        t16, t32 = t16.cpu().numpy(), t32.cpu().numpy()
+        assert np.all(np.abs(t16 - t32) <= 1e-2 * np.abs(t32)), (t16, t32)
+        assert t16[-1] > t16[0]                       # still ascending
+        Un = U16.cpu().double().numpy()
+        assert np.abs(Un.T @ Un - np.eye(128)).max() < 1e-5
+    assert torch.equal(one16[1], j16[0][1])           # single-problem bf16 route = joint route

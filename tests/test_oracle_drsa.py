@@ -65,3 +65,13 @@ def test_polar_matches_orthogonalize(fx):
     V = fx["small_U0"] + fx["small_G0"]
     P = drsa_ref.polar(V)
     assert np.abs(P - fx["small_orth0"]).max() < 1e-5
+
+
+def test_bf16_round_matches_torch():
+    """oracle bf16 rounding (used by the bf16-path closed form) = torch's float32->bfloat16 (RNE)."""
+    import torch
+    rng = np.random.default_rng(0)
+    x = np.concatenate([rng.standard_normal(10000).astype(np.float32) * 10 ** rng.uniform(-5, 5, 10000).astype(np.float32),
+                        np.array([0.0, -0.0, 1.0, 1.00390625, 1.01171875, 3.0e-39], dtype=np.float32)])
+    ref = torch.from_numpy(x).to(torch.bfloat16).float().numpy()
+    assert np.array_equal(drsa_ref.bf16_round(x), ref)
