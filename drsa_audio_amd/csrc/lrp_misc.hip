@@ -201,7 +201,10 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
 //   G_q   = [a > 0] (a (.) v) / stab(den, eps_den)   ReLU-backward + the conv rule's division below
 // Tiles of 64 pixels (RPT rows x TW cols), lanes = pixels; one tile per workgroup.
 // ===========================================================================
-constexpr int PT_BWD = 1;   // tiles per workgroup (backward): one tile, many workgroups
+#ifndef DRSA_PT_BWD
+#define DRSA_PT_BWD 1
+#endif
+constexpr int PT_BWD = DRSA_PT_BWD;   // tiles per workgroup (backward)
 #ifndef PROJ_STAGE_UNROLL
 #define PROJ_STAGE_UNROLL 1
 #endif

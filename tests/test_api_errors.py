@@ -1,0 +1,95 @@
+"""Error behaviour of the host layer and the C ABI (CPU: every check fires before device work).
+
+Mirrors the reference's runtime asserts (drsa.py:61-62, modify_model.py:40-41,
+sound.py:37,41, dataloading.py:174-175) and the no-CPU-fallback rule: product entry points
+raise on CPU tensors instead of computing there."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from drsa_audio_amd import _capi
+
+
+def test_subspace_optimizer_asserts_like_reference():
+    from drsa_audio_amd.xai.drsa.drsa import SubspaceOptimizer
+    U = torch.eye(8)
+    A = torch.rand(10, 8)
+    with pytest.raises(AssertionError):
+        SubspaceOptimizer(U, A, A, ".", num_concepts=0)
+    with pytest.raises(AssertionError):
+        SubspaceOptimizer(U, A, A, ".", num_concepts=3)
+    with pytest.raises(_capi.DrsaAmdError):
+        SubspaceOptimizer(U, A, A, ".", num_concepts=4, device="cpu")
+
+
+def test_projection_model_layer_range():
+    from drsa_audio_amd.model.create_model import VGGType
+    from drsa_audio_amd.model.modify_model import ProjectionModel
+    m = VGGType(n_filters=(8, 8, 16, 16, 16), n_dense=32, n_classes=2, pool_kernels=((2, 2),) * 5,
+                input_size=(64, 64), conv_bn=False, dense_bn=False, block_depth=1)
+    for bad in (0, len(m.features)):
+        with pytest.raises(ValueError):
+            ProjectionModel(m, bad, torch.eye(16), 4)
+
+
+def test_product_paths_refuse_cpu_tensors():
+    from drsa_audio_amd.utils.dataloading import Loader
+    from drsa_audio_amd.xai.drsa.preprocessing import normalize_vectors
+    from drsa_audio_amd.xai.drsa.drsa import orthogonalize
+    ld = Loader("gtzan", device="cpu")
+    with pytest.raises(_capi.DrsaAmdError):
+        ld.transform_wav(torch.zeros(1, 48000))
+    with pytest.raises(_capi.DrsaAmdError):
+        normalize_vectors(torch.rand(4, 8))
+    with pytest.raises(_capi.DrsaAmdError):
+        orthogonalize(torch.eye(8))
+
+
+def test_lrp_engine_refuses_cpu_model():
+    from drsa_audio_amd.model.create_model import VGGType
+    from drsa_audio_amd.utils.constants import LRP_NAME_MAP_GTZAN
+    from drsa_audio_amd.zennit.composites import NameMapComposite
+    from drsa_audio_amd.xai.explain.attribute import compute_relevances
+    m = VGGType(n_filters=(32, 32, 64, 64, 128), n_dense=128, pool_kernels=((2, 2),) * 5, input_size=(128, 128),
+                conv_bn=False, dense_bn=False, block_depth=1).eval()
+    with pytest.raises(_capi.DrsaAmdError):
+        compute_relevances(m, torch.zeros(1, 1, 128, 128), NameMapComposite(LRP_NAME_MAP_GTZAN), class_idx=0)
+
+
+def test_get_slice_asserts():
+    from drsa_audio_amd.utils.sound import get_slice
+    # sound.py:41 compares the start point (seconds) with a sample count, as the reference does
+    get_slice(torch.zeros(1, 16000 * 4), 3, 0, 1, 16000)
+    with pytest.raises(AssertionError):
+        get_slice(torch.zeros(1, 16000 * 4), 3, 17000, 1, 16000)
+    with pytest.raises(AssertionError):                      # sound.py:37 not enough audio for 8 chunks
+        get_slice(torch.zeros(1, 16000 * 10), 3, 0, 8, 16000)
+
+
+def test_c_abi_argument_validation_without_gpu():
+    lib = _capi.load()
+    P = ctypes.c_void_p
+    # logmel: null pointers, odd n_fft, frames past the end
+    assert lib.drsa_amd_logmel(None, 1, 48000, 1, 0, 48000, 800, 360, 128, 128, 1, None, None, None, None, None, 0,
+                               1, 1, -4.0, 1e-7, None, None) == -1
+    assert b"null" in lib.drsa_amd_last_error()
+    buf = (ctypes.c_float * 4)()
+    ib = (ctypes.c_int * 4)()
+    p, q = ctypes.cast(buf, P).value, ctypes.cast(ib, P).value
+    assert lib.drsa_amd_logmel(p, 1, 48000, 1, 0, 48000, 801, 360, 128, 128, 1, p, q, q, q, p, 1, 1, 1, -4.0, 1e-7,
+                               p, None) == -1
+    assert lib.drsa_amd_logmel(p, 1, 48000, 1, 0, 48000, 800, 360, 128, 140, 1, p, q, q, q, p, 1, 1, 1, -4.0, 1e-7,
+                               p, None) == -1
+    assert b"frames" in lib.drsa_amd_last_error()
+    # DRSA vectors: bad layout; pooled relevance with an odd map
+    assert lib.drsa_amd_drsa_vectors(p, p, None, q, 1, 4, 4, 4, 1, 1, 2, 7, p, p, None) == -1
+    assert lib.drsa_amd_drsa_vectors(p, p, q, q, 1, 4, 5, 4, 2, 2, 2, 0, p, p, None) == -1
+    # pool kernel must divide the map
+    assert lib.drsa_amd_maxpool_capture(p, None, p, q, None, 1, 4, 6, 8, 4, 4, None) == -1
+    # joint DRSA: no problems
+    assert lib.drsa_amd_drsa_run_multi(0, None, 10, 1, None) == -1
+    # workspace size query rejects unsupported problems
+    assert lib.drsa_amd_drsa_workspace_bytes(100, 48, 4) == 0
+    assert lib.drsa_amd_drsa_workspace_bytes(100, 128, 3) == 0
