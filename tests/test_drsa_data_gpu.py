@@ -119,3 +119,29 @@ def test_training_data_feeds_drsa_and_matches_oracle_objective(tmp_path):
     a2, c2 = load_and_normalize_data(p, DEV)
     np.testing.assert_allclose(a2.cpu().numpy(), Ar.numpy(), rtol=2e-6, atol=1e-7)
     np.testing.assert_allclose(c2.cpu().numpy(), Cr.numpy(), rtol=2e-6, atol=1e-7)
+
+
+def test_prototype_search_matches_oracle():
+    """get_prototypes_ts (prototypes.py:14-130) on device vs the oracle: same winning subset,
+    objectives within 1e-5 relative, bit-exact prototype vectors."""
+    from drsa_audio_amd.xai.drsa.prototypes import get_prototypes_ts, subset_objectives
+    net = gtzan128()
+    B, n, K = 16, 4, 4
+    x = logmel(B, seed=31)
+    U = torch.from_numpy(np.linalg.qr(np.random.default_rng(3).standard_normal((64, 64)))[0].astype(np.float32))
+    a, c, names, sp = get_prototypes_ts(_gpu(net), 7, U.to(DEV), NameMapComposite(LRP_NAME_MAP_GTZAN), x.to(DEV), 3,
+                                        loaded_samples=[f"s{i}" for i in range(B)], num_concepts=K, n=n, seed=42)
+    perm = torch.randperm(B, generator=torch.Generator().manual_seed(42))
+    act, rel = _oracle_maps(net, LRP_NAME_MAP_GTZAN, x[perm], "features.7", 3)
+    b, d = act.shape[:2]
+    va = act.reshape(b, d, -1).transpose(-2, -1)
+    vc = drsa_ref.compute_context_vectors(va, rel.reshape(b, d, -1).transpose(-2, -1))
+    objs = [float(drsa_ref.obj_val(va[i * n:(i + 1) * n].reshape(-1, d), vc[i * n:(i + 1) * n].reshape(-1, d), U, K,
+                                   d // K)) for i in range(B // n)]
+    best = int(np.argmax(objs))
+    assert names == [f"s{int(i)}" for i in perm[best * n:(best + 1) * n]]
+    assert torch.equal(a.cpu(), va[best * n:(best + 1) * n].reshape(-1, d))
+    assert torch.equal(c.cpu(), vc[best * n:(best + 1) * n].reshape(-1, d))
+    got = subset_objectives(va.to(DEV).contiguous(), vc.to(DEV).contiguous(), U.to(DEV), K, n).cpu().numpy()
+    np.testing.assert_allclose(got, objs, rtol=1e-5)
+    assert sp is not None and len(sp) == n
