@@ -1,0 +1,155 @@
+// First-layer forward (Cin = 1) with the fused ReLU + 2x2 max-pool + argmax + LRP denominator.
+//
+// The generic MFMA conv (lrp_conv_kernel.h) does only 9 useful k-steps per staged chunk here
+// and spends its time in the LDS staging and the epilogue; the layer is HBM-bound on its
+// pooled outputs (y, argmax, den: 9 B per pooled cell and channel).  This kernel keeps the
+// whole 4x10 input patch of four adjacent pool windows in registers, runs every output
+// pixel's 9-tap fma chain on the VALU (same k order as the MFMA kernel and
+// oracle/lrp_exact.c:conv2d_exact, so the result is bit-identical), and writes float4 rows of
+// y and den plus one packed uint32 of argmax bytes per channel.
+//
+// Reference: cxai/model/create_model.py:100-137 (conv -> ReLU -> MaxPool2d) and the rule
+// denominators of SURVEY App. A (WSquare map / Epsilon z / Gamma z+ + z-).
+#include "common.h"
+#include "lrp_conv.h"
+
+#include <stdlib.h>
+
+namespace {
+
+constexpr int kThreads = 256;
+
+// DEN: 0 none, 1 input-independent map (WSquare / Flat), 2 computed from the rule's sets
+template <int NG, int DEN>
+__global__ __launch_bounds__(kThreads) void first_conv_pool_kernel(ConvArgs a, int cout_p, int total) {
+  const int t = blockIdx.x * kThreads + threadIdx.x;
+  if (t >= total) return;
+  const int H = a.H, W = a.W, H2 = H >> 1, W2 = W >> 1, gq = W2 >> 2;
+  const int b = t / (H2 * gq), rem = t % (H2 * gq);
+  const int qy = rem / gq, g4 = rem % gq;
+  const int y0 = 2 * qy - 1, x0 = 8 * g4 - 1;
+
+  // input patch rows y0..y0+3, columns x0..x0+9 (zero outside the image)
+  float xin[4][10];
+  const float* src = a.in + (size_t)b * H * W;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int yy = y0 + r;
+    const bool rok = yy >= 0 && yy < H;
+    const float* row = src + (size_t)(rok ? yy : 0) * W;
+    const float4 v0 = *reinterpret_cast<const float4*>(row + x0 + 1);
+    const float4 v1 = *reinterpret_cast<const float4*>(row + x0 + 5);
+    const float l = row[x0 >= 0 ? x0 : 0];
+    const float rr = row[x0 + 9 < W ? x0 + 9 : W - 1];
+    xin[r][0] = (rok && x0 >= 0) ? l : 0.f;
+    xin[r][1] = rok ? v0.x : 0.f; xin[r][2] = rok ? v0.y : 0.f; xin[r][3] = rok ? v0.z : 0.f; xin[r][4] = rok ? v0.w : 0.f;
+    xin[r][5] = rok ? v1.x : 0.f; xin[r][6] = rok ? v1.y : 0.f; xin[r][7] = rok ? v1.z : 0.f; xin[r][8] = rok ? v1.w : 0.f;
+    xin[r][9] = (rok && x0 + 9 < W) ? rr : 0.f;
+  }
+
+  const size_t plane2 = (size_t)H2 * W2;
+  const size_t obase = ((size_t)b * a.cout) * plane2 + (size_t)qy * W2 + 4 * g4;
+
+  // blockIdx.y: channel slice (more waves in flight for the store stream)
+  const int cper = (a.cout + gridDim.y - 1) / gridDim.y;
+  const int c_lo = blockIdx.y * cper, c_hi = min(a.cout, c_lo + cper);
+  for (int co = c_lo; co < c_hi; ++co) {
+    float w[NG][9];
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+      for (int k = 0; k < 9; ++k) w[g][k] = a.wts[(size_t)(g * 9 + k) * cout_p + co];
+    const float b0 = a.bias ? a.bias[co] : 0.f;
+
+    float ym[4], dn[4];
+    uint32_t amw = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      // window pixels in torch's row-major order: s = 2 * py + px
+      float yy[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int py = s >> 1, px = s & 1;
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) acc = __builtin_fmaf(xin[py + k / 3][2 * j + px + k % 3], w[0][k], acc);
+        const float z = acc + b0;
+        float y = z > 0.f ? z : 0.f;
+        if (z != z) y = z;   // relu(NaN) = NaN
+        yy[s] = y;
+      }
+      // torch max_pool2d: first maximum in window order; NaN wins
+      int am = 0;
+      float m = yy[0];
+#pragma unroll
+      for (int s = 1; s < 4; ++s)
+        if (yy[s] > m || (yy[s] != yy[s] && m == m)) { m = yy[s]; am = s; }
+      ym[j] = m;
+      amw |= (uint32_t)am << (8 * j);
+      if constexpr (DEN == 1) {
+        const int py = am >> 1, px = am & 1;
+        dn[j] = a.den_map[((size_t)co * H + 2 * qy + py) * W + 8 * g4 + 2 * j + px];
+      } else if constexpr (DEN == 2) {
+        // the rule's denominator at the argmax pixel only (every chain is per pixel)
+        float xs[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+          // select the tap inputs of pixel `am` (4-way, branch-free)
+          const float c0 = xin[k / 3][2 * j + k % 3], c1 = xin[k / 3][2 * j + 1 + k % 3];
+          const float c2 = xin[1 + k / 3][2 * j + k % 3], c3 = xin[1 + k / 3][2 * j + 1 + k % 3];
+          xs[k] = am == 0 ? c0 : (am == 1 ? c1 : (am == 2 ? c2 : c3));
+        }
+        const float bpos = a.bias ? a.bias[cout_p + co] : 0.f;
+        if constexpr (NG >= 2) {
+          const float bneg = a.bias ? a.bias[2 * cout_p + co] : 0.f;
+          float a1 = 0.f;
+#pragma unroll
+          for (int k = 0; k < 9; ++k) a1 = __builtin_fmaf(fmaxf(xs[k], 0.f), w[1][k], a1);
+          const float z0 = a1 + bpos;
+          float z1 = bneg;
+          if constexpr (NG == 3) {
+            float a2 = 0.f;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) a2 = __builtin_fmaf(fminf(xs[k], 0.f), w[2][k], a2);
+            z1 = a2 + bneg;
+          }
+          dn[j] = z0 + z1;
+        } else {
+          // Epsilon: den = conv(x; W) + b_den
+          float a0 = 0.f;
+#pragma unroll
+          for (int k = 0; k < 9; ++k) a0 = __builtin_fmaf(xs[k], w[0][k], a0);
+          dn[j] = a0 + bpos;
+        }
+      }
+    }
+    const size_t o = obase + (size_t)co * plane2;
+    *reinterpret_cast<float4*>(a.out + o) = make_float4(ym[0], ym[1], ym[2], ym[3]);
+    *reinterpret_cast<uint32_t*>(a.out_amax + o) = amw;
+    if constexpr (DEN != 0) *reinterpret_cast<float4*>(a.out_den + o) = make_float4(dn[0], dn[1], dn[2], dn[3]);
+  }
+}
+
+template <int NG>
+int launch_ng(const ConvArgs& a, int cout_p, int B, hipStream_t s) {
+  const int total = B * (a.H / 2) * (a.W / 8);
+  const char* cs_v = getenv("DRSA_AMD_FIRST_FWD_CSPLIT");   // tuning knob (0 = heuristic)
+  const int cs_env = cs_v ? atoi(cs_v) : 0;
+  // splitting the channels over more waves measured no gain at the bench shape (store-bound)
+  const int cs = cs_env > 0 ? cs_env : 1;
+  const dim3 grid((total + kThreads - 1) / kThreads, cs);
+  if (!a.out_den) hipLaunchKernelGGL((first_conv_pool_kernel<NG, 0>), grid, dim3(kThreads), 0, s, a, cout_p, total);
+  else if (a.den_map) hipLaunchKernelGGL((first_conv_pool_kernel<NG, 1>), grid, dim3(kThreads), 0, s, a, cout_p, total);
+  else hipLaunchKernelGGL((first_conv_pool_kernel<NG, 2>), grid, dim3(kThreads), 0, s, a, cout_p, total);
+  DRSA_LAUNCH_CHECK();
+  return DRSA_OK;
+}
+
+}  // namespace
+
+// Cin = 1, pooled output, W % 8 == 0 (checked by the caller, drsa_amd_conv_fwd)
+int drsa_first_conv_pool(const ConvArgs& a, int cout_p, int ng, int B, hipStream_t s) {
+  if (ng == 1) return launch_ng<1>(a, cout_p, B, s);
+  if (ng == 2) return launch_ng<2>(a, cout_p, B, s);
+  return launch_ng<3>(a, cout_p, B, s);
+}

@@ -23,3 +23,7 @@ struct ConvArgs {
   float eps;
   int dbg;                  // ablation only (DRSA_AMD_CONV_DBG): 1 no staging loads, 2 no epilogue I/O, 4 no MFMA
 };
+
+// conv_first.hip: Cin = 1 forward with fused ReLU + 2x2 pool + argmax + den (VALU; W % 8 == 0)
+#include <hip/hip_runtime.h>
+int drsa_first_conv_pool(const ConvArgs& a, int cout_p, int ng, int B, hipStream_t s);

@@ -77,6 +77,13 @@ int drsa_amd_conv_fwd(const float* in, const float* wts, const float* bias, cons
   DRSA_REQUIRE(!pool || out_amax, "conv_fwd: pool needs out_amax");
   DRSA_REQUIRE(pool || W % 4 == 0, "conv_fwd: an unpooled output needs W %% 4 == 0 (float4 epilogue; got W=%d)", W);
   const int cin_p = cin_pad(cin), cout_p = pad32(cout);
+  const int first_generic = env_int("DRSA_AMD_CONV_FIRST_GENERIC", 0);   // per call: tests compare both paths
+  if (cin == 1 && pool && W % 8 == 0 && !first_generic) {
+    ConvArgs a{};
+    a.in = in; a.wts = wts; a.bias = bias; a.den_map = den_map; a.out = out; a.out_amax = out_amax;
+    a.out_den = out_den; a.H = H; a.W = W; a.cin = cin; a.cout = cout; a.clones = 1;
+    return drsa_first_conv_pool(a, cout_p, ng, B, (hipStream_t)stream);
+  }
   const Entry* e = find(cin_p, cout_p, W, ng, A_DENSE, pool ? EPI_FWD_POOL : EPI_FWD_RELU);
   if (!e) {
     drsa::set_error("conv_fwd: no kernel for cin=%d cout=%d W=%d ng=%d pool=%d", cin, cout, W, ng, pool);
