@@ -105,6 +105,61 @@ __global__ __launch_bounds__(256) void linear_kernel(LinArgs a) {
   }
 }
 
+// Forward with K % 4 == 0 (the classifier input, K = 2048): 128-wide K chunks loaded as float4
+// and the next chunk prefetched into registers while the current one runs, so the one
+// k-ordered chain per output (oracle/lrp_exact.c:linear_exact) is no longer bound by one load
+// round trip per 32 k.
+constexpr int LFK = 128;
+
+__global__ __launch_bounds__(256) void linear_fwd_kernel(LinArgs a) {
+  __shared__ __attribute__((aligned(16))) float As[LT][LFK + 4];   // [m][k]
+  __shared__ float Bs[LFK][LT + 1];                               // [k][n]
+  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int m0 = blockIdx.x * LT, n0 = blockIdx.y * LT;
+  const int wm = (w & 1) * 16, wn = (w >> 1) * 16;
+  constexpr int NV = LT * LFK / 4 / 256;   // float4 per thread per operand
+  float4 ra[NV], rb[NV];
+#define LFWD_LOAD(K0)                                                                                     \
+  _Pragma("unroll") for (int i = 0; i < NV; ++i) {                                                        \
+    const int idx = tid + i * 256, r = idx / (LFK / 4), k = (K0) + (idx % (LFK / 4)) * 4;                 \
+    const int m = m0 + r, n = n0 + r;                                                                     \
+    const bool oa = m < a.M && k < a.K, ob = n < a.N && k < a.K;                                          \
+    const float4 va = *reinterpret_cast<const float4*>(a.A + (oa ? (size_t)m * a.K + k : 0));             \
+    const float4 vb = *reinterpret_cast<const float4*>(a.W + (ob ? (size_t)n * a.K + k : 0));             \
+    ra[i] = oa ? va : make_float4(0.f, 0.f, 0.f, 0.f);                                                    \
+    rb[i] = ob ? vb : make_float4(0.f, 0.f, 0.f, 0.f);                                                    \
+  }
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  LFWD_LOAD(0)
+  for (int k0 = 0; k0 < a.K; k0 += LFK) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int idx = tid + i * 256, r = idx / (LFK / 4), c = (idx % (LFK / 4)) * 4;
+      *reinterpret_cast<float4*>(&As[r][c]) = ra[i];
+      Bs[c][r] = rb[i].x; Bs[c + 1][r] = rb[i].y; Bs[c + 2][r] = rb[i].z; Bs[c + 3][r] = rb[i].w;
+    }
+    __syncthreads();
+    if (k0 + LFK < a.K) { LFWD_LOAD(k0 + LFK) }
+#pragma unroll
+    for (int kk = 0; kk < LFK; kk += 4) {
+      const float av = As[wm + (lane & 15)][kk + (lane >> 4)];
+      const float bv = Bs[kk + (lane >> 4)][wn + (lane & 15)];
+      acc = mfma16(av, bv, acc);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = m0 + wm + (lane >> 4) * 4 + r, n = n0 + wn + (lane & 15);
+    if (m >= a.M || n >= a.N) continue;
+    const size_t o = (size_t)m * a.N + n;
+    const float zz = acc[r] + (a.bias ? a.bias[n] : 0.f);
+    a.out[o] = zz;
+    if (a.out_relu) a.out_relu[o] = zz > 0.f ? zz : (zz != zz ? zz : 0.f);
+  }
+#undef LFWD_LOAD
+}
+
 // ===========================================================================
 // projection forward: h = a_vec U, a' = h U^T, optional 2x2 max-pool of a'
 //   a [B][D][H][W] -> h [B][D][H*W] (channel-major), ap [B][D][H][W], pooled + argmax
@@ -128,7 +183,8 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
   const int TW = W < 32 ? W : 32, RPT = P / TW;      // tile = RPT rows x TW cols
   const int HW = H * W, xt = W / TW;
   for (int i = tid; i < D * D; i += 256) Us[(i / D) * LD + i % D] = U[i];
-  constexpr int NB = D / 16, TILES = NB * (P / 16);
+  constexpr int NB = D / 16;
+  static_assert(P / 16 == 4, "one 16-pixel block per wave");
   for (int t = 0; t < PT; ++t) {
     const int tile = blockIdx.x * PT + t;
     if (tile >= (H / RPT) * xt) break;
@@ -139,36 +195,49 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
       as[c * PL + p] = a[((size_t)b * D + c) * HW + (y0 + p / TW) * W + x0 + p % TW];
     }
     __syncthreads();
-    // h[j][p] = sum_c U[c][j] a[c][p]
-    for (int q = w; q < TILES; q += 4) {
-      const int jb = q / (P / 16), pb = q % (P / 16);
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
+    // h[j][p] = sum_c U[c][j] a[c][p]: wave w owns pixel block w and runs the NB output blocks
+    // as independent MFMA chains sharing the B operand (same per-element k order as one chain)
+    {
+      f32x4 acc[NB];
+#pragma unroll
+      for (int jb = 0; jb < NB; ++jb) acc[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
       for (int k0 = 0; k0 < D; k0 += 4) {
         const int c = k0 + (lane >> 4);
-        acc = mfma16(Us[c * LD + jb * 16 + (lane & 15)], as[c * PL + pb * 16 + (lane & 15)], acc);
+        const float bv = as[c * PL + w * 16 + (lane & 15)];
+#pragma unroll
+        for (int jb = 0; jb < NB; ++jb) acc[jb] = mfma16(Us[c * LD + jb * 16 + (lane & 15)], bv, acc[jb]);
       }
-      for (int r = 0; r < 4; ++r) {
-        const int j = jb * 16 + (lane >> 4) * 4 + r, p = pb * 16 + (lane & 15);
-        hs[j * PL + p] = acc[r];
-        h[((size_t)b * D + j) * HW + (y0 + p / TW) * W + x0 + p % TW] = acc[r];
-      }
+#pragma unroll
+      for (int jb = 0; jb < NB; ++jb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = jb * 16 + (lane >> 4) * 4 + r, p = w * 16 + (lane & 15);
+          hs[j * PL + p] = acc[jb][r];
+          if (h) h[((size_t)b * D + j) * HW + (y0 + p / TW) * W + x0 + p % TW] = acc[jb][r];
+        }
     }
     __syncthreads();
     // a'[c][p] = sum_j U[c][j] h[j][p]
-    for (int q = w; q < TILES; q += 4) {
-      const int cb = q / (P / 16), pb = q % (P / 16);
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
+    {
+      f32x4 acc[NB];
+#pragma unroll
+      for (int cb = 0; cb < NB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
       for (int k0 = 0; k0 < D; k0 += 4) {
         const int j = k0 + (lane >> 4);
-        acc = mfma16(Us[(cb * 16 + (lane & 15)) * LD + j], hs[j * PL + pb * 16 + (lane & 15)], acc);
+        const float bv = hs[j * PL + w * 16 + (lane & 15)];
+#pragma unroll
+        for (int cb = 0; cb < NB; ++cb) acc[cb] = mfma16(Us[(cb * 16 + (lane & 15)) * LD + j], bv, acc[cb]);
       }
-      for (int r = 0; r < 4; ++r) {
-        const int c = cb * 16 + (lane >> 4) * 4 + r, p = pb * 16 + (lane & 15);
-        as[c * PL + p] = acc[r];   // a tile no longer needed: holds a' now
-        ap[((size_t)b * D + c) * HW + (y0 + p / TW) * W + x0 + p % TW] = acc[r];
-      }
+#pragma unroll
+      for (int cb = 0; cb < NB; ++cb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = cb * 16 + (lane >> 4) * 4 + r, p = w * 16 + (lane & 15);
+          as[c * PL + p] = acc[cb][r];   // a tile no longer needed: holds a' now
+          if (ap) ap[((size_t)b * D + c) * HW + (y0 + p / TW) * W + x0 + p % TW] = acc[cb][r];
+        }
     }
     if (pool) {
       __syncthreads();
@@ -322,6 +391,168 @@ __global__ __launch_bounds__(256) void projection_bwd_kernel(
           G[(orow * D + c) * HW + pixl] = gq;
         }
       }
+    }
+  }
+}
+
+// ===========================================================================
+// projection backward with h and a' recomputed from a (no h / a' buffers in HBM: the forward
+// then writes only the pooled a' and its argmax).  Same math and the same MFMA operand order
+// as projection_fwd_kernel (h, a') and projection_bwd_kernel (t, clones), so every value is
+// bit-identical to the stored-buffer path.  Each wave owns one 16-pixel block of the 64-pixel
+// tile end to end, so after U is staged no workgroup barrier is needed:
+//   region A [D][16]: a, then g1;  region B [D][16]: h, then g2   (wave-private LDS)
+// ===========================================================================
+#ifndef DRSA_PT_RC
+#define DRSA_PT_RC 4
+#endif
+constexpr int PT_RC = DRSA_PT_RC;   // tiles per workgroup (U staged once)
+#ifndef DRSA_PROJ_RC_WPE
+#define DRSA_PROJ_RC_WPE 3
+#endif
+
+template <int D>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? DRSA_PROJ_RC_WPE : 1))) void projection_bwd_rc_kernel(
+    const float* __restrict__ gp, const uint8_t* __restrict__ amax, const float* __restrict__ a,
+    const float* __restrict__ den, const float* __restrict__ U, float* __restrict__ G, int H, int W, int K,
+    float eps_proj, float eps_den, int sparse, int has_den, int fanout) {
+  constexpr int P = 64, LD = D + 1, PW = 16, NB = D / 16;
+  constexpr bool PF = D <= 64;   // keep a / den of the output rows in registers
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+  float* Us = sm;                                   // [D][LD]
+  float* RA = Us + D * LD + w * 2 * D * PW;         // [D][PW]
+  float* RB = RA + D * PW;                          // [D][PW]
+  const int b = blockIdx.y;
+  const int TW = W < 32 ? W : 32, RPT = P / TW;
+  const int HW = H * W, xt = W / TW, H2 = H / 2, W2 = W / 2;
+  const int dk = D / K;
+  const int nq = fanout ? (K + 1) : 1;
+  const int pc = lane & 15, rg = lane >> 4;         // pixel column / row group of the MFMA layouts
+  for (int i = tid; i < D * D; i += 256) Us[(i / D) * LD + i % D] = U[i];
+  __syncthreads();
+  for (int t = 0; t < PT_RC; ++t) {
+    const int tile = blockIdx.x * PT_RC + t;
+    if (tile >= (H / RPT) * xt) break;
+    const int y0 = (tile / xt) * RPT, x0 = (tile % xt) * TW;
+    const int pl = w * 16 + pc;
+    const int py = y0 + pl / TW, px = x0 + pl % TW;
+    const size_t pixl = (size_t)py * W + px;
+    // a (and den) at rows c = i*16 + 4 rg + r: the output layout of every GEMM below
+    float av[NB * 4], dv[PF ? NB * 4 : 1];
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = i * 16 + rg * 4 + r;
+        const size_t os = ((size_t)b * D + c) * HW + pixl;
+        av[i * 4 + r] = a[os];
+        if constexpr (PF) dv[i * 4 + r] = has_den ? den[os] : 1.f;
+      }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < NB * 4; ++i) RA[(((i >> 2) * 16) + rg * 4 + (i & 3)) * PW + pc] = av[i];
+    __builtin_amdgcn_wave_barrier();
+    // Every GEMM below runs its NB output blocks as independent MFMA chains that share the B
+    // operand read (per element the k order is the single-chain order of the stored path).
+    // h[j][p] = sum_c U[c][j] a[c][p]        (projection_fwd_kernel order)
+    {
+      f32x4 acc[NB];
+#pragma unroll
+      for (int jb = 0; jb < NB; ++jb) acc[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+      for (int k0 = 0; k0 < D; k0 += 4) {
+        const int c = k0 + rg;
+        const float bv = RA[c * PW + pc];
+#pragma unroll
+        for (int jb = 0; jb < NB; ++jb) acc[jb] = mfma16(Us[c * LD + jb * 16 + pc], bv, acc[jb]);
+      }
+#pragma unroll
+      for (int jb = 0; jb < NB; ++jb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) RB[(jb * 16 + rg * 4 + r) * PW + pc] = acc[jb][r];
+    }
+    __builtin_amdgcn_wave_barrier();
+    // a'[c][p] = sum_j U[c][j] h[j][p];  g1 = R_a' / stab(a')  -> region A
+    {
+      f32x4 acc[NB];
+#pragma unroll
+      for (int cb = 0; cb < NB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+      for (int k0 = 0; k0 < D; k0 += 4) {
+        const int j = k0 + rg;
+        const float bv = RB[j * PW + pc];
+#pragma unroll
+        for (int cb = 0; cb < NB; ++cb) acc[cb] = mfma16(Us[(cb * 16 + pc) * LD + j], bv, acc[cb]);
+      }
+#pragma unroll
+      for (int cb = 0; cb < NB; ++cb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = cb * 16 + rg * 4 + r;
+          float R;
+          if (sparse) {
+            const size_t q = ((size_t)b * D + c) * H2 * W2 + (py >> 1) * W2 + (px >> 1);
+            R = (amax[q] == (((py & 1) << 1) | (px & 1))) ? gp[q] : 0.f;
+          } else {
+            R = gp[((size_t)b * D + c) * HW + pixl];
+          }
+          RA[c * PW + pc] = R / stab(acc[cb][r], eps_proj);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // t[j][p] = sum_c U[c][j] g1[c][p];  g2 = h (.) t / stab(h)  -> region B (in place of h)
+    {
+      f32x4 acc[NB];
+#pragma unroll
+      for (int jb = 0; jb < NB; ++jb) acc[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+      for (int k0 = 0; k0 < D; k0 += 4) {
+        const int c = k0 + rg;
+        const float bv = RA[c * PW + pc];
+#pragma unroll
+        for (int jb = 0; jb < NB; ++jb) acc[jb] = mfma16(Us[c * LD + jb * 16 + pc], bv, acc[jb]);
+      }
+#pragma unroll
+      for (int jb = 0; jb < NB; ++jb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float* e = RB + (jb * 16 + rg * 4 + r) * PW + pc;   // this lane's own h element
+          const float hx = *e;
+          *e = (hx * acc[jb][r]) / stab(hx, eps_proj);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int qi = 0; qi < nq; ++qi) {
+      const int q = fanout ? qi : b % (K + 1);
+      const int j0 = q == 0 ? 0 : (q - 1) * dk, j1 = q == 0 ? D : q * dk;
+      const size_t orow = fanout ? (size_t)b * (K + 1) + q : (size_t)b;
+      f32x4 acc[NB];
+#pragma unroll
+      for (int cb = 0; cb < NB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int k0 = j0; k0 < j1; k0 += 4) {
+        const int j = k0 + rg;
+        const bool ok = j < j1;
+        const float gb = ok ? RB[j * PW + pc] : 0.f;
+#pragma unroll
+        for (int cb = 0; cb < NB; ++cb) acc[cb] = mfma16(ok ? Us[(cb * 16 + pc) * LD + j] : 0.f, gb, acc[cb]);
+      }
+#pragma unroll
+      for (int cb = 0; cb < NB; ++cb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = cb * 16 + rg * 4 + r;
+          const size_t os = ((size_t)b * D + c) * HW + pixl;
+          const float ax = av[cb * 4 + r];
+          float dx = 1.f;
+          if constexpr (PF) dx = dv[cb * 4 + r];
+          else if (has_den) dx = den[os];
+          const float Rv = ax * acc[cb][r];
+          float gq;
+          if (has_den) gq = (ax > 0.f) ? Rv / stab(dx, eps_den) : 0.f;
+          else gq = (ax > 0.f) ? Rv : 0.f;
+          G[(orow * D + c) * HW + pixl] = gq;
+        }
     }
   }
 }
@@ -621,6 +852,8 @@ template <int D>
 size_t proj_fwd_lds() { return ((size_t)D * (D + 1) + 2 * (size_t)D * 68) * sizeof(float); }
 template <int D>
 size_t proj_bwd_lds() { return ((size_t)D * (D + 1) + 2 * (size_t)D * 68) * sizeof(float); }
+template <int D>
+size_t proj_bwd_rc_lds() { return ((size_t)D * (D + 1) + 4 * 2 * (size_t)D * 16) * sizeof(float); }
 
 }  // namespace
 
@@ -631,7 +864,11 @@ int drsa_amd_linear_fwd(const float* x, const float* Wt, const float* bias, floa
   DRSA_REQUIRE(M > 0 && N > 0 && K > 0, "linear_fwd: bad shape");
   LinArgs a{};
   a.A = x; a.W = Wt; a.bias = bias; a.out = z_out; a.out_relu = relu_out; a.M = M; a.N = N; a.K = K; a.bwd = 0;
-  hipLaunchKernelGGL(linear_kernel, dim3((M + LT - 1) / LT, (N + LT - 1) / LT), dim3(256), 0, (hipStream_t)stream, a);
+  // long K (float4-aligned rows): the prefetching kernel; same chain order, same results
+  if (K % 4 == 0 && K >= LFK)
+    hipLaunchKernelGGL(linear_fwd_kernel, dim3((M + LT - 1) / LT, (N + LT - 1) / LT), dim3(256), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(linear_kernel, dim3((M + LT - 1) / LT, (N + LT - 1) / LT), dim3(256), 0, (hipStream_t)stream, a);
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;
 }
@@ -659,6 +896,7 @@ int drsa_amd_projection_fwd(const float* a, const float* U, float* h, float* ap,
   DRSA_REQUIRE((W == 8 || W == 16 || W % 32 == 0) && H % (64 / TW) == 0,
                "projection_fwd: W must be 8, 16 or a multiple of 32 and H a multiple of 64/min(W,32) (got %dx%d)", H, W);
   DRSA_REQUIRE(!pool || (pooled && amax), "projection_fwd: pool needs outputs");
+  DRSA_REQUIRE(pool || ap, "projection_fwd: without pool a' (ap) is the output");
   hipStream_t s = (hipStream_t)stream;
   const int tiles = (H / (64 / TW)) * (W / TW);
   const dim3 grid((tiles + PT - 1) / PT, B);
@@ -690,8 +928,28 @@ int drsa_amd_projection_bwd(const float* gp, const uint8_t* amax, const float* a
   DRSA_REQUIRE(K > 0 && D % K == 0, "projection_bwd: K must divide d");
   hipStream_t s = (hipStream_t)stream;
   const int tiles = (H / (64 / TW)) * (W / TW);
-  const dim3 grid((tiles + PT_BWD - 1) / PT_BWD, B);
   const int sparse = amax != nullptr, has_den = den != nullptr;
+  if (!ap || !h) {   // recompute h and a' from a
+    const dim3 grid((tiles + PT_RC - 1) / PT_RC, B);
+    switch (D) {
+#define PR(DD)                                                                                        \
+  case DD: {                                                                                          \
+    static bool set = false;                                                                          \
+    if (!set) { int rc = with_lds(projection_bwd_rc_kernel<DD>, proj_bwd_rc_lds<DD>()); if (rc) return rc; set = true; } \
+    hipLaunchKernelGGL(projection_bwd_rc_kernel<DD>, grid, dim3(256), proj_bwd_rc_lds<DD>(), s, gp, amax, a, den, U, G, \
+                       H, W, K, eps_proj, eps_den, sparse, has_den, fanout);                         \
+    break;                                                                                            \
+  }
+      PR(16) PR(32) PR(64) PR(128)
+#undef PR
+      default:
+        drsa::set_error("projection_bwd: unsupported d=%d", D);
+        return DRSA_EUNSUPPORTED;
+    }
+    DRSA_LAUNCH_CHECK();
+    return DRSA_OK;
+  }
+  const dim3 grid((tiles + PT_BWD - 1) / PT_BWD, B);
   switch (D) {
 #define PB(DD)                                                                                        \
   case DD: {                                                                                          \

@@ -23,6 +23,7 @@ batch size.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -33,6 +34,10 @@ from .. import _capi
 from .._capi import POST_DIV, POST_MASK, POST_NONE, XM_MUL, XM_NONE, XM_SPLIT
 from ..zennit import rules as R
 from ..zennit.canonizers import SequentialMergeBatchNorm
+
+# store h and a' in HBM for projection_bwd instead of recomputing them there (A/B comparisons
+# only; both paths are bit-identical)
+_PROJ_STORE = os.environ.get("DRSA_AMD_PROJ_STORE", "0") == "1"
 
 
 def _pad32(c: int) -> int:
@@ -395,14 +400,16 @@ class LRPEngine:
                 rec.update(a=a, den=den)
                 if st.proj is not None:
                     P = st.proj
-                    hb = self._buf((li, "h"), (B, st.cout, h * w))        # channel-major
-                    ap = self._buf((li, "ap"), (B, st.cout, h, w))
+                    # h and a' are recomputed by projection_bwd from a (no HBM round trip); a' is
+                    # stored only when it is the stage output (no pool after the projection)
+                    hb = self._buf((li, "h"), (B, st.cout, h * w)) if _PROJ_STORE else None
+                    ap = self._buf((li, "ap"), (B, st.cout, h, w)) if (_PROJ_STORE or not P.pool_after) else None
                     if P.pool_after:
                         pooled = self._buf((li, "y"), (B, st.cout, h // 2, w // 2))
                         amax = self._buf((li, "amax"), (B, st.cout, h // 2, w // 2), torch.uint8)
                     else:
                         pooled = amax = None
-                    self._call("projection_fwd", "drsa_amd_projection_fwd", a.data_ptr(), P.U.data_ptr(), hb.data_ptr(), ap.data_ptr(),
+                    self._call("projection_fwd", "drsa_amd_projection_fwd", a.data_ptr(), P.U.data_ptr(), _capi.ptr(hb), _capi.ptr(ap),
                                _capi.ptr(pooled), _capi.ptr(amax), B, st.cout, h, w, 1 if P.pool_after else 0, s)
                     rec.update(h=hb, ap=ap, amax=amax)
                     if P.pool_after:
@@ -507,7 +514,7 @@ class LRPEngine:
                 if not P.mask:
                     raise EngineError("engine: projection without SubspaceHook is not supported yet")
                 self._call("projection_bwd", "drsa_amd_projection_bwd", g.data_ptr(), _capi.ptr(rec["amax"] if P.pool_after else None),
-                           rec["ap"].data_ptr(), rec["h"].data_ptr(), rec["a"].data_ptr(),
+                           _capi.ptr(rec["ap"] if _PROJ_STORE else None), _capi.ptr(rec["h"]), rec["a"].data_ptr(),
                            _capi.ptr(den if post == POST_DIV else None), P.U.data_ptr(), G.data_ptr(), B, st.cout,
                            h, w, K, P.eps_inv, eps, 1 if fan else 0, s)
                 g, clones, Bq = G, nq, B * nq

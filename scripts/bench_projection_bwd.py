@@ -20,8 +20,12 @@ G = torch.empty(B * (K + 1), D, H, W, device=dev)
 s = _capi.stream_ptr()
 
 
+RC = os.environ.get("RC", "1") == "1"   # recompute h and a' (engine default) vs stored buffers
+
+
 def run():
-    _capi.call("drsa_amd_projection_bwd", g.data_ptr(), amax.data_ptr(), ap.data_ptr(), h.data_ptr(), a.data_ptr(),
+    _capi.call("drsa_amd_projection_bwd", g.data_ptr(), amax.data_ptr(), None if RC else ap.data_ptr(),
+               None if RC else h.data_ptr(), a.data_ptr(),
                den.data_ptr(), U.data_ptr(), G.data_ptr(), B, D, H, W, K, 1e-6, 1e-7, 1, s)
 
 
@@ -36,4 +40,4 @@ e1.record()
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / 20
 byts = (g.numel() + 4 * a.numel() + G.numel()) * 4 + amax.numel()
-print(json.dumps({"ms": ms, "GBs": byts / ms / 1e6, "tflops": 2 * 3 * B * H * W * D * D / ms / 1e9}))
+print(json.dumps({"lib": os.environ.get("DRSA_AMD_LIB", "default"), "rc": RC, "ms": ms, "GBs": byts / ms / 1e6, "tflops": 2 * 3 * B * H * W * D * D / ms / 1e9}))

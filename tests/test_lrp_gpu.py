@@ -83,6 +83,22 @@ def test_heatmap_generator_bit_exact(net, layer_idx):
     assert np.array_equal(hg.info["input"], x.numpy())
 
 
+@pytest.mark.parametrize("layer_idx", [7, 10])
+def test_projection_recompute_equals_stored(net, layer_idx, monkeypatch):
+    """projection_bwd recomputing h and a' from a (default) == the stored-buffer path, bitwise."""
+    from drsa_audio_amd.engine import plan
+    x = logmel(6, seed=30 + layer_idx).to(DEV)
+    out = {}
+    for store in (False, True):
+        monkeypatch.setattr(plan, "_PROJ_STORE", store)
+        hg = HeatmapGenerator(_gpu_model(net), u64(), LRP_NAME_MAP_GTZAN, "blues", num_concepts=4,
+                              layer_idx=layer_idx)
+        hg.generate_subspace_heatmaps(x)
+        out[store] = {k: hg.info[k].copy() for k in ("standard_heatmaps", "subspace_heatmaps", "mask")}
+    for k in out[False]:
+        assert np.array_equal(out[False][k], out[True][k]), k
+
+
 def test_heatmap_generator_batch_one_keeps_dims(net):
     x = logmel(1, seed=21)
     hg = HeatmapGenerator(_gpu_model(net), u64(), LRP_NAME_MAP_GTZAN, "pop", num_concepts=4, layer_idx=7)
