@@ -71,11 +71,11 @@ __device__ __forceinline__ f32x4 mfma16_bf16(u16x8 a, u16x8 b, f32x4 c) {
                                                  0, 0, 0);
 }
 
-// zennit Stabilizer: t + eps * (sign(t) + [t == 0])
+// zennit Stabilizer: t + eps * (sign(t) + [t == 0]).  sign(t) + [t == 0] is exactly +1 for
+// t >= 0 (including -0), -1 for t < 0, and 0 for NaN (where t + 0 = NaN = t - eps), so the
+// select below is bit-identical with one compare instead of three.
 __device__ __forceinline__ float stab(float t, float eps) {
-  float sgn = (t > 0.f) ? 1.f : ((t < 0.f) ? -1.f : 0.f);
-  float z = (t == 0.f) ? 1.f : 0.f;
-  return t + (z + sgn) * eps;
+  return t + ((t >= 0.f) ? eps : -eps);
 }
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
