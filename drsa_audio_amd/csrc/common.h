@@ -78,6 +78,15 @@ __device__ __forceinline__ float stab(float t, float eps) {
   return t + ((t >= 0.f) ? eps : -eps);
 }
 
+// n / d (IEEE) computed unconditionally: the empty asm pins the quotient in a VGPR, so a
+// following select does not get turned into an exec branch around the division sequence (which
+// also drags the operand loads into the branch and serialises their latency).
+__device__ __forceinline__ float div_nb(float n, float d) {
+  float q = n / d;
+  asm volatile("" : "+v"(q));
+  return q;
+}
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 

@@ -590,18 +590,19 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
     } else {   // EPI_BWD: R = xmode(acc, x) -> post -> out
       // float4 group i = tid + it * 256: the pixel (py, px) is fixed per thread and the staged
       // row advances by CS = 256 / Q per iteration, so every address is a per-thread base plus
-      // a channel offset (32-bit) and x is loaded once for the rule and the division
+      // a channel offset.  Loads come from clamped (always valid) addresses and the arithmetic
+      // runs unconditionally (no exec branches that would serialise the load latency); only the
+      // store is masked.  x is loaded once for the rule and the division.
       constexpr int Q = TH * TW / 4, CS = kThreads / Q;
       static_assert(kThreads % Q == 0, "float4 groups per tile must divide the block");
       const int cl0 = tid / Q, rem = tid % Q;
       const int py = rem / (TW / 4), px = (rem % (TW / 4)) * 4;
       const bool pix_ok = ty0 + py < H && tx0 + px < W;
       const int HW = H * W;
-      const size_t pix = (size_t)(ty0 + py) * W + tx0 + px;
+      const size_t pix = pix_ok ? (size_t)(ty0 + py) * W + tx0 + px : 0;
       const float* xs = a.x ? a.x + (size_t)bs * a.cout * HW + pix : nullptr;
       const float* ds = a.den ? a.den + (size_t)bs * a.cout * HW + pix : nullptr;
       float* oqp = a.out + (size_t)bq * a.cout * HW + pix;
-      const float* Tp = T + (cl0 * TH + py) * TWP + px;
       const bool need_x = (a.xmode != XM_NONE || a.post != POST_NONE) && !(a.dbg & 2);
      for (int sub = 0; sub < ES; ++sub) {
       float4 Rk[V4T], xk[V4T];
@@ -610,20 +611,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
       for (int it = 0; it < V4T; ++it) {
         const int cl = cl0 + it * CS;
         const int co = gchs(cl, v, sub);
-        Rk[it] = make_float4(0.f, 0.f, 0.f, 0.f);
-        xk[it] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (cl < TCH && co < a.cout && pix_ok) {
-          const float4 t = *reinterpret_cast<const float4*>(Tp + it * CS * TH * TWP);
-          if (need_x) xk[it] = *reinterpret_cast<const float4*>(xs + (size_t)co * HW);
-          const float4 x = xk[it];
-          if (a.xmode == XM_NONE || (a.dbg & 2)) {
-            Rk[it] = t;
-          } else if (a.xmode == XM_MUL) {
-            Rk[it] = make_float4(x.x * t.x, x.y * t.y, x.z * t.z, x.w * t.w);
-          } else {
-            Rk[it] = make_float4(fmaxf(x.x, 0.f) * t.x, fmaxf(x.y, 0.f) * t.y, fmaxf(x.z, 0.f) * t.z,
-                                 fmaxf(x.w, 0.f) * t.w);
-          }
+        const bool ok = cl < TCH && co < a.cout;
+        const int clc = ok ? cl : 0, coc = ok ? co : 0;
+        const float4 t = *reinterpret_cast<const float4*>(T + (clc * TH + py) * TWP + px);
+        xk[it] = need_x ? *reinterpret_cast<const float4*>(xs + (size_t)coc * HW) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 x = xk[it];
+        if (a.xmode == XM_NONE || (a.dbg & 2)) {
+          Rk[it] = t;
+        } else if (a.xmode == XM_MUL) {
+          Rk[it] = make_float4(x.x * t.x, x.y * t.y, x.z * t.z, x.w * t.w);
+        } else {
+          Rk[it] = make_float4(fmaxf(x.x, 0.f) * t.x, fmaxf(x.y, 0.f) * t.y, fmaxf(x.z, 0.f) * t.z,
+                               fmaxf(x.w, 0.f) * t.w);
         }
       }
       if constexpr (NG >= 2) {
@@ -633,14 +632,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
           for (int it = 0; it < V4T; ++it) {
             const int cl = cl0 + it * CS;
             const int co = gchs(cl, v, sub);
-            if (cl < TCH && co < a.cout && pix_ok) {
-              const float4 t = *reinterpret_cast<const float4*>(Tp + it * CS * TH * TWP);
-              const float4 x = xk[it];
-              Rk[it].x += fminf(x.x, 0.f) * t.x;
-              Rk[it].y += fminf(x.y, 0.f) * t.y;
-              Rk[it].z += fminf(x.z, 0.f) * t.z;
-              Rk[it].w += fminf(x.w, 0.f) * t.w;
-            }
+            const int clc = (cl < TCH && co < a.cout) ? cl : 0;
+            const float4 t = *reinterpret_cast<const float4*>(T + (clc * TH + py) * TWP + px);
+            const float4 x = xk[it];
+            Rk[it].x += fminf(x.x, 0.f) * t.x;
+            Rk[it].y += fminf(x.y, 0.f) * t.y;
+            Rk[it].z += fminf(x.z, 0.f) * t.z;
+            Rk[it].w += fminf(x.w, 0.f) * t.w;
           }
         }
       }
@@ -648,28 +646,31 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
       for (int it = 0; it < V4T; ++it) {
         const int cl = cl0 + it * CS;
         const int co = gchs(cl, v, sub);
-        if (cl < TCH && co < a.cout && pix_ok) {
-          float4 R = Rk[it];
-          if (a.dbg & 2) {
-            if (R.x == 12345.f) oqp[(size_t)co * HW] = 1.f;
-            continue;
-          }
-          if (a.post == POST_DIV) {
-            const float4 x = xk[it];
-            const float4 d = *reinterpret_cast<const float4*>(ds + (size_t)co * HW);
-            R.x = (x.x > 0.f) ? R.x / stab(d.x, a.eps) : 0.f;
-            R.y = (x.y > 0.f) ? R.y / stab(d.y, a.eps) : 0.f;
-            R.z = (x.z > 0.f) ? R.z / stab(d.z, a.eps) : 0.f;
-            R.w = (x.w > 0.f) ? R.w / stab(d.w, a.eps) : 0.f;
-          } else if (a.post == POST_MASK) {
-            const float4 x = xk[it];
-            R.x = (x.x > 0.f) ? R.x : 0.f;
-            R.y = (x.y > 0.f) ? R.y : 0.f;
-            R.z = (x.z > 0.f) ? R.z : 0.f;
-            R.w = (x.w > 0.f) ? R.w : 0.f;
-          }
-          *reinterpret_cast<float4*>(oqp + (size_t)co * HW) = R;
+        const bool ok = cl < TCH && co < a.cout;
+        const int coc = ok ? co : 0;
+        float4 R = Rk[it];
+        if (a.dbg & 2) {
+          if (ok && pix_ok && R.x == 12345.f) oqp[(size_t)coc * HW] = 1.f;
+          continue;
         }
+        if (a.post == POST_DIV) {
+          const float4 x = xk[it];
+          const float4 d = *reinterpret_cast<const float4*>(ds + (size_t)coc * HW);
+          // quotients first (evaluated for every lane), then the ReLU-backward select
+          const float qx = div_nb(R.x, stab(d.x, a.eps)), qy = div_nb(R.y, stab(d.y, a.eps));
+          const float qz = div_nb(R.z, stab(d.z, a.eps)), qw = div_nb(R.w, stab(d.w, a.eps));
+          R.x = (x.x > 0.f) ? qx : 0.f;
+          R.y = (x.y > 0.f) ? qy : 0.f;
+          R.z = (x.z > 0.f) ? qz : 0.f;
+          R.w = (x.w > 0.f) ? qw : 0.f;
+        } else if (a.post == POST_MASK) {
+          const float4 x = xk[it];
+          R.x = (x.x > 0.f) ? R.x : 0.f;
+          R.y = (x.y > 0.f) ? R.y : 0.f;
+          R.z = (x.z > 0.f) ? R.z : 0.f;
+          R.w = (x.w > 0.f) ? R.w : 0.f;
+        }
+        if (ok && pix_ok) *reinterpret_cast<float4*>(oqp + (size_t)coc * HW) = R;
       }
      }
     }

@@ -96,7 +96,8 @@ __global__ __launch_bounds__(256) void linear_kernel(LinArgs a) {
       if (a.xmode == XM_MUL) R = a.x[o] * R;
       if (a.post == POST_DIV) {
         const float xv = a.x[o];
-        R = (xv > 0.f) ? R / stab(a.den[o], a.eps_post) : 0.f;
+        const float q = div_nb(R, stab(a.den[o], a.eps_post));
+        R = (xv > 0.f) ? q : 0.f;
       } else if (a.post == POST_MASK) {
         R = (a.x[o] > 0.f) ? R : 0.f;
       }
@@ -333,7 +334,8 @@ __global__ __launch_bounds__(256) void projection_bwd_kernel(
       if (sparse) {
         const int H2 = H / 2, W2 = W / 2;
         const size_t q = ((size_t)b * D + c) * H2 * W2 + (y >> 1) * W2 + (x >> 1);
-        R = (amax[q] == (((y & 1) << 1) | (x & 1))) ? gp[q] : 0.f;
+        const float gv = gp[q];
+        R = (amax[q] == (((y & 1) << 1) | (x & 1))) ? gv : 0.f;
       } else {
         R = gp[((size_t)b * D + c) * HW + y * W + x];
       }
@@ -386,8 +388,12 @@ __global__ __launch_bounds__(256) void projection_bwd_kernel(
           else { ax = a[os]; dx = has_den ? den[os] : 1.f; }
           const float Rv = ax * acc[r];
           float gq;
-          if (has_den) gq = (ax > 0.f) ? Rv / stab(dx, eps_den) : 0.f;
-          else gq = (ax > 0.f) ? Rv : 0.f;
+          if (has_den) {
+            const float qd = div_nb(Rv, stab(dx, eps_den));   // every lane, then the select
+            gq = (ax > 0.f) ? qd : 0.f;
+          } else {
+            gq = (ax > 0.f) ? Rv : 0.f;
+          }
           G[(orow * D + c) * HW + pixl] = gq;
         }
       }
@@ -493,7 +499,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? D
           float R;
           if (sparse) {
             const size_t q = ((size_t)b * D + c) * H2 * W2 + (py >> 1) * W2 + (px >> 1);
-            R = (amax[q] == (((py & 1) << 1) | (px & 1))) ? gp[q] : 0.f;
+            const float gv = gp[q];   // unconditional load, then the argmax select
+            R = (amax[q] == (((py & 1) << 1) | (px & 1))) ? gv : 0.f;
           } else {
             R = gp[((size_t)b * D + c) * HW + pixl];
           }
@@ -549,8 +556,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? D
           else if (has_den) dx = den[os];
           const float Rv = ax * acc[cb][r];
           float gq;
-          if (has_den) gq = (ax > 0.f) ? Rv / stab(dx, eps_den) : 0.f;
-          else gq = (ax > 0.f) ? Rv : 0.f;
+          if (has_den) {
+            const float qd = div_nb(Rv, stab(dx, eps_den));   // every lane, then the select
+            gq = (ax > 0.f) ? qd : 0.f;
+          } else {
+            gq = (ax > 0.f) ? Rv : 0.f;
+          }
           G[(orow * D + c) * HW + pixl] = gq;
         }
     }
