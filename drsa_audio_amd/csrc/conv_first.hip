@@ -104,7 +104,7 @@ __global__ __launch_bounds__(kThreads) void first_conv_pool_kernel(ConvArgs a, i
           const float bneg = a.bias ? a.bias[2 * cout_p + co] : 0.f;
           float a1 = 0.f;
 #pragma unroll
-          for (int k = 0; k < 9; ++k) a1 = __builtin_fmaf(fmaxf(xs[k], 0.f), w[1][k], a1);
+          for (int k = 0; k < 9; ++k) a1 = __builtin_fmaf(NG == 3 ? fmaxf(xs[k], 0.f) : xs[k], w[1][k], a1);
           const float z0 = a1 + bpos;
           float z1 = bneg;
           if constexpr (NG == 3) {

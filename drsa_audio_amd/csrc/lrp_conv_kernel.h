@@ -349,10 +349,10 @@ __device__ __forceinline__ void mfma_chunk(const float* halo, const float* wl, c
 #pragma unroll
         for (int u = 0; u < MPW; ++u) {
           float x = xr[cur][u];
+          // NG == 2 is the Gamma forward on a non-negative input (ABI contract): x+ = x, so both
+          // sets read the same operand with no per-k-step transform
           if constexpr (EPI != EPI_BWD && NG == 3) {
             x = (g == 0) ? x : (g == 1 ? fmaxf(x, 0.f) : fminf(x, 0.f));
-          } else if constexpr (EPI != EPI_BWD && NG == 2) {
-            x = (g == 0) ? x : fmaxf(x, 0.f);
           }
           acc[g][u][v] = mfma32(wr[cur][g][v], x, acc[g][u][v]);
         }

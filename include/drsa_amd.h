@@ -91,7 +91,8 @@ int drsa_amd_subspace_relevances(const float* act, const float* ctx, int64_t B, 
 size_t drsa_amd_conv_weight_floats(int cin, int cout, int ng);
 
 /* Forward conv3x3 'same' + bias + ReLU [+ 2x2 max-pool with argmax] and the layer's LRP
- * denominator (Gamma: ng = 2 (x >= 0) or 3; Epsilon: ng = 1; WSquare/Flat: den_map).
+ * denominator (Gamma: ng = 2 for x >= 0, where set 1 is applied to x as is, or ng = 3 with
+ * the x+ / x- split; Epsilon: ng = 1; WSquare/Flat: den_map).
  * Replaces the model forward (create_model.py:91-97) plus the modified forwards zennit's
  * BasicHook re-runs in backward (attribute.py:98-107 via zennit.core.BasicHook). */
 int drsa_amd_conv_fwd(const float* in, const float* wts, const float* bias, const float* den_map, float* out,
