@@ -16,8 +16,8 @@ import json
 import sys
 from collections import defaultdict
 
-OURS = ("conv3x3_kernel", "linear_kernel", "projection_fwd_kernel", "projection_bwd_kernel",
-        "first_layer_bwd", "heatmap_sort_kernel")
+OURS = ("conv3x3_kernel", "linear_kernel", "linear_fwd_kernel", "projection_fwd_kernel", "projection_bwd_kernel",
+        "projection_bwd_rc_kernel", "first_conv_pool_kernel", "first_layer_bwd", "heatmap_sort_kernel")
 
 
 def _ours(name):
