@@ -119,14 +119,17 @@ int drsa_amd_linear_bwd(const float* R, const int* seed_cls, int one_hot, const 
                         float eps, const float* W, const float* x, int xmode, const float* den, int post,
                         float eps_post, float* out, int M, int Nout, int Kin, void* stream);
 
-/* ProjectionModel forward (modify_model.py:75-123): h = a_vec U, a' = h U^T [, 2x2 pool]. */
+/* ProjectionModel forward (modify_model.py:75-123): h = a_vec U, a' = h U^T [, 2x2 pool].
+ * h and ap may be NULL (not stored); ap is required when pool == 0 (it is the output). */
 int drsa_amd_projection_fwd(const float* a, const float* U, float* h, float* ap, float* pooled, uint8_t* amax, int B,
                             int D, int H, int W, int pool, void* stream);
 
 /* Epsilon(invprojection) -> SubspaceHook mask -> Epsilon(projection) -> ReLU backward ->
  * division of the conv rule below (explainer.py:198-203, attribute.py:42-60).
  * fanout != 0: each sample yields K+1 clones (standard + K subspaces); fanout == 0: row b is
- * clone (b mod (K+1)) of a replicated batch (explainer.py:92 semantics). */
+ * clone (b mod (K+1)) of a replicated batch (explainer.py:92 semantics).
+ * ap or h NULL: h and a' are recomputed from a in the kernel (same MFMA order as
+ * drsa_amd_projection_fwd, so the result is bit-identical to passing the stored buffers). */
 int drsa_amd_projection_bwd(const float* gp, const uint8_t* amax, const float* ap, const float* h, const float* a,
                             const float* den, const float* U, float* G, int B, int D, int H, int W, int K,
                             float eps_proj, float eps_den, int fanout, void* stream);
