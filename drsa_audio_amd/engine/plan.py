@@ -199,10 +199,11 @@ class LRPEngine:
                     raise EngineError("engine: a ProjectionModel layer must be followed by MaxPool2d(2) or no pool")
             rule = rules.get(f"features.{name}")
             kind = _kind(rule)
-            if kind not in (None, "epsilon", "gamma", "wsquare", "flat"):
+            if kind not in (None, "epsilon", "gamma", "wsquare", "flat", "zplus"):
                 raise EngineError(f"engine: rule {type(rule).__name__} on conv features.{name} is not supported yet")
             eps = {None: 0.0, "epsilon": getattr(rule, "epsilon", 0.0), "gamma": getattr(rule, "stabilizer", 0.0),
-                   "wsquare": getattr(rule, "stabilizer", 0.0), "flat": getattr(rule, "stabilizer", 0.0)}[kind]
+                   "wsquare": getattr(rule, "stabilizer", 0.0), "flat": getattr(rule, "stabilizer", 0.0),
+                   "zplus": getattr(rule, "stabilizer", 0.0)}[kind]
             st = ConvStage(name=f"features.{name}", cin=m.in_channels, cout=m.out_channels, rule_kind=kind,
                            eps=float(eps), pool=pool, proj=proj, input_nonneg=prev_nonneg, W=W, b=b, rule=rule,
                            relu_name=relu_name, pool_name=pool_name, pool_k=pool_k)
@@ -300,6 +301,18 @@ class LRPEngine:
             Wp, Wn = W + g * W.clamp(min=0), W + g * W.clamp(max=0)
             bp, bn = bd + g * bd.clamp(min=0), bd + g * bd.clamp(max=0)
             bias3[1, :st.cout], bias3[2, :st.cout] = bp, bn
+            sets = [W, Wp] + ([Wn] if not st.input_nonneg else [])
+            st.ng_fwd = len(sets)
+            st.den_kind = "gamma"
+            if st.input_nonneg:
+                st.ng_bwd, st.xmode_bwd, bsets = 1, XM_MUL, [Wp]
+            else:
+                st.ng_bwd, st.xmode_bwd, bsets = 2, XM_SPLIT, [Wp, Wn]
+        elif k == "zplus":
+            # zennit ZPlus: (x+, W+, b+) and (x-, W-, 0) with one shared denominator: the Gamma
+            # kernels with the clamped weight sets and a zero second bias
+            Wp, Wn = W.clamp(min=0), W.clamp(max=0)
+            bias3[1, :st.cout], bias3[2, :st.cout] = bd.clamp(min=0), 0.0
             sets = [W, Wp] + ([Wn] if not st.input_nonneg else [])
             st.ng_fwd = len(sets)
             st.den_kind = "gamma"

@@ -6,8 +6,10 @@ Semantics (reference name maps ``constants.py:27-51``):
   WSquare(ε)   R_in = Jᵀ_{W²}(R / stab_ε(conv(1; W², b²)))
   Flat(ε)      as WSquare with W -> 1, b -> 0
   Pass()       R_in = R_out (activation layers only)
-``ZPlus``, ``AlphaBeta``, ``Norm`` are accepted as descriptors but not executed by the HIP
-engine yet (compiling a composite that maps them raises ``NotImplementedError``).
+  ZPlus(ε)     z = f(x+; W+, b+) + f(x-; W-, 0);  R_in = x+ ⊙ Jᵀ_{W+} g + x- ⊙ Jᵀ_{W-} g,
+               g = R / stab_ε(z)   (conv layers; runs on the Gamma kernels with these sets)
+``AlphaBeta`` and ``Norm`` are accepted as descriptors but not executed by the HIP engine yet
+(compiling a composite that maps them raises ``NotImplementedError``).
 """
 from __future__ import annotations
 

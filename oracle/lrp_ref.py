@@ -359,6 +359,15 @@ def rule_backward_analytic(L: Layer, rule: RuleSpec, x: torch.Tensor, z: torch.T
             w2, b2 = torch.ones_like(w), _mod(b, torch.zeros_like)
         den = _aff(L, torch.ones_like(x), w2, b2, ops)
         return _aff_jt(L, x.shape, w2, R / stabilize(den, eps), ops)
+    if kind == "zplus":
+        # zennit ZPlus: inputs (x+, x-), params (W+, b+) and (W-, 0); one shared denominator
+        eps = rule[1]
+        wp, wn = w.clamp(min=0), w.clamp(max=0)
+        bp = _mod(b, lambda t: t.clamp(min=0))
+        xp, xn = x.clamp(min=0), x.clamp(max=0)
+        den = _aff(L, xp, wp, bp, ops) + _aff(L, xn, wn, _mod(b, torch.zeros_like), ops)
+        g = R / stabilize(den, eps)
+        return xp * _aff_jt(L, x.shape, wp, g, ops) + xn * _aff_jt(L, x.shape, wn, g, ops)
     raise ValueError(f"oracle: unknown rule {rule}")
 
 
@@ -405,6 +414,13 @@ def rule_backward_zennit(L: Layer, rule: RuleSpec, x: torch.Tensor, z: torch.Ten
         ins, outs = run([torch.ones_like(x)], [(w2, b2)])
         g, = torch.autograd.grad(outs, ins, [R / stabilize(outs[0].detach(), eps)])
         return g
+    if kind == "zplus":
+        eps = rule[1]
+        params = [(w.clamp(min=0), _mod(b, lambda t: t.clamp(min=0))), (w.clamp(max=0), _mod(b, torch.zeros_like))]
+        ins, outs = run([x.clamp(min=0), x.clamp(max=0)], params)
+        g = R / stabilize(outs[0].detach() + outs[1].detach(), eps)
+        grads = torch.autograd.grad(outs, ins, [g, g])
+        return sum(i.detach() * gg for i, gg in zip(ins, grads))
     raise ValueError(f"oracle: unknown rule {rule}")
 
 

@@ -34,7 +34,7 @@ def spec(name_map):
             t = ("epsilon", r.epsilon)
         elif k == "gamma":
             t = ("gamma", r.gamma, r.stabilizer)
-        elif k in ("wsquare", "flat"):
+        elif k in ("wsquare", "flat", "zplus"):
             t = (k, r.stabilizer)
         elif k == "pass":
             t = ("pass",)

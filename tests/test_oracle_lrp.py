@@ -215,3 +215,50 @@ def test_product_bn_fold_matches_oracle_merge():
     w, b = SequentialMergeBatchNorm.fold(net.features[3].weight.detach(), net.features[3].bias.detach(),
                                          net.features[4])
     assert torch.equal(w, merged.features[3].weight) and torch.equal(b, merged.features[3].bias)
+
+
+def _conv_layer(cin=3, cout=4, bias=False, seed=0):
+    torch.manual_seed(seed)
+    conv = nn.Conv2d(cin, cout, 3, padding=1, bias=bias)
+    return conv, lrp_ref.Layer("c", conv, "conv")
+
+
+def test_zplus_conservation_bias_free_conv():
+    """ZPlus (zennit 0.5.1 semantics, restated): sum R_in = sum R * den / stab(den) with
+    den = conv(x+; W+) + conv(x-; W-) when the conv has no bias."""
+    conv, L = _conv_layer()
+    x = torch.randn(2, 3, 6, 5, dtype=torch.float64)
+    conv = conv.double()
+    L = lrp_ref.Layer("c", conv, "conv")
+    z = conv(x).detach()
+    R = torch.randn_like(z)
+    eps = 1e-6
+    Rin = lrp_ref.rule_backward_analytic(L, ("zplus", eps), x, z, R)
+    w = conv.weight.detach()
+    den = nn.functional.conv2d(x.clamp(min=0), w.clamp(min=0), padding=1) + \
+        nn.functional.conv2d(x.clamp(max=0), w.clamp(max=0), padding=1)
+    expect = (R * den / lrp_ref.stabilize(den, eps)).sum((1, 2, 3))
+    assert torch.allclose(Rin.sum((1, 2, 3)), expect, rtol=1e-10, atol=1e-12)
+
+
+def test_zplus_zennit_structured_equals_analytic():
+    conv, L = _conv_layer(bias=True, seed=3)
+    x = torch.randn(2, 3, 8, 8)
+    z = conv(x).detach()
+    R = torch.randn_like(z)
+    Ra = lrp_ref.rule_backward_analytic(L, ("zplus", 1e-6), x, z, R)
+    Rz = lrp_ref.rule_backward_zennit(L, ("zplus", 1e-6), x, z, R)
+    assert torch.allclose(Ra, Rz, rtol=1e-5, atol=1e-6)
+
+
+def test_zplus_is_the_large_gamma_limit_on_nonnegative_input():
+    """Known answer: on x >= 0 with no bias, Gamma(gamma) -> ZPlus as gamma -> inf."""
+    conv, L = _conv_layer(seed=5)
+    conv = conv.double()
+    L = lrp_ref.Layer("c", conv, "conv")
+    x = torch.rand(2, 3, 7, 7, dtype=torch.float64)
+    z = conv(x).detach()
+    R = torch.rand_like(z) * (z > 0)
+    Rzp = lrp_ref.rule_backward_analytic(L, ("zplus", 1e-12), x, z, R)
+    Rg = lrp_ref.rule_backward_analytic(L, ("gamma", 1e7, 1e-12), x, z, R)
+    assert (Rzp - Rg).abs().max() <= 1e-5 * Rzp.abs().max()
