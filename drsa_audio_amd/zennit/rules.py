@@ -8,8 +8,11 @@ Semantics (reference name maps ``constants.py:27-51``):
   Pass()       R_in = R_out (activation layers only)
   ZPlus(ε)     z = f(x+; W+, b+) + f(x-; W-, 0);  R_in = x+ ⊙ Jᵀ_{W+} g + x- ⊙ Jᵀ_{W-} g,
                g = R / stab_ε(z)   (conv layers; runs on the Gamma kernels with these sets)
+  AlphaBeta(α, β, ε)  positive set (x+, W+, b+) + (x-, W-, 0), negative set (x+, W-, b-) + (x-, W+, 0),
+               one denominator per set; R_in = α·pos − β·neg (restated in oracle/lrp_ref.py and
+               pinned there by known-answer tests; not yet executed by the HIP engine)
 ``AlphaBeta`` and ``Norm`` are accepted as descriptors but not executed by the HIP engine yet
-(compiling a composite that maps them raises ``NotImplementedError``).
+(compiling a composite that maps them raises ``EngineError``, a ``NotImplementedError``).
 """
 from __future__ import annotations
 

@@ -368,6 +368,19 @@ def rule_backward_analytic(L: Layer, rule: RuleSpec, x: torch.Tensor, z: torch.T
         den = _aff(L, xp, wp, bp, ops) + _aff(L, xn, wn, _mod(b, torch.zeros_like), ops)
         g = R / stabilize(den, eps)
         return xp * _aff_jt(L, x.shape, wp, g, ops) + xn * _aff_jt(L, x.shape, wn, g, ops)
+    if kind == "alphabeta":
+        # zennit AlphaBeta: positive set (x+, W+, b+) + (x-, W-, 0), negative set (x+, W-, b-) +
+        # (x-, W+, 0); one denominator per set; R_in = alpha * pos - beta * neg
+        alpha, beta, eps = rule[1], rule[2], rule[3]
+        wp, wn = w.clamp(min=0), w.clamp(max=0)
+        bp, bn, b0 = (_mod(b, lambda t: t.clamp(min=0)), _mod(b, lambda t: t.clamp(max=0)),
+                      _mod(b, torch.zeros_like))
+        xp, xn = x.clamp(min=0), x.clamp(max=0)
+        gp = R / stabilize(_aff(L, xp, wp, bp, ops) + _aff(L, xn, wn, b0, ops), eps)
+        gn = R / stabilize(_aff(L, xp, wn, bn, ops) + _aff(L, xn, wp, b0, ops), eps)
+        pos = xp * _aff_jt(L, x.shape, wp, gp, ops) + xn * _aff_jt(L, x.shape, wn, gp, ops)
+        neg = xp * _aff_jt(L, x.shape, wn, gn, ops) + xn * _aff_jt(L, x.shape, wp, gn, ops)
+        return alpha * pos - beta * neg
     raise ValueError(f"oracle: unknown rule {rule}")
 
 
@@ -421,6 +434,19 @@ def rule_backward_zennit(L: Layer, rule: RuleSpec, x: torch.Tensor, z: torch.Ten
         g = R / stabilize(outs[0].detach() + outs[1].detach(), eps)
         grads = torch.autograd.grad(outs, ins, [g, g])
         return sum(i.detach() * gg for i, gg in zip(ins, grads))
+    if kind == "alphabeta":
+        alpha, beta, eps = rule[1], rule[2], rule[3]
+        wp, wn = w.clamp(min=0), w.clamp(max=0)
+        b0 = _mod(b, torch.zeros_like)
+        params = [(wp, _mod(b, lambda t: t.clamp(min=0))), (wn, b0),
+                  (wn, _mod(b, lambda t: t.clamp(max=0))), (wp, b0)]
+        ins, outs = run([x.clamp(min=0), x.clamp(max=0)] * 2, params)
+        o = [t.detach() for t in outs]
+        gp = R / stabilize(o[0] + o[1], eps)
+        gn = R / stabilize(o[2] + o[3], eps)
+        grads = torch.autograd.grad(outs, ins, [gp, gp, gn, gn])
+        r = [i.detach() * g for i, g in zip(ins, grads)]
+        return alpha * (r[0] + r[1]) - beta * (r[2] + r[3])
     raise ValueError(f"oracle: unknown rule {rule}")
 
 

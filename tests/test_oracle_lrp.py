@@ -251,6 +251,46 @@ def test_zplus_zennit_structured_equals_analytic():
     assert torch.allclose(Ra, Rz, rtol=1e-5, atol=1e-6)
 
 
+def test_alphabeta_one_zero_is_zplus():
+    """Known answer (zennit 0.5.1 semantics, restated): AlphaBeta(alpha=1, beta=0) is ZPlus."""
+    conv, L = _conv_layer(bias=True, seed=7)
+    x = torch.randn(2, 3, 8, 8)
+    z = conv(x).detach()
+    R = torch.randn_like(z)
+    Rab = lrp_ref.rule_backward_analytic(L, ("alphabeta", 1.0, 0.0, 1e-6), x, z, R)
+    Rzp = lrp_ref.rule_backward_analytic(L, ("zplus", 1e-6), x, z, R)
+    assert torch.equal(Rab, Rzp)
+
+
+def test_alphabeta_conservation_bias_free_conv():
+    """sum R_in = sum R * (alpha * den+/stab(den+) - beta * den-/stab(den-)) without bias."""
+    conv, L = _conv_layer(seed=9)
+    conv = conv.double()
+    L = lrp_ref.Layer("c", conv, "conv")
+    x = torch.randn(2, 3, 6, 5, dtype=torch.float64)
+    z = conv(x).detach()
+    R = torch.randn_like(z)
+    eps, alpha, beta = 1e-6, 2.0, 1.0
+    Rin = lrp_ref.rule_backward_analytic(L, ("alphabeta", alpha, beta, eps), x, z, R)
+    w = conv.weight.detach()
+    c2 = nn.functional.conv2d
+    dp = c2(x.clamp(min=0), w.clamp(min=0), padding=1) + c2(x.clamp(max=0), w.clamp(max=0), padding=1)
+    dn = c2(x.clamp(min=0), w.clamp(max=0), padding=1) + c2(x.clamp(max=0), w.clamp(min=0), padding=1)
+    expect = (R * (alpha * dp / lrp_ref.stabilize(dp, eps) - beta * dn / lrp_ref.stabilize(dn, eps))).sum((1, 2, 3))
+    assert torch.allclose(Rin.sum((1, 2, 3)), expect, rtol=1e-10, atol=1e-12)
+
+
+def test_alphabeta_zennit_structured_equals_analytic():
+    conv, L = _conv_layer(bias=True, seed=11)
+    x = torch.randn(2, 3, 8, 8)
+    z = conv(x).detach()
+    R = torch.randn_like(z)
+    rule = ("alphabeta", 2.0, 1.0, 1e-6)
+    Ra = lrp_ref.rule_backward_analytic(L, rule, x, z, R)
+    Rz = lrp_ref.rule_backward_zennit(L, rule, x, z, R)
+    assert torch.allclose(Ra, Rz, rtol=1e-5, atol=1e-5)
+
+
 def test_zplus_is_the_large_gamma_limit_on_nonnegative_input():
     """Known answer: on x >= 0 with no bias, Gamma(gamma) -> ZPlus as gamma -> inf."""
     conv, L = _conv_layer(seed=5)
