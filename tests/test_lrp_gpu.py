@@ -164,6 +164,15 @@ def test_zplus_rule_bit_exact(net):
         assert np.array_equal(hg.info[k], ref[k]), k
 
 
+def test_alphabeta_refused_loudly(net):
+    """AlphaBeta is restated in the oracle only; the engine must refuse it, not fall back."""
+    from drsa_audio_amd.engine.plan import EngineError
+    from drsa_audio_amd.zennit.rules import AlphaBeta
+    nm = [(["features.3"], AlphaBeta(alpha=2.0, beta=1.0)), (["classifier.0"], Epsilon(epsilon=1e-7))]
+    with pytest.raises(EngineError):
+        compute_relevances(_gpu_model(net), logmel(1, seed=3).to(DEV), NameMapComposite(nm), class_idx=0)
+
+
 def test_gradient_attributor_with_tensor_output_relevance(net):
     x = logmel(2, seed=23)
     m = _gpu_model(net)
