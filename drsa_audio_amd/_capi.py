@@ -24,6 +24,7 @@ SIGNATURES = {
     "drsa_amd_last_error": (C.c_char_p, []),
     "drsa_amd_version": (_i32, []),
     "drsa_amd_drsa_workspace_bytes": (_sz, [_i64, _i32, _i32]),
+    "drsa_amd_drsa_slab_floats": (_sz, [_i32, _i32]),
     "drsa_amd_drsa_partial": (_i32, [_fp, _fp, _i64, _i32, _i32, _fp, _fp, _vp, _sz, _vp]),
     "drsa_amd_drsa_finish": (_i32, [_fp, _i64, _i32, _i32, _fp, _fp, _fp, _i32, _ip, _vp]),
     "drsa_amd_drsa_step": (_i32, [_fp, _fp, _i64, _i32, _i32, _fp, _fp, _fp, _vp, _sz, _vp]),
@@ -32,7 +33,8 @@ SIGNATURES = {
     "drsa_amd_drsa_run_multi": (_i32, [_i32, _vp, _i32, _i32, _vp]),
     "drsa_amd_drsa_partial_bf16": (_i32, [_vp, _vp, _i64, _i32, _i32, _fp, _fp, _vp, _sz, _vp]),
     "drsa_amd_polar": (_i32, [_fp, _i32, _fp, _ip, _vp]),
-    "drsa_amd_subspace_relevances": (_i32, [_fp, _fp, _i64, _i64, _i32, _i32, _fp, _fp, _vp]),
+    "drsa_amd_subspace_relevances_workspace_bytes": (_sz, [_i64, _i64, _i32, _i32]),
+    "drsa_amd_subspace_relevances": (_i32, [_fp, _fp, _i64, _i64, _i32, _i32, _fp, _fp, _vp, _sz, _vp]),
     "drsa_amd_conv_weight_floats": (_sz, [_i32, _i32, _i32]),
     "drsa_amd_conv_fwd": (_i32, [_fp, _fp, _fp, _fp, _fp, _vp, _fp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
     "drsa_amd_conv_bwd": (_i32, [_fp, _vp, _fp, _fp, _fp, _fp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
@@ -100,6 +102,8 @@ def check(rc: int, what: str = "") -> None:
 
 
 def require_gpu(t: torch.Tensor, name: str, dtype=torch.float32) -> None:
+    if not isinstance(t, torch.Tensor):
+        raise DrsaAmdError(f"{name}: expected a torch.Tensor on the GPU, got {type(t).__name__}")
     if not t.is_cuda:
         raise DrsaAmdError(f"{name}: tensor must live on the GPU (HIP device); got {t.device}. "
                            "drsa_audio_amd has no CPU path.")

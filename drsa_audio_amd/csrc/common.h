@@ -14,7 +14,17 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // ---------------------------------------------------------------------------
 namespace drsa {
 void set_error(const char* fmt, ...);
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (current device, kernel); thread-safe.
+int ensure_smem(const void* fn, size_t bytes);
+// multiprocessor count of the current device (cached per device); thread-safe.
+int cu_count();
 }  // namespace drsa
+
+#define DRSA_SMEM(fn, bytes)                                           \
+  do {                                                                 \
+    int _rc = drsa::ensure_smem((const void*)(fn), (size_t)(bytes));   \
+    if (_rc) return _rc;                                               \
+  } while (0)
 
 #define DRSA_OK 0
 #define DRSA_EINVAL (-1)

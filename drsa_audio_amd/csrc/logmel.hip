@@ -567,7 +567,7 @@ extern "C" int drsa_amd_logmel(const float* wav, int64_t n_songs, int64_t song_s
   const size_t smem = (size_t)off * 4;
   DRSA_REQUIRE(smem <= 160 * 1024, "logmel: LDS footprint %zu B exceeds 160 KB (n_mels*width too large)", smem);
   const void* fn = fast ? (const void*)logmel800_kernel : (const void*)logmel_kernel;
-  DRSA_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+  DRSA_SMEM(fn, smem);
   if (fast)
     hipLaunchKernelGGL(logmel800_kernel, dim3((unsigned)n_chunks), dim3(LM_THREADS), smem, (hipStream_t)stream, a);
   else

@@ -44,14 +44,7 @@ const Entry* find(int cin_p, int cout_p, int W, int ng, int amode, int epi) {
 }
 
 int launch(const Entry* e, const ConvArgs& args, int batch, hipStream_t s) {
-  static const void* attr_done[512] = {nullptr};
-  static int n_done = 0;
-  bool done = false;
-  for (int i = 0; i < n_done; ++i) done |= attr_done[i] == (const void*)e->fn;
-  if (!done) {
-    DRSA_HIP(hipFuncSetAttribute((const void*)e->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->lds));
-    if (n_done < 512) attr_done[n_done++] = (const void*)e->fn;
-  }
+  DRSA_SMEM(e->fn, e->lds);   // per device, thread-safe
   const int tiles = ((args.H + e->th - 1) / e->th) * ((args.W + e->tw - 1) / e->tw);
   hipLaunchKernelGGL(e->fn, dim3(tiles, batch), dim3(kThreads), e->lds, s, args);
   DRSA_LAUNCH_CHECK();

@@ -855,8 +855,7 @@ __global__ __launch_bounds__(256) void heatmap_sort_kernel(const float* __restri
 
 template <typename F>
 int with_lds(F* fn, size_t lds) {
-  DRSA_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  return DRSA_OK;
+  return drsa::ensure_smem((const void*)fn, lds);   // per device, thread-safe
 }
 
 template <int D>
@@ -914,8 +913,7 @@ int drsa_amd_projection_fwd(const float* a, const float* U, float* h, float* ap,
   switch (D) {
 #define PF(DD)                                                                                        \
   case DD: {                                                                                          \
-    static bool set = false;                                                                          \
-    if (!set) { int rc = with_lds(projection_fwd_kernel<DD>, proj_fwd_lds<DD>()); if (rc) return rc; set = true; } \
+    { int rc = with_lds(projection_fwd_kernel<DD>, proj_fwd_lds<DD>()); if (rc) return rc; }                                  \
     hipLaunchKernelGGL(projection_fwd_kernel<DD>, grid, dim3(256), proj_fwd_lds<DD>(), s, a, U, h, ap, pooled, amax, \
                        H, W, pool);                                                                   \
     break;                                                                                            \
@@ -945,8 +943,7 @@ int drsa_amd_projection_bwd(const float* gp, const uint8_t* amax, const float* a
     switch (D) {
 #define PR(DD)                                                                                        \
   case DD: {                                                                                          \
-    static bool set = false;                                                                          \
-    if (!set) { int rc = with_lds(projection_bwd_rc_kernel<DD>, proj_bwd_rc_lds<DD>()); if (rc) return rc; set = true; } \
+    { int rc = with_lds(projection_bwd_rc_kernel<DD>, proj_bwd_rc_lds<DD>()); if (rc) return rc; }                                  \
     hipLaunchKernelGGL(projection_bwd_rc_kernel<DD>, grid, dim3(256), proj_bwd_rc_lds<DD>(), s, gp, amax, a, den, U, G, \
                        H, W, K, eps_proj, eps_den, sparse, has_den, fanout);                         \
     break;                                                                                            \
@@ -964,8 +961,7 @@ int drsa_amd_projection_bwd(const float* gp, const uint8_t* amax, const float* a
   switch (D) {
 #define PB(DD)                                                                                        \
   case DD: {                                                                                          \
-    static bool set = false;                                                                          \
-    if (!set) { int rc = with_lds(projection_bwd_kernel<DD>, proj_bwd_lds<DD>()); if (rc) return rc; set = true; } \
+    { int rc = with_lds(projection_bwd_kernel<DD>, proj_bwd_lds<DD>()); if (rc) return rc; }                                  \
     hipLaunchKernelGGL(projection_bwd_kernel<DD>, grid, dim3(256), proj_bwd_lds<DD>(), s, gp, amax, ap, h, a, den, U, \
                        G, H, W, K, eps_proj, eps_den, sparse, has_den, fanout);                               \
     break;                                                                                            \
@@ -988,12 +984,7 @@ int drsa_amd_first_layer_bwd(const float* g, const uint8_t* amax, const float* w
     const int H2 = H / 2, W2 = W / 2;
     const dim3 grid(((H2 + FQ_Y - 1) / FQ_Y) * ((W2 + FQ_X - 1) / FQ_X), Bq);
     constexpr size_t lds = sizeof(float) * FQ_C * FQ_PY * FQ_PX;
-    static bool set = false;
-    if (!set) {
-      DRSA_HIP(hipFuncSetAttribute((const void*)first_layer_bwd_pooled_kernel,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      set = true;
-    }
+    DRSA_SMEM(first_layer_bwd_pooled_kernel, lds);
     hipLaunchKernelGGL(first_layer_bwd_pooled_kernel, grid, dim3(256), lds, (hipStream_t)stream, g, amax, w2f, out,
                        C, H, W, clones);
   } else {

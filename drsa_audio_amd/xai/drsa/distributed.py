@@ -3,7 +3,7 @@
 Each rank holds a shard of the activation/context rows.  One step:
 
     gs_local = [A_r^T (R (.) C_r U) + C_r^T (R (.) A_r U)  |  S_k,r]     (drsa_amd_drsa_partial)
-    gs       = all_reduce(gs_local, SUM)                                  (RCCL over xGMI: d*d+K fp32)
+    gs       = all_reduce(gs_local, SUM)                                  (RCCL over xGMI: slab fp32)
     f, U'    = finish(gs, N_total)                                         (drsa_amd_drsa_finish)
 
 The all-reduce payload is 16.4 KB at d=64 (64.1 KB at d=128): latency-bound, one collective
@@ -30,11 +30,14 @@ class HipBackend:
     """libdrsa_amd kernels on the rank's GPU."""
 
     def __init__(self, A: torch.Tensor, C: torch.Tensor, d: int, K: int):
-        from .drsa import DrsaWorkspace
+        from .drsa import DrsaWorkspace, slab_floats
         self.A, self.C, self.d, self.K = A, C, d, K
         self.ws = DrsaWorkspace(max(A.size(0), 1), d, K, A.device)
-        self.gs = torch.empty(d * d + K, device=A.device, dtype=torch.float32)
+        self.gs = torch.empty(slab_floats(d, K), device=A.device, dtype=torch.float32)
         self.f = torch.empty(1, device=A.device, dtype=torch.float32)
+
+    def slab_size(self) -> int:
+        return self.gs.numel()
 
     def partial(self, U: torch.Tensor) -> torch.Tensor:
         _capi.call("drsa_amd_drsa_partial", self.A.data_ptr(), self.C.data_ptr(), self.A.size(0), self.d, self.K,
@@ -91,7 +94,7 @@ def sharded_run_joint(problems, steps: int, group=None, backends=None):
     if dist.is_initialized():
         dist.all_reduce(n, op=dist.ReduceOp.SUM, group=group)
     N_tot = [int(v) for v in n.tolist()]
-    sizes = [U0.size(0) ** 2 + K for _, _, U0, K in problems]
+    sizes = [b.slab_size() for b in backends]
     offs = np.concatenate([[0], np.cumsum(sizes)]).astype(int)
     Us = [U0.detach().clone().contiguous() for _, _, U0, _ in problems]
     trajs: List[List[torch.Tensor]] = [[] for _ in range(P)]

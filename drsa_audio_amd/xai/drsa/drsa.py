@@ -27,7 +27,7 @@ import torch
 from ... import _capi
 
 __all__ = ["SubspaceOptimizer", "generalized_fmean", "project_grad", "orthogonalize",
-           "objective_fn", "main", "DrsaWorkspace"]
+           "objective_fn", "main", "DrsaWorkspace", "slab_floats"]
 
 
 def _dev(device) -> torch.device:
@@ -39,6 +39,17 @@ def _dev(device) -> torch.device:
     return device
 
 
+def slab_floats(d: int, K: int) -> int:
+    """Floats of the [gradient | S] slab exchanged between drsa_partial and drsa_finish (the
+    all-reduce payload of a sharded run): d*d + K for power-of-two shapes, padded coordinates
+    otherwise (e.g. 128*128 + 4 for VGGish layer 19, d = 100, K = 4)."""
+    n = _capi.lib().drsa_amd_drsa_slab_floats(int(d), int(K))
+    if n == 0:
+        raise _capi.DrsaAmdError(f"unsupported DRSA problem d={d} K={K} (d <= 128, K | d, d/K padded to a power "
+                                 "of two <= 64 with K * padded width <= 128)")
+    return int(n)
+
+
 class DrsaWorkspace:
     """Device scratch for one (N, d, K) problem: partial slabs, reduced gradient, counters."""
 
@@ -47,9 +58,10 @@ class DrsaWorkspace:
         if nbytes == 0:
             raise _capi.DrsaAmdError(f"unsupported DRSA problem N={N} d={d} K={K}")
         self.N, self.d, self.K = int(N), int(d), int(K)
+        self.slab = int(slab_floats(d, K))
         self.buf = torch.empty(int(nbytes), dtype=torch.uint8, device=device)
         self.counter = torch.zeros(4, dtype=torch.int32, device=device)
-        self.gs = torch.empty(d * d + K, dtype=torch.float32, device=device)
+        self.gs = torch.empty(self.slab, dtype=torch.float32, device=device)
         self.f = torch.empty(1, dtype=torch.float32, device=device)
 
     @property

@@ -93,16 +93,34 @@ def get_class_composite(name_map: List[Tuple[List[str], object]], num_concepts: 
 
 def compute_subspace_relevances(act_vecs: torch.Tensor, ctx_vecs: torch.Tensor, U: torch.Tensor,
                                 n_concepts: int = 4) -> torch.Tensor:
-    """r[b, k] = sum_n sum_{j in block k} (a_n U)_j (c_n U)_j  for act/ctx [b, N, d] (or [N, d])."""
+    """r[b, k] = sum_n sum_{j in block k} (a_n U)_j (c_n U)_j  for act/ctx [b, N, d] (or [N, d]),
+    any d <= 128 with n_concepts | d (drsa_amd_subspace_relevances)."""
     assert act_vecs.dim() < 4 or ctx_vecs.dim() < 4, "Please provide act and ctx vectors reshaped to [batch, N, d]"
     a = act_vecs if act_vecs.dim() == 3 else act_vecs.unsqueeze(0)
     c = ctx_vecs if ctx_vecs.dim() == 3 else ctx_vecs.unsqueeze(0)
+    for t, name in ((a, "act_vecs"), (c, "ctx_vecs"), (U, "U")):
+        if not isinstance(t, torch.Tensor) or not t.is_cuda:
+            raise _capi.DrsaAmdError(f"compute_subspace_relevances: {name} must be a GPU tensor "
+                                     f"(drsa_audio_amd has no CPU path)")
+    if c.device != a.device or U.device != a.device:
+        raise ValueError("compute_subspace_relevances: act_vecs, ctx_vecs and U must be on one device")
+    if a.dim() != 3 or c.shape != a.shape:
+        raise ValueError(f"act_vecs and ctx_vecs must have the same [batch, N, d] shape "
+                         f"(got {tuple(act_vecs.shape)} and {tuple(ctx_vecs.shape)})")
+    b, N, d = a.shape
+    if U.shape != (d, d):
+        raise ValueError(f"U must be [{d}, {d}] for d={d} (got {tuple(U.shape)})")
+    if n_concepts <= 0 or d % n_concepts:
+        raise ValueError(f"n_concepts={n_concepts} must be a positive divisor of d={d}")
     a = a.to(torch.float32).contiguous()
     c = c.to(torch.float32).contiguous()
-    U = U.to(a.device, torch.float32).contiguous()
-    _capi.require_gpu(a, "act_vecs")
-    b, N, d = a.shape
+    U = U.to(torch.float32).contiguous()
     out = torch.empty(b, n_concepts, device=a.device)
+    nbytes = _capi.lib().drsa_amd_subspace_relevances_workspace_bytes(b, N, d, n_concepts)
+    if nbytes == 0:
+        raise _capi.DrsaAmdError(f"compute_subspace_relevances: unsupported problem b={b} N={N} d={d} "
+                                 f"n_concepts={n_concepts} (d <= 128)")
+    ws = torch.empty(int(nbytes), dtype=torch.uint8, device=a.device)
     _capi.call("drsa_amd_subspace_relevances", a.data_ptr(), c.data_ptr(), b, N, d, n_concepts, U.data_ptr(),
-               out.data_ptr(), _capi.stream_ptr(a.device))
+               out.data_ptr(), ws.data_ptr(), ws.numel(), _capi.stream_ptr(a.device))
     return out

@@ -33,16 +33,23 @@ int drsa_amd_version(void);
 
 /* ------------------------------------------------------------------------- *
  * DRSA optimiser (cxai/xai/drsa/drsa.py)
- * Supported: d in {16, 32, 64, 128}; d % K == 0; d/K in {1,2,4,8,16,32,64}.
+ * Supported: d <= 128, d % K == 0, with dk = d/K padded to DKp = next power of two (<= 64)
+ * and DP = next power of two >= max(16, K*DKp) <= 128.  d in {16,32,64,128} runs unpadded;
+ * e.g. d = 100, K = 4 (VGGish layer 19, getdrsadata.py:119) runs as DP = 128, DKp = 32.
  * ------------------------------------------------------------------------- */
 
-/* Bytes of device workspace needed by the drsa_* calls below for N rows. */
+/* Bytes of device workspace needed by the drsa_* calls below for N rows (0: unsupported). */
 size_t drsa_amd_drsa_workspace_bytes(int64_t N, int d, int K);
 
-/* Local (shard) pass: gs_out[0:d*d] = A^T (R (.) CU) + C^T (R (.) AU) (unscaled gradient,
- * R = relu block sums broadcast over each concept block), gs_out[d*d : d*d+K] = S_k =
- * sum_n relu(s_nk)^2.  Sum gs_out over shards (e.g. one RCCL all-reduce), then call
- * drsa_amd_drsa_finish with the global row count.
+/* Floats of the gradient slab gs (DP*DP + DP/DKp, padded coordinates) exchanged between
+ * drsa_amd_drsa_partial and drsa_amd_drsa_finish (the all-reduce payload of a sharded run).
+ * Equals d*d + K when d is a power of two >= 16 and d/K is a power of two; 0 if unsupported. */
+size_t drsa_amd_drsa_slab_floats(int d, int K);
+
+/* Local (shard) pass: gs_out[0:DP*DP] = A^T (R (.) CU) + C^T (R (.) AU) (unscaled gradient,
+ * R = relu block sums broadcast over each concept block), gs_out[DP*DP : DP*DP+Kp] = S_k =
+ * sum_n relu(s_nk)^2 (padded coordinates; drsa_amd_drsa_slab_floats).  Sum gs_out over
+ * shards (e.g. one RCCL all-reduce), then call drsa_amd_drsa_finish with the global row count.
  * Replaces the forward+autograd half of SubspaceOptimizer.run (drsa.py:91-100). */
 int drsa_amd_drsa_partial(const float* A, const float* C, int64_t N, int d, int K, const float* U,
                           float* gs_out, void* workspace, size_t workspace_bytes, void* stream);
@@ -70,13 +77,15 @@ int drsa_amd_drsa_run(const float* A, const float* C, int64_t N, int d, int K, f
                       int steps, float* f_traj, int* counter, void* workspace, size_t workspace_bytes,
                       int use_graph, void* stream);
 
-/* orthogonalize (drsa.py:201-221): U_out = V (V^T V)^{-1/2}, Newton-Schulz on device. */
+/* orthogonalize (drsa.py:201-221): U_out = V (V^T V)^{-1/2}, Newton-Schulz on device, d <= 128. */
 int drsa_amd_polar(const float* V, int d, float* U_out, int* iters_out, void* stream);
 
 /* compute_subspace_relevances (explainer.py:206-242): out[b][k] = sum_n sum_{j in block k}
- * (act[b][n] U)_j (ctx[b][n] U)_j for act, ctx [B][N][d]. */
+ * (act[b][n] U)_j (ctx[b][n] U)_j for act, ctx [B][N][d], d <= 128, K | d.  The workspace
+ * (drsa_amd_subspace_relevances_workspace_bytes) holds per-chunk partial sums. */
+size_t drsa_amd_subspace_relevances_workspace_bytes(int64_t B, int64_t N, int d, int K);
 int drsa_amd_subspace_relevances(const float* act, const float* ctx, int64_t B, int64_t N, int d, int K,
-                                 const float* U, float* out, void* stream);
+                                 const float* U, float* out, void* workspace, size_t workspace_bytes, void* stream);
 
 
 /* ------------------------------------------------------------------------- *

@@ -196,6 +196,122 @@ def _preprocessing():
             "norm_ctx": ns["normalize_vectors"](ctx).numpy()}
 
 
+def _extract(relpath: str, names, ns):
+    """exec ONLY the named top-level functions of a reference source file into ``ns`` (the
+    module itself imports zennit, absent here).  Nothing is persisted."""
+    import ast
+    tree = ast.parse(pathlib.Path(REF, relpath).read_text())
+    for node in tree.body:
+        if isinstance(node, ast.FunctionDef) and node.name in names:
+            exec(compile(ast.Module(body=[node], type_ignores=[]), relpath, "exec"), ns)
+    return ns
+
+
+# compute_subspace_relevances cases: (b or 0 for a 2-D [N, d] input, N, d, K, seed)
+SUBREL_CASES = [(1, 20000, 64, 4, 1), (3, 1000, 16, 1, 2), (3, 500, 64, 8, 3), (1, 3000, 128, 16, 4),
+                (3, 777, 128, 4, 5), (2, 20, 100, 4, 6), (1, 5000, 100, 4, 7), (0, 300, 64, 4, 8),
+                (3, 1, 16, 16, 9), (1, 20000, 128, 8, 10), (3, 4099, 32, 2, 11), (1, 2048, 100, 1, 12)]
+
+
+def subrel_inputs(b: int, N: int, d: int, seed: int):
+    """act = |N(0,1)| (post-ReLU), ctx = N(0,1) + 0.3, U = N(0,1)/sqrt(d) (any square matrix;
+    orthogonality is not needed by the formula, and a LAPACK-free U regenerates bit-exactly)."""
+    rng = np.random.default_rng(5000 + seed)
+    shape = (b, N, d) if b else (N, d)
+    act = np.abs(rng.standard_normal(shape)).astype(np.float32)
+    ctx = (rng.standard_normal(shape) + 0.3).astype(np.float32)
+    U = (rng.standard_normal((d, d)) / np.sqrt(d)).astype(np.float32)
+    return act, ctx, U
+
+
+def _subspace_relevances():
+    """Reference compute_subspace_relevances (explainer.py:206-242) on SUBREL_CASES."""
+    from typing import List, Tuple
+    ns = _extract("cxai/xai/explain/explainer.py", {"compute_subspace_relevances"},
+                  {"torch": torch, "np": np, "List": List, "Tuple": Tuple})
+    out = {}
+    for i, (b, N, d, K, seed) in enumerate(SUBREL_CASES):
+        act, ctx, U = subrel_inputs(b, N, d, seed)
+        r = ns["compute_subspace_relevances"](torch.from_numpy(act), torch.from_numpy(ctx),
+                                              torch.from_numpy(U), K)
+        out[f"case{i}_meta"] = np.array([b, N, d, K, seed])
+        out[f"case{i}_rel"] = r.numpy()
+        out[f"case{i}_checksum"] = np.array([act.sum(dtype=np.float64), ctx.sum(dtype=np.float64),
+                                             U.sum(dtype=np.float64)])
+    return out
+
+
+# long-horizon reference runs: tag -> (N, d, K, data seed, U0 source, steps)
+DRSA_LONG = {"c3": (20000, 64, 4, 3, "u64_seed42", 2000),     # SURVEY 8(d) C3, drsa.py:76 default
+             "c4": (160000, 64, 8, 3, "u64_seed42", 10),      # C4 shape (8 x 20 000 rows)
+             "d100": (20000, 100, 4, 13, "ortho100", 500)}    # VGGish j=19 (getdrsadata.py:119)
+
+
+def _drsa_long(rdrsa):
+    from scipy.stats import ortho_group
+    out = {}
+    for tag, (N, d, K, seed, usrc, steps) in DRSA_LONG.items():
+        A, C = drsa_inputs(N, d, seed)
+        if usrc == "u64_seed42":
+            np.random.seed(42)
+            U0 = ortho_group.rvs(64).astype(np.float32)
+        else:
+            np.random.seed(100)
+            U0 = ortho_group.rvs(d).astype(np.float32)
+        opt = rdrsa.SubspaceOptimizer(torch.from_numpy(U0), torch.from_numpy(A), torch.from_numpy(C), "/nonexistent",
+                                      num_concepts=K, device=torch.device("cpu"))
+        losses = []
+        opt.save_train_stats = lambda arr: losses.extend(float(a) for a in arr)
+        opt.save_model = lambda: None
+        t0 = __import__("time").time()
+        opt.run(steps=steps)
+        print(f"[gen_fixtures] reference run {tag}: {steps} steps in {__import__('time').time() - t0:.1f} s")
+        out[f"{tag}_meta"] = np.array([N, d, K, seed, steps])
+        out[f"{tag}_U0"] = U0
+        out[f"{tag}_A_checksum"] = np.array([A.sum(dtype=np.float64), C.sum(dtype=np.float64)])
+        out[f"{tag}_traj"] = np.array(losses)
+        out[f"{tag}_Ufinal"] = opt.U.detach().numpy().copy()
+    return out
+
+
+def _drsa_main(rdrsa):
+    """drsa.main (drsa.py:241-301) end to end on a small problem: every run's trajectory and final
+    U, captured by replacing the two save methods (no files are read back)."""
+    runs = []
+    cls = rdrsa.SubspaceOptimizer
+    orig_stats, orig_model = cls.save_train_stats, cls.save_model
+
+    def rec_stats(self, arr):
+        runs.append({"traj": np.array([float(a) for a in arr])})
+
+    def rec_model(self):
+        runs.append({"U": self.U.detach().numpy().copy()})
+    cls.save_train_stats, cls.save_model = rec_stats, rec_model
+    try:
+        A, C = drsa_inputs(3000, 32, 17)
+        with tempfile.TemporaryDirectory() as td:
+            rdrsa.main(torch.from_numpy(A), torch.from_numpy(C), td, num_concepts=4, steps=25, runs=3, seed=42,
+                       device=torch.device("cpu"))
+    finally:
+        cls.save_train_stats, cls.save_model = orig_stats, orig_model
+    # save_model is called before save_train_stats (drsa.py:119-120)
+    Us = [r["U"] for r in runs if "U" in r]
+    trajs = [r["traj"] for r in runs if "traj" in r]
+    return {"main_meta": np.array([3000, 32, 4, 17, 25, 3, 42]), "main_Ufinal": np.stack(Us),
+            "main_traj": np.stack(trajs)}
+
+
+def main_round2():
+    """Round-2 fixtures (separate files, so round-1 fixtures stay byte-identical)."""
+    OUT.mkdir(parents=True, exist_ok=True)
+    rdrsa, _, _ = _import_reference()
+    np.savez_compressed(OUT / "subspace_rel_fixture.npz", **_subspace_relevances())
+    long = _drsa_long(rdrsa)
+    long.update(_drsa_main(rdrsa))
+    np.savez_compressed(OUT / "drsa_long_fixture.npz", **long)
+    print("round-2 fixtures written to", OUT)
+
+
 def main():
     OUT.mkdir(parents=True, exist_ok=True)
     rdrsa, rcm, rmm = _import_reference()
@@ -213,4 +329,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--round2" in sys.argv:
+        main_round2()
+    else:
+        main()

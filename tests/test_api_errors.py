@@ -91,5 +91,9 @@ def test_c_abi_argument_validation_without_gpu():
     # joint DRSA: no problems
     assert lib.drsa_amd_drsa_run_multi(0, None, 10, 1, None) == -1
     # workspace size query rejects unsupported problems
-    assert lib.drsa_amd_drsa_workspace_bytes(100, 48, 4) == 0
+    assert lib.drsa_amd_drsa_workspace_bytes(100, 48, 5) == 0      # K must divide d
+    assert lib.drsa_amd_drsa_workspace_bytes(100, 100, 5) == 0     # padded 5 x 32 > 128
+    assert lib.drsa_amd_drsa_workspace_bytes(100, 100, 4) > 0      # VGGish layer 19 (padded to 128)
+    assert lib.drsa_amd_drsa_slab_floats(100, 4) == 128 * 128 + 4
+    assert lib.drsa_amd_drsa_slab_floats(64, 4) == 64 * 64 + 4
     assert lib.drsa_amd_drsa_workspace_bytes(100, 128, 3) == 0

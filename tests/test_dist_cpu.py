@@ -20,6 +20,9 @@ class OracleBackend:
     def __init__(self, A, C, d, K):
         self.A, self.C, self.d, self.K = A.double().numpy(), C.double().numpy(), d, K
 
+    def slab_size(self):
+        return self.d * self.d + self.K
+
     def partial(self, U):
         Ud = U.double().numpy()
         XA, XC = self.A @ Ud, self.C @ Ud
