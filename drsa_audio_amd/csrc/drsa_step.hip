@@ -28,6 +28,11 @@
 // all-reduce of the sharded path) is in padded coordinates: drsa_amd_drsa_slab_floats(d, K).
 #include "common.h"
 #include "drsa_amd.h"
+#include "polar_ns.h"
+
+#ifndef DRSA_PARTIAL_STAMP
+#define DRSA_PARTIAL_STAMP(slot)
+#endif
 
 #include <type_traits>
 
@@ -60,6 +65,18 @@ Geom geom(int d, int K) {
 }
 
 inline size_t slab_floats(const Geom& g) { return (size_t)g.DP * g.DP + g.Kp; }
+// per-workgroup slab stride in the workspace: 16-B aligned rows for the float4 reduce
+inline size_t slab_stride(const Geom& g) { return (slab_floats(g) + 3) / 4 * 4; }
+
+// v if keep else +0.f, by bit mask: a use that is unconditional, so the compiler neither sinks the
+// load that produced v into a branch nor has to wait for it before the use
+__device__ __forceinline__ float keep_or_zero(float v, bool keep) {
+  return __uint_as_float(__float_as_uint(v) & (keep ? 0xffffffffu : 0u));
+}
+__device__ __forceinline__ float4 keep_or_zero4(float4 v, bool keep) {
+  return make_float4(keep_or_zero(v.x, keep), keep_or_zero(v.y, keep), keep_or_zero(v.z, keep),
+                     keep_or_zero(v.w, keep));
+}
 
 // m-th padded column of the embedding (pairs with padded row d + m in the identity block)
 __device__ __forceinline__ int pad_col(int m, int K, int dk, int DKp) {
@@ -77,36 +94,131 @@ struct PCfg {
   static constexpr int CG = DP / CW;               // column groups
   static constexpr int NCB = CW / 16;              // 16-wide column blocks per group
   static constexpr int NIB = DP / 16;              // Gt row blocks
-  static constexpr int NW = (DP * CW > 4096) ? 4 : 8;
+  // waves: 16 where the registers allow (4 per SIMD hide the staging latency), fewer for wide groups
+  static constexpr int NW = (DP * CW > 4096) ? 4 : ((DP <= 64 && CW == 16) ? 16 : 8);
+  static constexpr int NT = NW * 64;
   static constexpr int KP = DP / DKP;
+  static constexpr int RT = DP <= 64 ? 128 : 96;   // rows per staged tile (one tile at N/CUs <= RT)
   static constexpr int LDA = DP + 4;               // staging row stride (16-B aligned rows)
-  static constexpr int STAGE = 2 * 16 * LDA;       // floats per wave (A and C, 16 rows)
-  static constexpr size_t stage_floats = (size_t)NW * STAGE;
+  static constexpr int NV = RT * DP / 4;           // float4 slots per matrix per tile
+  static constexpr int PFN = (NV + NT - 1) / NT;   // prefetch registers (float4) per matrix per thread
+  static constexpr size_t tile_floats = 2 * (size_t)RT * LDA;
   static constexpr size_t red_floats = (size_t)NW * DP * CW + (size_t)NW * 64 * NCB;
-  static constexpr size_t lds_bytes = (stage_floats > red_floats ? stage_floats : red_floats) * sizeof(float);
+  static constexpr size_t lds_bytes = (tile_floats > red_floats ? tile_floats : red_floats) * sizeof(float);
 };
 
 template <int DP, int DKP>
-constexpr int partial_threads() { return PCfg<DP, DKP>::NW * 64; }
+constexpr int partial_threads() { return PCfg<DP, DKP>::NT; }
 
 // BF: A and C are bf16 in HBM (C5: "bf16 MFMA projection with fp32 accumulate"); GEMM1
 // (XA = A U, XC = C U) runs on v_mfma_f32_16x16x32_bf16 with U rounded to bf16 (RNE) once per
 // launch; everything after it (relu, S, the gradient GEMM on the exactly widened A/C, slab) is fp32.
+//
+// Workgroup g owns row blocks [rb0, rb1) (16 rows each), staged RT rows at a time into LDS by
+// all threads (the next tile is prefetched into registers while the current one is computed);
+// wave w owns column group w % CG and the tile's row blocks w / CG, w / CG + NW / CG, ...
 template <int DP, int DKP, bool BF>
 __global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_kernel(
     const void* __restrict__ A_, const void* __restrict__ C_, int64_t N, int d, int K, int dk,
     const float* __restrict__ U, float* __restrict__ partials, int64_t rb_total) {
   using Cfg = PCfg<DP, DKP>;
-  constexpr int CW = Cfg::CW, CG = Cfg::CG, NCB = Cfg::NCB, NIB = Cfg::NIB, NW = Cfg::NW, KP = Cfg::KP;
-  constexpr int LDA = Cfg::LDA, WPG = NW / CG, NQ = DP / 16, NQ2 = DP / 32 > 0 ? DP / 32 : 1;
+  constexpr int CW = Cfg::CW, CG = Cfg::CG, NCB = Cfg::NCB, NIB = Cfg::NIB, NW = Cfg::NW, NT = Cfg::NT;
+  constexpr int KP = Cfg::KP, RT = Cfg::RT, LDA = Cfg::LDA, NV = Cfg::NV, PFN = Cfg::PFN;
+  constexpr int WPG = NW / CG, NQ = DP / 16, NQ2 = DP / 32 > 0 ? DP / 32 : 1;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
   const int l15 = lane & 15, lg = lane >> 4;
   const int cg = w % CG;
+  float* As = smem;                 // [RT][LDA]
+  float* Cs = smem + RT * LDA;      // [RT][LDA]
+  const float* A = reinterpret_cast<const float*>(A_);
+  const float* C = reinterpret_cast<const float*>(C_);
+  const uint16_t* Ab = reinterpret_cast<const uint16_t*>(A_);
+  const uint16_t* Cb = reinterpret_cast<const uint16_t*>(C_);
+  const bool vec = (d & 3) == 0;
 
-  // ---- embedded U for this wave's column group, in MFMA B-operand order ----
-  // fp32: ureg[cb][q][t] = Up[16q + 4lg + t][16(cg NCB + cb) + l15]
-  // bf16: ubf[cb][q2][j] = bf16(Up[32 q2 + 8 lg + j][...])
+  const int64_t rb0 = (int64_t)blockIdx.x * rb_total / gridDim.x;
+  const int64_t rb1 = (int64_t)(blockIdx.x + 1) * rb_total / gridDim.x;
+  const int ntile = (int)((rb1 - rb0 + RT / 16 - 1) / (RT / 16));
+
+  // ---- tile staging: global -> registers (prefetch) -> LDS; rows >= N and columns >= d are 0 ----
+  float4 pa[PFN], pc[PFN];
+  uint32_t okm = 0;
+  static_assert(PFN <= 32, "prefetch mask");
+  // Loads are unconditional from a clamped (always valid) address and masked afterwards, so they
+  // issue back to back with no exec branches or per-load waits.
+  auto load_tile = [&](int t) {
+    const int64_t r0 = (rb0 + (int64_t)t * (RT / 16)) * 16;
+    const int64_t rmax = rb1 * 16 < N ? rb1 * 16 : N;
+#pragma unroll
+    for (int p = 0; p < PFN; ++p) {
+      const int i = tid + p * NT;
+      const int row = (i / (DP / 4)) % RT, col = 4 * (i % (DP / 4));
+      const bool ok = i < NV && r0 + row < rmax && col < d;
+      const size_t off = ok ? (size_t)(r0 + row) * d + col : 0;
+      float4 a, c;
+      if constexpr (BF) {   // 4 bf16 -> 4 fp32 (exact)
+        if (vec) {
+          const uint2 ua = *reinterpret_cast<const uint2*>(Ab + off);
+          const uint2 uc = *reinterpret_cast<const uint2*>(Cb + off);
+          a = make_float4(__uint_as_float(ua.x << 16), __uint_as_float(ua.x & 0xffff0000u),
+                          __uint_as_float(ua.y << 16), __uint_as_float(ua.y & 0xffff0000u));
+          c = make_float4(__uint_as_float(uc.x << 16), __uint_as_float(uc.x & 0xffff0000u),
+                          __uint_as_float(uc.y << 16), __uint_as_float(uc.y & 0xffff0000u));
+        } else {
+          float va[4], vc[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const size_t o = (ok && col + u < d) ? off + u : 0;
+            const uint32_t xa = Ab[o], xc = Cb[o];
+            va[u] = keep_or_zero(__uint_as_float(xa << 16), col + u < d);
+            vc[u] = keep_or_zero(__uint_as_float(xc << 16), col + u < d);
+          }
+          a = make_float4(va[0], va[1], va[2], va[3]);
+          c = make_float4(vc[0], vc[1], vc[2], vc[3]);
+        }
+      } else {
+        if (vec) {
+          a = *reinterpret_cast<const float4*>(A + off);
+          c = *reinterpret_cast<const float4*>(C + off);
+        } else {
+          float va[4], vc[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const size_t o = (ok && col + u < d) ? off + u : 0;
+            const float xa = A[o], xc = C[o];
+            va[u] = keep_or_zero(xa, col + u < d);
+            vc[u] = keep_or_zero(xc, col + u < d);
+          }
+          a = make_float4(va[0], va[1], va[2], va[3]);
+          c = make_float4(vc[0], vc[1], vc[2], vc[3]);
+        }
+      }
+      pa[p] = a;                       // masked at the store (no wait for the data here)
+      pc[p] = c;
+      okm = (okm & ~(1u << p)) | ((ok ? 1u : 0u) << p);
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int p = 0; p < PFN; ++p) {
+      const int i = tid + p * NT;
+      if (i < NV) {
+        const int row = i / (DP / 4), col = 4 * (i % (DP / 4));
+        const bool ok = (okm >> p) & 1u;
+        *reinterpret_cast<float4*>(As + row * LDA + col) = keep_or_zero4(pa[p], ok);
+        *reinterpret_cast<float4*>(Cs + row * LDA + col) = keep_or_zero4(pc[p], ok);
+      }
+    }
+  };
+  DRSA_PARTIAL_STAMP(0);
+  if (ntile > 0) load_tile(0);
+  DRSA_PARTIAL_STAMP(1);
+
+  // ---- embedded U for this wave's column group, in MFMA B-operand order (loads all independent,
+  //      issued back to back, overlapping the tile loads above) ----
+  //   fp32: ureg[cb][q][t] = Up[16q + 4lg + t][16(cg NCB + cb) + l15]
+  //   bf16: ubf[cb][q2][j] = bf16(Up[32 q2 + 8 lg + j][...])
   float ureg[BF ? 1 : NCB][BF ? 1 : NQ][4];
   u16x8 ubf[BF ? NCB : 1][BF ? NQ2 : 1];
 #pragma unroll
@@ -114,14 +226,15 @@ __global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_ker
     const int jp = 16 * (cg * NCB + cb) + l15;
     const int kc = jp / DKP, l = jp % DKP;
     const bool real = kc < K && l < dk;
-    const int j = kc * dk + l;
+    const int j = real ? kc * dk + l : 0;
     if constexpr (!BF) {
 #pragma unroll
       for (int q = 0; q < NQ; ++q)
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const int k = 16 * q + 4 * lg + t;
-          ureg[cb][q][t] = (real && k < d) ? U[(size_t)k * d + j] : 0.f;
+          const float v = U[(size_t)(k < d ? k : 0) * d + j];   // clamped address, masked after
+          ureg[cb][q][t] = keep_or_zero(v, real && k < d);
         }
     } else {
 #pragma unroll
@@ -129,7 +242,8 @@ __global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_ker
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) {
           const int k = 32 * q2 + 8 * lg + jj;
-          const uint32_t u = __float_as_uint((real && k < d) ? U[(size_t)k * d + j] : 0.f);
+          const float v = U[(size_t)(k < d ? k : 0) * d + j];
+          const uint32_t u = __float_as_uint(keep_or_zero(v, real && k < d));
           ubf[cb][q2][jj] = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
         }
     }
@@ -143,171 +257,130 @@ __global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_ker
   float sacc[NCB];
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb) sacc[cb] = 0.f;
-
-  float* As = smem + (size_t)w * Cfg::STAGE;
-  float* Cs = As + 16 * LDA;
-  const float* A = reinterpret_cast<const float*>(A_);
-  const float* C = reinterpret_cast<const float*>(C_);
-  const uint16_t* Ab = reinterpret_cast<const uint16_t*>(A_);
-  const uint16_t* Cb = reinterpret_cast<const uint16_t*>(C_);
   const int nq_live = (d + 15) / 16;   // k chunks / Gt row blocks that can be nonzero
 
-  const int64_t rb0 = (int64_t)blockIdx.x * rb_total / gridDim.x;
-  const int64_t rb1 = (int64_t)(blockIdx.x + 1) * rb_total / gridDim.x;
-  for (int64_t rb = rb0 + w / CG; rb < rb1; rb += WPG) {
-    const int64_t r0 = rb * 16;
-    // ---- stage 16 rows of A and C (rows >= N and columns >= d are zero) ----
-    if ((d & 3) == 0) {
-      for (int i = lane; i < 16 * (DP / 4); i += 64) {
-        const int row = i / (DP / 4), col = 4 * (i % (DP / 4));
-        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), c = a;
-        if (r0 + row < N && col < d) {
-          const size_t off = (size_t)(r0 + row) * d + col;
-          if constexpr (BF) {   // 4 bf16 -> 4 fp32 (exact)
-            const uint2 ua = *reinterpret_cast<const uint2*>(Ab + off);
-            const uint2 uc = *reinterpret_cast<const uint2*>(Cb + off);
-            a = make_float4(__uint_as_float(ua.x << 16), __uint_as_float(ua.x & 0xffff0000u),
-                            __uint_as_float(ua.y << 16), __uint_as_float(ua.y & 0xffff0000u));
-            c = make_float4(__uint_as_float(uc.x << 16), __uint_as_float(uc.x & 0xffff0000u),
-                            __uint_as_float(uc.y << 16), __uint_as_float(uc.y & 0xffff0000u));
-          } else {
-            a = *reinterpret_cast<const float4*>(A + off);
-            c = *reinterpret_cast<const float4*>(C + off);
-          }
+  DRSA_PARTIAL_STAMP(2);
+  if (ntile > 0) store_tile();
+  __syncthreads();
+  DRSA_PARTIAL_STAMP(3);
+  for (int t = 0; t < ntile; ++t) {
+    if (t + 1 < ntile) load_tile(t + 1);
+    const int64_t rbt = rb0 + (int64_t)t * (RT / 16);
+    const int nrb = (int)((rb1 - rbt) < (RT / 16) ? (rb1 - rbt) : (RT / 16));
+    for (int rbl = w / CG; rbl < nrb; rbl += WPG) {
+      const float* Ar = As + 16 * rbl * LDA;
+      const float* Cr = Cs + 16 * rbl * LDA;
+      // ---- GEMM1: XA, XC for the 16 rows and this wave's NCB column blocks ----
+      f32x4 xa[NCB], xc[NCB];
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) { xa[cb] = f32x4{0.f, 0.f, 0.f, 0.f}; xc[cb] = xa[cb]; }
+      if constexpr (!BF) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          if (q >= nq_live) break;
+          const float4 a4 = *reinterpret_cast<const float4*>(Ar + l15 * LDA + 16 * q + 4 * lg);
+          const float4 c4 = *reinterpret_cast<const float4*>(Cr + l15 * LDA + 16 * q + 4 * lg);
+          const float av[4] = {a4.x, a4.y, a4.z, a4.w}, cv[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+          for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+            for (int cb = 0; cb < NCB; ++cb) {
+              xa[cb] = mfma16(av[tt], ureg[cb][q][tt], xa[cb]);
+              xc[cb] = mfma16(cv[tt], ureg[cb][q][tt], xc[cb]);
+            }
         }
-        *reinterpret_cast<float4*>(As + row * LDA + col) = a;
-        *reinterpret_cast<float4*>(Cs + row * LDA + col) = c;
-      }
-    } else {
-      for (int i = lane; i < 16 * DP; i += 64) {
-        const int row = i / DP, col = i % DP;
-        float a = 0.f, c = 0.f;
-        if (r0 + row < N && col < d) {
-          const size_t off = (size_t)(r0 + row) * d + col;
-          if constexpr (BF) {
-            a = __uint_as_float((uint32_t)Ab[off] << 16);
-            c = __uint_as_float((uint32_t)Cb[off] << 16);
-          } else {
-            a = A[off];
-            c = C[off];
-          }
-        }
-        As[row * LDA + col] = a;
-        Cs[row * LDA + col] = c;
-      }
-    }
-    // The staging writes and the reads below are this wave's own LDS traffic (in order per
-    // wave); the fence keeps the compiler from moving reads above the writes.
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-    // ---- GEMM1: XA, XC for the 16 rows and this wave's NCB column blocks ----
-    f32x4 xa[NCB], xc[NCB];
+      } else {
 #pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) { xa[cb] = f32x4{0.f, 0.f, 0.f, 0.f}; xc[cb] = xa[cb]; }
-    if constexpr (!BF) {
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        if (q >= nq_live) break;
-        const float4 a4 = *reinterpret_cast<const float4*>(As + l15 * LDA + 16 * q + 4 * lg);
-        const float4 c4 = *reinterpret_cast<const float4*>(Cs + l15 * LDA + 16 * q + 4 * lg);
-        const float av[4] = {a4.x, a4.y, a4.z, a4.w}, cv[4] = {c4.x, c4.y, c4.z, c4.w};
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
+        for (int q2 = 0; q2 < NQ2; ++q2) {
+          const float* pa8 = Ar + l15 * LDA + 32 * q2 + 8 * lg;
+          const float* pc8 = Cr + l15 * LDA + 32 * q2 + 8 * lg;
+          const float4 a0 = *reinterpret_cast<const float4*>(pa8), a1 = *reinterpret_cast<const float4*>(pa8 + 4);
+          const float4 c0 = *reinterpret_cast<const float4*>(pc8), c1 = *reinterpret_cast<const float4*>(pc8 + 4);
+          u16x8 ab, cbv;   // widened bf16 values: the top 16 bits are exact
+          ab[0] = __float_as_uint(a0.x) >> 16; ab[1] = __float_as_uint(a0.y) >> 16;
+          ab[2] = __float_as_uint(a0.z) >> 16; ab[3] = __float_as_uint(a0.w) >> 16;
+          ab[4] = __float_as_uint(a1.x) >> 16; ab[5] = __float_as_uint(a1.y) >> 16;
+          ab[6] = __float_as_uint(a1.z) >> 16; ab[7] = __float_as_uint(a1.w) >> 16;
+          cbv[0] = __float_as_uint(c0.x) >> 16; cbv[1] = __float_as_uint(c0.y) >> 16;
+          cbv[2] = __float_as_uint(c0.z) >> 16; cbv[3] = __float_as_uint(c0.w) >> 16;
+          cbv[4] = __float_as_uint(c1.x) >> 16; cbv[5] = __float_as_uint(c1.y) >> 16;
+          cbv[6] = __float_as_uint(c1.z) >> 16; cbv[7] = __float_as_uint(c1.w) >> 16;
 #pragma unroll
           for (int cb = 0; cb < NCB; ++cb) {
-            xa[cb] = mfma16(av[t], ureg[cb][q][t], xa[cb]);
-            xc[cb] = mfma16(cv[t], ureg[cb][q][t], xc[cb]);
+            xa[cb] = mfma16_bf16(ab, ubf[cb][q2], xa[cb]);
+            xc[cb] = mfma16_bf16(cbv, ubf[cb][q2], xc[cb]);
           }
-      }
-    } else {
-#pragma unroll
-      for (int q2 = 0; q2 < NQ2; ++q2) {
-        const float* pa = As + l15 * LDA + 32 * q2 + 8 * lg;
-        const float* pc = Cs + l15 * LDA + 32 * q2 + 8 * lg;
-        const float4 a0 = *reinterpret_cast<const float4*>(pa), a1 = *reinterpret_cast<const float4*>(pa + 4);
-        const float4 c0 = *reinterpret_cast<const float4*>(pc), c1 = *reinterpret_cast<const float4*>(pc + 4);
-        u16x8 ab, cbv;   // widened bf16 values: the top 16 bits are exact
-        ab[0] = __float_as_uint(a0.x) >> 16; ab[1] = __float_as_uint(a0.y) >> 16;
-        ab[2] = __float_as_uint(a0.z) >> 16; ab[3] = __float_as_uint(a0.w) >> 16;
-        ab[4] = __float_as_uint(a1.x) >> 16; ab[5] = __float_as_uint(a1.y) >> 16;
-        ab[6] = __float_as_uint(a1.z) >> 16; ab[7] = __float_as_uint(a1.w) >> 16;
-        cbv[0] = __float_as_uint(c0.x) >> 16; cbv[1] = __float_as_uint(c0.y) >> 16;
-        cbv[2] = __float_as_uint(c0.z) >> 16; cbv[3] = __float_as_uint(c0.w) >> 16;
-        cbv[4] = __float_as_uint(c1.x) >> 16; cbv[5] = __float_as_uint(c1.y) >> 16;
-        cbv[6] = __float_as_uint(c1.z) >> 16; cbv[7] = __float_as_uint(c1.w) >> 16;
-#pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) {
-          xa[cb] = mfma16_bf16(ab, ubf[cb][q2], xa[cb]);
-          xc[cb] = mfma16_bf16(cbv, ubf[cb][q2], xc[cb]);
         }
       }
-    }
 
-    // ---- s = sum over the concept block of XA (.) XC, r = relu(s); S partial ----
-    // lane holds rows 4 lg + r, column 16 (cg NCB + cb) + l15
-    float rr[NCB][4];
-    if constexpr (DKP >= 16) {   // the whole column group is one concept
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = 0.f;
-#pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) v += xa[cb][r] * xc[cb][r];
-        v += shfl_xor(v, 1); v += shfl_xor(v, 2); v += shfl_xor(v, 4); v += shfl_xor(v, 8);
-        const float rv = v > 0.f ? v : 0.f;
-#pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) rr[cb][r] = rv;
-      }
-      if (l15 == 0) {
-        float acc = 0.f;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc += rr[0][r] * rr[0][r];
-        sacc[0] += acc;
-      }
-    } else {
-#pragma unroll
-      for (int cb = 0; cb < NCB; ++cb) {
+      // ---- s = sum over the concept block of XA (.) XC, r = relu(s); S partial ----
+      // lane holds rows 4 lg + r, column 16 (cg NCB + cb) + l15
+      float rr[NCB][4];
+      if constexpr (DKP >= 16) {   // the whole column group is one concept
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float v = xa[cb][r] * xc[cb][r];
-          if constexpr (DKP >= 2) v += shfl_xor(v, 1);
-          if constexpr (DKP >= 4) v += shfl_xor(v, 2);
-          if constexpr (DKP >= 8) v += shfl_xor(v, 4);
-          rr[cb][r] = v > 0.f ? v : 0.f;
+          float v = 0.f;
+#pragma unroll
+          for (int cb = 0; cb < NCB; ++cb) v += xa[cb][r] * xc[cb][r];
+          v += shfl_xor(v, 1); v += shfl_xor(v, 2); v += shfl_xor(v, 4); v += shfl_xor(v, 8);
+          const float rv = v > 0.f ? v : 0.f;
+#pragma unroll
+          for (int cb = 0; cb < NCB; ++cb) rr[cb][r] = rv;
         }
-        if ((l15 % DKP) == 0) {
+        if (l15 == 0) {
           float acc = 0.f;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc += rr[cb][r] * rr[cb][r];
-          sacc[cb] += acc;
+          for (int r = 0; r < 4; ++r) acc += rr[0][r] * rr[0][r];
+          sacc[0] += acc;
         }
-      }
-    }
-
-    // ---- GEMM2: Gt[i][j] += sum_n A[n][i] P[n][j] + C[n][i] Q[n][j]  (P = r XC, Q = r XA) ----
-    // k-step t covers rows n = 4 lg + t: the B operand is this lane's own MFMA output register t.
-#pragma unroll
-    for (int ib = 0; ib < NIB; ++ib) {
-      if (ib >= nq_live) break;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const float av = As[(4 * lg + t) * LDA + 16 * ib + l15];
-        const float cv = Cs[(4 * lg + t) * LDA + 16 * ib + l15];
+      } else {
 #pragma unroll
         for (int cb = 0; cb < NCB; ++cb) {
-          g[ib][cb] = mfma16(av, rr[cb][t] * xc[cb][t], g[ib][cb]);
-          g[ib][cb] = mfma16(cv, rr[cb][t] * xa[cb][t], g[ib][cb]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = xa[cb][r] * xc[cb][r];
+            if constexpr (DKP >= 2) v += shfl_xor(v, 1);
+            if constexpr (DKP >= 4) v += shfl_xor(v, 2);
+            if constexpr (DKP >= 8) v += shfl_xor(v, 4);
+            rr[cb][r] = v > 0.f ? v : 0.f;
+          }
+          if ((l15 % DKP) == 0) {
+            float acc = 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc += rr[cb][r] * rr[cb][r];
+            sacc[cb] += acc;
+          }
+        }
+      }
+
+      // ---- GEMM2: Gt[i][j] += sum_n A[n][i] P[n][j] + C[n][i] Q[n][j]  (P = r XC, Q = r XA) ----
+      // k-step tt covers rows n = 4 lg + tt: the B operand is this lane's own MFMA output register.
+#pragma unroll
+      for (int ib = 0; ib < NIB; ++ib) {
+        if (ib >= nq_live) break;
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) {
+          const float av = Ar[(4 * lg + tt) * LDA + 16 * ib + l15];
+          const float cv = Cr[(4 * lg + tt) * LDA + 16 * ib + l15];
+#pragma unroll
+          for (int cb = 0; cb < NCB; ++cb) {
+            g[ib][cb] = mfma16(av, rr[cb][tt] * xc[cb][tt], g[ib][cb]);
+            g[ib][cb] = mfma16(cv, rr[cb][tt] * xa[cb][tt], g[ib][cb]);
+          }
         }
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (t + 1 < ntile) {
+      __syncthreads();
+      store_tile();
+      __syncthreads();
+    }
   }
 
   // ---- combine the waves of each column group in a fixed order -> slab ----
+  DRSA_PARTIAL_STAMP(4);
   __syncthreads();
+  DRSA_PARTIAL_STAMP(5);
   float* red = smem;                                  // [NW][DP][CW]
   float* sred = smem + (size_t)NW * DP * CW;          // [NW][64][NCB]
 #pragma unroll
@@ -319,26 +392,30 @@ __global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_ker
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb) sred[(w * 64 + lane) * NCB + cb] = sacc[cb];
   __syncthreads();
-  float* slab = partials + (size_t)blockIdx.x * (DP * DP + KP);
-  for (int e = tid; e < DP * DP; e += NW * 64) {
+  float* slab = partials + (size_t)blockIdx.x * ((DP * DP + KP + 3) / 4 * 4);
+  for (int e = tid; e < DP * DP; e += NT) {
     const int i = e / DP, j = e % DP, gcg = j / CW, jj = j % CW;
     float acc = 0.f;
     for (int ww = gcg; ww < NW; ww += CG) acc += red[((size_t)ww * DP + i) * CW + jj];
     slab[e] = acc;
   }
-  for (int k = tid; k < KP; k += NW * 64) {
+  for (int k = tid; k < KP; k += NT) {
     const int j0 = k * DKP, gcg = j0 / CW, cb = (j0 % CW) / 16, lo = DKP < 16 ? j0 % 16 : 0;
     float acc = 0.f;
     for (int ww = gcg; ww < NW; ww += CG)
       for (int q = 0; q < 4; ++q) acc += sred[(ww * 64 + 16 * q + lo) * NCB + cb];
     slab[DP * DP + k] = acc;
   }
+  DRSA_PARTIAL_STAMP(6);
 }
 
 // ---------------------------------------------------------------------------
-// reduce: out[e] = sum_p partials[p][e]   (fixed order: 4 interleaved chains, combined in order)
+// reduce: out[e] = sum_p partials[p][e] over the P workgroup slabs (row stride ES); fixed order:
+// 4 interleaved chains p = g, g + 4, ... combined in order g = 0..3 (deterministic, no atomics).
+// (Measured against float4 / 64-group and slab-split variants in scripts/probe_reduce.hip: the
+// kernel boundary behind 4-17 MB of freshly written slabs dominates; this one is the fastest.)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void drsa_reduce_kernel(const float* __restrict__ partials, int P, int E,
+__global__ __launch_bounds__(256) void drsa_reduce_kernel(const float* __restrict__ partials, int P, int E, int ES,
                                                           float* __restrict__ out) {
   __shared__ float part[4][64];
   const int l = threadIdx.x & 63, grp = threadIdx.x >> 6;
@@ -346,139 +423,34 @@ __global__ __launch_bounds__(256) void drsa_reduce_kernel(const float* __restric
   float acc = 0.f;
   if (e < E) {
 #pragma unroll 8
-    for (int p = grp; p < P; p += 4) acc += partials[(size_t)p * E + e];
+    for (int p = grp; p < P; p += 4) acc += partials[(size_t)p * ES + e];
   }
   part[grp][l] = acc;
   __syncthreads();
   if (grp == 0 && e < E) out[e] = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
 }
 
-// ---------------------------------------------------------------------------
-// polar factor by Newton-Schulz, one workgroup, matrices in LDS [DP][LD]
-//   X0 = a V (a from the first Gram matrix: sqrt(DP / tr) unless that overshoots the inf-norm);
-//   P = X^T X (upper block triangle, mirrored), T = 1.5 I - 0.5 P, X <- X T until max|P - I| < tol.
-// ---------------------------------------------------------------------------
+// the polar runs at PD = max(32, DP) (32x32 MFMA tiles; a d <= 16 problem is embedded once more)
 template <int DP>
-constexpr int fin_threads() { return DP >= 64 ? 1024 : 256; }
+constexpr int polar_dim() { return DP < 32 ? 32 : DP; }
 template <int DP>
-constexpr int ns_ld() { return DP + 16; }   // column reads (the Gram operands) hit 64 distinct banks
-
-template <int NT>
-__device__ float block_max(float v, float* red) {
-  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, shfl_xor(v, m));
-  __syncthreads();
-  if (lane_id() == 0) red[wave_id()] = v;
-  __syncthreads();
-  float r = red[0];
-#pragma unroll
-  for (int i = 1; i < NT / 64; ++i) r = fmaxf(r, red[i]);
-  return r;
+constexpr size_t finish_lds() {
+  return (2 * (size_t)polar_dim<DP>() * ns_ld<polar_dim<DP>()>() + 64 + ns_scratch_floats<polar_dim<DP>()>()) *
+         sizeof(float);
 }
-
-template <int DP>
-__device__ int polar_ns(float* X, float* T, float* red, float tol, int max_iter) {
-  constexpr int NT = fin_threads<DP>(), LD = ns_ld<DP>(), NB = DP / 16, NWV = NT / 64;
-  constexpr int NSYM = NB * (NB + 1) / 2, NFULL = NB * NB, NTW = (NFULL + NWV - 1) / NWV;
-  constexpr int TPR = NT / DP;   // threads per row in the inf-norm pass (8 or 16)
-  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
-  const int l15 = lane & 15, lg = lane >> 4;
-  int it = 0;
-  for (;; ++it) {
-    __syncthreads();   // X complete
-    // ---- P = X^T X on the upper block triangle, written (and mirrored) into T ----
-    for (int t = w; t < NSYM; t += NWV) {
-      int ib = 0, rem = t;
-      while (rem >= NB - ib) { rem -= NB - ib; ++ib; }
-      const int jb = ib + rem;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-      for (int k0 = 0; k0 < DP; k0 += 4) {
-        const int kk = k0 + lg;
-        acc = mfma16(X[kk * LD + 16 * ib + l15], X[kk * LD + 16 * jb + l15], acc);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * ib + 4 * lg + r, col = 16 * jb + l15;
-        T[row * LD + col] = acc[r];
-        if (ib != jb) T[col * LD + row] = acc[r];   // X^T X is exactly symmetric (products commute)
-      }
-    }
-    __syncthreads();
-    if (it == 0) {
-      // scaling a^2 = DP / tr(P) if a^2 ||P||_inf < 2.9 else 1 / ||P||_inf (fixed-order sums)
-      float tr = 0.f;
-      for (int i = lane; i < DP; i += 64) tr += T[i * LD + i];
-      for (int m = 32; m >= 1; m >>= 1) tr += shfl_xor(tr, m);   // every wave gets the same value
-      const int row = tid / TPR, part = tid % TPR;
-      float rs = 0.f;
-      for (int c = part; c < DP; c += TPR) rs += fabsf(T[row * LD + c]);
-      for (int m = 1; m < TPR; m <<= 1) rs += shfl_xor(rs, m);
-      const float rowmax = block_max<NT>(rs, red);
-      float a2 = (float)DP / tr;
-      if (a2 * rowmax >= 2.9f) a2 = 1.f / rowmax;
-      const float a = sqrtf(a2);
-      for (int e = tid; e < DP * DP; e += NT) {
-        const int r = e / DP, c = e % DP;
-        X[r * LD + c] *= a;
-        T[r * LD + c] *= a2;
-      }
-      __syncthreads();
-    }
-    // ---- err = max|P - I|, T = 1.5 I - 0.5 P ----
-    float err = 0.f;
-    for (int e = tid; e < DP * DP; e += NT) {
-      const int r = e / DP, c = e % DP;
-      const float pv = T[r * LD + c];
-      err = fmaxf(err, fabsf(pv - (r == c ? 1.f : 0.f)));
-      T[r * LD + c] = (r == c ? 1.5f : 0.f) - 0.5f * pv;
-    }
-    err = block_max<NT>(err, red + 32);
-    if (err < tol || it >= max_iter) break;
-    // ---- X <- X T (all reads before any write) ----
-    f32x4 acc[NTW];
-#pragma unroll
-    for (int q = 0; q < NTW; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-    for (int k0 = 0; k0 < DP; k0 += 4) {
-      const int kk = k0 + lg;
-#pragma unroll
-      for (int q = 0; q < NTW; ++q) {
-        const int t = w + NWV * q;
-        if (t < NFULL) {
-          const int ib = t / NB, jb = t % NB;
-          acc[q] = mfma16(X[(16 * ib + l15) * LD + kk], T[kk * LD + 16 * jb + l15], acc[q]);
-        }
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < NTW; ++q) {
-      const int t = w + NWV * q;
-      if (t < NFULL) {
-        const int ib = t / NB, jb = t % NB;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) X[(16 * ib + 4 * lg + r) * LD + 16 * jb + l15] = acc[q][r];
-      }
-    }
-  }
-  __syncthreads();
-  return it;
-}
-
-template <int DP>
-constexpr size_t finish_lds() { return (2 * (size_t)DP * ns_ld<DP>() + 64) * sizeof(float); }
 
 // mode 0: full step (f, U_out = polar(U + G)); mode 1: objective only
 template <int DP>
-__global__ __launch_bounds__(fin_threads<DP>()) void drsa_finish_kernel(
+__global__ __launch_bounds__(fin_threads<polar_dim<DP>()>()) void drsa_finish_kernel(
     const float* __restrict__ gs, double n_total, int d, int K, int DKP, const float* __restrict__ U,
     float* __restrict__ U_out, float* __restrict__ f_out, int* __restrict__ step_counter, int f_stride_by_counter,
     int mode, float tol, int max_iter, int* __restrict__ iters_out) {
-  constexpr int NT = fin_threads<DP>(), LD = ns_ld<DP>();
+  constexpr int PD = polar_dim<DP>(), NT = fin_threads<PD>(), LD = ns_ld<PD>();
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* X = smem;
-  float* T = X + DP * LD;
-  float* red = T + DP * LD;   // 64 floats
+  float* T = X + PD * LD;
+  float* red = T + PD * LD;   // 64 floats
+  float* scr = red + 64;      // k-split partial tiles (polar_ns)
   __shared__ double dterm[128];
   __shared__ float cvec[128];
   __shared__ double fsh;
@@ -503,15 +475,20 @@ __global__ __launch_bounds__(fin_threads<DP>()) void drsa_finish_kernel(
   if (tid == 0) f_out[slot] = (float)f;
   if (mode == 1) return;
   __syncthreads();
-  // X = embed(U + Gt diag(c))
-  for (int e = tid; e < DP * DP; e += NT) {
-    const int ip = e / DP, jp = e % DP, kc = jp / DKP, l = jp % DKP;
-    float v;
-    if (ip < d) v = (kc < K && l < dk) ? U[(size_t)ip * d + kc * dk + l] + gs[e] * cvec[kc] : 0.f;
-    else v = (jp == pad_col(ip - d, K, dk, DKP)) ? 1.f : 0.f;
-    X[ip * LD + jp] = v;
+  // X = embed(U + Gt diag(c)); padded rows pair with the padded columns through an identity block
+  // (loads from clamped addresses, pinned, so all of them are in flight at once: no exec branches)
+#pragma unroll
+  for (int q = 0; q < (PD * PD + NT - 1) / NT; ++q) {
+    const int e = tid + q * NT;
+    const int ip = e / PD, jp = e % PD, kc = jp / DKP, l = jp % DKP;
+    const bool real = e < PD * PD && ip < d && jp < DP && kc < K && l < dk;
+    const float u = U[real ? (size_t)ip * d + kc * dk + l : 0];
+    const float gv = gs[real ? ip * DP + jp : 0];
+    const float rv = keep_or_zero(u + gv * cvec[kc < K ? kc : 0], real);
+    const float v = ip < d ? rv : ((jp == pad_col(ip - d, K, dk, DKP)) ? 1.f : 0.f);
+    if (e < PD * PD) X[ip * LD + jp] = v;
   }
-  const int it = polar_ns<DP>(X, T, red, tol, max_iter);
+  const int it = polar_ns<PD>(X, T, red, scr, tol, max_iter);
   for (int e = tid; e < d * d; e += NT) {
     const int i = e / d, j = e % d;
     U_out[e] = X[i * LD + (j / dk) * DKP + j % dk];
@@ -522,7 +499,7 @@ __global__ __launch_bounds__(fin_threads<DP>()) void drsa_finish_kernel(
   }
 }
 
-// polar only (orthogonalize API): any d <= 128, embedded as diag(V, I) in DP = pow2ceil(d)
+// polar only (orthogonalize API): any d <= 128, embedded as diag(V, I) in DP = pow2ceil(max(32, d))
 template <int DP>
 __global__ __launch_bounds__(fin_threads<DP>()) void polar_kernel(const float* __restrict__ V, int d,
                                                                   float* __restrict__ U_out, float tol, int max_iter,
@@ -532,11 +509,16 @@ __global__ __launch_bounds__(fin_threads<DP>()) void polar_kernel(const float* _
   float* X = smem;
   float* T = X + DP * LD;
   float* red = T + DP * LD;
-  for (int e = threadIdx.x; e < DP * DP; e += NT) {
+  float* scr = red + 64;
+#pragma unroll
+  for (int q = 0; q < (DP * DP + NT - 1) / NT; ++q) {
+    const int e = threadIdx.x + q * NT;
     const int i = e / DP, j = e % DP;
-    X[i * LD + j] = (i < d && j < d) ? V[(size_t)i * d + j] : (i == j ? 1.f : 0.f);
+    const bool real = e < DP * DP && i < d && j < d;
+    const float v = keep_or_zero(V[real ? (size_t)i * d + j : 0], real);
+    if (e < DP * DP) X[i * LD + j] = (i < d && j < d) ? v : (i == j ? 1.f : 0.f);
   }
-  const int it = polar_ns<DP>(X, T, red, tol, max_iter);
+  const int it = polar_ns<DP>(X, T, red, scr, tol, max_iter);
   for (int e = threadIdx.x; e < d * d; e += NT) U_out[e] = X[(e / d) * LD + e % d];
   if (iters_out && threadIdx.x == 0) *iters_out = it;
 }
@@ -562,7 +544,7 @@ int launch_partial(const void* A, const void* C, int64_t N, const Geom& g, const
                    const PartialPlan& pl, hipStream_t s) {
   using Cfg = PCfg<DP, DKP>;
   DRSA_SMEM((drsa_partial_kernel<DP, DKP, BF>), Cfg::lds_bytes);
-  hipLaunchKernelGGL((drsa_partial_kernel<DP, DKP, BF>), dim3(pl.grid), dim3(Cfg::NW * 64), Cfg::lds_bytes, s, A, C,
+  hipLaunchKernelGGL((drsa_partial_kernel<DP, DKP, BF>), dim3(pl.grid), dim3(Cfg::NT), Cfg::lds_bytes, s, A, C,
                      N, g.d, g.K, g.dk, U, partials, pl.rb_total);
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;
@@ -607,7 +589,8 @@ int launch_finish(const float* gs, double n_total, const Geom& g, const float* U
                   int* counter, int by_counter, int mode, float tol, int max_iter, int* iters, hipStream_t s) {
   const size_t lds = finish_lds<DP>();
   DRSA_SMEM(drsa_finish_kernel<DP>, lds);
-  hipLaunchKernelGGL(drsa_finish_kernel<DP>, dim3(1), dim3(fin_threads<DP>()), lds, s, gs, n_total, g.d, g.K, g.DKp,
+  hipLaunchKernelGGL(drsa_finish_kernel<DP>, dim3(1), dim3(fin_threads<polar_dim<DP>()>()), lds, s, gs, n_total, g.d,
+                     g.K, g.DKp,
                      U, U_out, f_out, counter, by_counter, mode, tol, max_iter, iters);
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;
@@ -630,8 +613,7 @@ constexpr int kPolarMaxIter = 40;
 // workspace layout: [partials grid*E] [gs E] [16 B pad]
 size_t ws_bytes(int64_t N, const Geom& g) {
   const PartialPlan pl = plan_partial(N);
-  const size_t E = slab_floats(g);
-  return ((size_t)pl.grid * E + E) * sizeof(float) + 64;
+  return ((size_t)pl.grid * slab_stride(g) + slab_floats(g)) * sizeof(float) + 64;
 }
 
 int partial_impl(const void* A, const void* C, int64_t N, int d, int K, const float* U, float* gs_out, void* ws,
@@ -654,14 +636,15 @@ int partial_impl(const void* A, const void* C, int64_t N, int d, int K, const fl
   float* partials = (float*)ws;
   int rc = dispatch_partial(A, C, N, g, U, partials, pl, s, dtype == 1);
   if (rc) return rc;
+  const size_t ES = slab_stride(g);
   hipLaunchKernelGGL(drsa_reduce_kernel, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, s, partials, pl.grid, (int)E,
-                     gs_out);
+                     (int)ES, gs_out);
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;
 }
 
 float* ws_gs(void* ws, int64_t N, const Geom& g) {
-  return (float*)ws + (size_t)plan_partial(N).grid * slab_floats(g);
+  return (float*)ws + (size_t)plan_partial(N).grid * slab_stride(g);
 }
 
 }  // namespace
@@ -932,9 +915,8 @@ int drsa_amd_polar(const float* V, int d, float* U_out, int* iters_out, void* st
     DRSA_LAUNCH_CHECK();
     return DRSA_OK;
   };
-  const int DP = pow2ceil(d < 16 ? 16 : d);
+  const int DP = pow2ceil(d < 32 ? 32 : d);
   switch (DP) {
-    case 16: return go(std::integral_constant<int, 16>{});
     case 32: return go(std::integral_constant<int, 32>{});
     case 64: return go(std::integral_constant<int, 64>{});
     default: return go(std::integral_constant<int, 128>{});

@@ -1,0 +1,209 @@
+// Polar factor by Newton-Schulz in one workgroup (shared by drsa_step.hip and scripts/probe_ns.hip).
+//   X0 = a V (a from the first Gram matrix: sqrt(DP / tr) unless that overshoots the inf-norm);
+//   P = X^T X (upper 32x32 block triangle, mirrored), T = 1.5 I - 0.5 P, X <- X T until max|P - I| < tol
+//   or until the next update provably lands there / rounding has become the floor.
+// fp32 MFMA 32x32x2 (exact f32 fma chains): per MFMA 2 LDS operand reads for 2048 MACs, and its
+// dependent-accumulator latency equals its issue time, so one wave per SIMD keeps the pipe busy.
+#pragma once
+#include "common.h"
+
+#ifndef DRSA_NS_STAMP
+#define DRSA_NS_STAMP(slot)
+#endif
+
+namespace {
+
+template <int DP>
+constexpr int fin_threads() { return DP >= 64 ? 1024 : 256; }
+// row stride == 2 (mod 64): the row-direction operand reads (X in X T) hit 64 distinct banks, the
+// column-direction ones 2-way at worst
+template <int DP>
+constexpr int ns_ld() { return DP + 2; }
+
+// single-barrier block max: red must be a slot nobody reads or writes between two calls that are
+// separated by at least one other __syncthreads (the per-iteration error uses alternating slots)
+template <int NT>
+__device__ float block_max1(float v, float* red) {
+  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, shfl_xor(v, m));
+  if (lane_id() == 0) red[wave_id()] = v;
+  __syncthreads();
+  float r = red[0];
+#pragma unroll
+  for (int i = 1; i < NT / 64; ++i) r = fmaxf(r, red[i]);
+  return r;
+}
+
+template <int NT>
+__device__ float block_max(float v, float* red) {
+  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, shfl_xor(v, m));
+  __syncthreads();
+  if (lane_id() == 0) red[wave_id()] = v;
+  __syncthreads();
+  float r = red[0];
+#pragma unroll
+  for (int i = 1; i < NT / 64; ++i) r = fmaxf(r, red[i]);
+  return r;
+}
+
+// 32x32x2 f32 MFMA tile accumulate: C/D lane l, reg r -> row (r&3) + 8(r>>2) + 4(l>>5), col l&31
+__device__ __forceinline__ int t32_row(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
+
+// k-split of the 32x32 tiles: below DP = 128 there are too few tiles to keep 16 waves busy, so each
+// tile's k range is split over KS waves and the partial tiles are summed in a fixed order (kq
+// ascending) through LDS scratch.
+template <int DP>
+constexpr int ns_ks() { return DP >= 128 ? 1 : 4; }
+template <int DP>
+constexpr size_t ns_scratch_floats() {
+  return ns_ks<DP>() == 1 ? 0 : (size_t)(DP / 32) * (DP / 32) * ns_ks<DP>() * 1024;
+}
+
+template <int DP>
+__device__ int polar_ns(float* X, float* T, float* red, float* scr, float tol, int max_iter) {
+  constexpr int NT = fin_threads<DP>(), LD = ns_ld<DP>(), NB = DP / 32, NWV = NT / 64, KS = ns_ks<DP>();
+  constexpr int NSYM = NB * (NB + 1) / 2, NFULL = NB * NB;
+  constexpr int KR = DP / KS;                       // k range per task
+  constexpr int TPR = NT / DP;   // threads per row in the inf-norm pass (8 or 16)
+  static_assert(DP >= 32, "polar_ns: DP >= 32 (callers embed smaller problems)");
+  static_assert(KS == 1 || (NSYM * KS <= NWV && NFULL * KS <= NWV), "one k-split task per wave");
+  constexpr int NTW = (NFULL * KS + NWV - 1) / NWV;
+  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int lo = lane & 31, hi = lane >> 5;
+  auto sym_tile = [](int t, int& ib, int& jb) {
+    ib = 0;
+    int rem = t;
+    while (rem >= NB - ib) { rem -= NB - ib; ++ib; }
+    jb = ib + rem;
+  };
+  // P element epilogue: raw (it == 0, scaling follows) or T = 1.5 I - 0.5 P with the error
+  auto put_p = [&](int it, int row, int col, float v, float& err) {
+    if (it > 0) {
+      const bool dg = row == col;
+      err = fmaxf(err, fabsf(v - (dg ? 1.f : 0.f)));
+      v = (dg ? 1.5f : 0.f) - 0.5f * v;
+    }
+    T[row * LD + col] = v;
+    if (row / 32 != col / 32) T[col * LD + row] = v;   // X^T X is exactly symmetric (products commute)
+  };
+  int it = 0;
+  float err_prev = 1.f;
+  for (;; ++it) {
+    __syncthreads();   // X complete
+    DRSA_NS_STAMP(4 * it + 0);
+    // ---- P = X^T X on the upper block triangle ----
+    float err = 0.f;
+    for (int t = w; t < NSYM * KS; t += NWV) {
+      int ib, jb;
+      sym_tile(t / KS, ib, jb);
+      const int kq = t % KS;
+      f32x16 acc = {};
+#pragma unroll 8
+      for (int k0 = kq * KR; k0 < (kq + 1) * KR; k0 += 2) {
+        const int kk = k0 + hi;
+        acc = mfma32(X[kk * LD + 32 * ib + lo], X[kk * LD + 32 * jb + lo], acc);
+      }
+      if constexpr (KS == 1) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) put_p(it, 32 * ib + t32_row(r, hi), 32 * jb + lo, acc[r], err);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) scr[(size_t)t * 1024 + r * 64 + lane] = acc[r];
+      }
+    }
+    if constexpr (KS > 1) {
+      __syncthreads();
+      for (int e = tid; e < NSYM * 1024; e += NT) {
+        const int tt = e / 1024, r = (e / 64) % 16, ln = e % 64;
+        int ib, jb;
+        sym_tile(tt, ib, jb);
+        float v = 0.f;
+#pragma unroll
+        for (int kq = 0; kq < KS; ++kq) v += scr[(size_t)(tt * KS + kq) * 1024 + r * 64 + ln];
+        put_p(it, 32 * ib + t32_row(r, ln >> 5), 32 * jb + (ln & 31), v, err);
+      }
+    }
+    if (it == 0) {
+      __syncthreads();
+      DRSA_NS_STAMP(4 * it + 1);
+      // scaling a^2 = DP / tr(P) if a^2 ||P||_inf < 2.9 else 1 / ||P||_inf (fixed-order sums)
+      float tr = 0.f;
+      for (int i = lane; i < DP; i += 64) tr += T[i * LD + i];
+      for (int m = 32; m >= 1; m >>= 1) tr += shfl_xor(tr, m);   // every wave gets the same value
+      const int row = tid / TPR, part = tid % TPR;
+      float rs = 0.f;
+      for (int c = part; c < DP; c += TPR) rs += fabsf(T[row * LD + c]);
+      for (int m = 1; m < TPR; m <<= 1) rs += shfl_xor(rs, m);
+      const float rowmax = block_max<NT>(rs, red);
+      float a2 = (float)DP / tr;
+      if (a2 * rowmax >= 2.9f) a2 = 1.f / rowmax;
+      const float a = sqrtf(a2);
+      for (int e = tid; e < DP * DP; e += NT) {
+        const int r = e / DP, c = e % DP;
+        X[r * LD + c] *= a;
+        const float pv = T[r * LD + c] * a2;
+        err = fmaxf(err, fabsf(pv - (r == c ? 1.f : 0.f)));
+        T[r * LD + c] = (r == c ? 1.5f : 0.f) - 0.5f * pv;
+      }
+    }
+    err = block_max1<NT>(err, red + 32 + 16 * (it & 1));
+    DRSA_NS_STAMP(4 * it + 2);
+    if (err < tol || it >= max_iter) break;
+    // Stop after this update when it provably lands below tol, or when fp32 rounding has become
+    // the floor: from a spectral error e = |1 - sigma^2| one iteration leaves 0.75 e^2 (1 + e/3),
+    // and e <= DP * err (entrywise max of the symmetric P - I); a quadratic step from err_prev <
+    // 1e-4 would be far below err_prev / 4, so a smaller drop is rounding noise, not convergence.
+    const bool last = (float)DP * err < 1e-4f || (it > 0 && err_prev < 1e-4f && err > 0.25f * err_prev);
+    err_prev = err;
+    // ---- X <- X T (all reads before any write) ----
+    f32x16 acc[NTW];
+#pragma unroll
+    for (int q = 0; q < NTW; ++q) acc[q] = f32x16{};
+#pragma unroll 4
+    for (int kr = 0; kr < KR; kr += 2) {
+#pragma unroll
+      for (int q = 0; q < NTW; ++q) {
+        const int t = w + NWV * q;
+        if (t < NFULL * KS) {
+          const int tile = t / KS, kq = t % KS, ib = tile / NB, jb = tile % NB;
+          const int kk = kq * KR + kr + hi;
+          acc[q] = mfma32(X[(32 * ib + lo) * LD + kk], T[kk * LD + 32 * jb + lo], acc[q]);
+        }
+      }
+    }
+    if constexpr (KS > 1) {
+#pragma unroll
+      for (int q = 0; q < NTW; ++q) {
+        const int t = w + NWV * q;
+        if (t < NFULL * KS)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) scr[(size_t)t * 1024 + r * 64 + lane] = acc[q][r];
+      }
+    }
+    __syncthreads();
+    DRSA_NS_STAMP(4 * it + 3);
+    if constexpr (KS == 1) {
+#pragma unroll
+      for (int q = 0; q < NTW; ++q) {
+        const int t = w + NWV * q;
+        if (t < NFULL) {
+          const int ib = t / NB, jb = t % NB;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) X[(32 * ib + t32_row(r, hi)) * LD + 32 * jb + lo] = acc[q][r];
+        }
+      }
+    } else {
+      for (int e = tid; e < NFULL * 1024; e += NT) {
+        const int tt = e / 1024, r = (e / 64) % 16, ln = e % 64, ib = tt / NB, jb = tt % NB;
+        float v = 0.f;
+#pragma unroll
+        for (int kq = 0; kq < KS; ++kq) v += scr[(size_t)(tt * KS + kq) * 1024 + r * 64 + ln];
+        X[(32 * ib + t32_row(r, ln >> 5)) * LD + 32 * jb + (ln & 31)] = v;
+      }
+    }
+    if (last) { ++it; break; }
+  }
+  __syncthreads();
+  return it;
+}
+
+}  // namespace

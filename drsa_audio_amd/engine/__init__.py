@@ -1,25 +1,75 @@
-"""HIP LRP engine: plan compilation + execution (see ``plan.py``)."""
+"""HIP LRP engine: plan compilation + execution (see ``plan.py``).
+
+``get_engine`` caches compiled plans per (model, composite) while the model's parameters are
+unchanged.  The cache holds the model and the composite only through weak references (the
+engine itself keeps no strong reference to either), drops an entry as soon as its model or
+composite is garbage-collected, and keeps at most ``DRSA_AMD_ENGINE_CACHE`` (default 8) entries
+in LRU order; an evicted engine releases its device buffers.  So a workflow that builds a new
+``HeatmapGenerator`` per pass (the reference does, cxai/xai/pixelflipping/cpf.py:161) keeps a
+bounded device footprint.
+"""
 from __future__ import annotations
+
+import os
+import weakref
+from collections import OrderedDict
 
 from .plan import EngineError, LRPEngine
 
-_CACHE = {}
+_MAX = max(1, int(os.environ.get("DRSA_AMD_ENGINE_CACHE", "8")))
+_CACHE: "OrderedDict[tuple, _Entry]" = OrderedDict()
+
+
+class _Entry:
+    __slots__ = ("model_ref", "comp_ref", "fp", "eng")
+
+    def __init__(self, model_ref, comp_ref, fp, eng):
+        self.model_ref, self.comp_ref, self.fp, self.eng = model_ref, comp_ref, fp, eng
 
 
 def _fingerprint(model):
     return tuple((p.data_ptr(), p._version) for p in model.parameters())
 
 
+def _ref(obj):
+    if obj is None:
+        return lambda: None
+    return weakref.ref(obj)
+
+
+def _evict(key) -> None:
+    e = _CACHE.pop(key, None)
+    if e is not None:
+        e.eng.release()
+
+
 def get_engine(model, composite) -> LRPEngine:
     """Compiled plan for (model, composite), cached while the model's parameters are unchanged."""
     key = (id(model), id(composite))
     fp = _fingerprint(model)
-    hit = _CACHE.get(key)
-    if hit is not None and hit[0] == fp and hit[1].model is model and hit[1].composite is composite:
-        return hit[1]
+    e = _CACHE.get(key)
+    if e is not None:
+        if e.model_ref() is model and e.comp_ref() is composite and e.fp == fp:
+            _CACHE.move_to_end(key)
+            return e.eng
+        _evict(key)          # stale: ids reused by new objects, or the weights changed
     eng = LRPEngine(model, composite)
-    _CACHE[key] = (fp, eng)
+    _CACHE[key] = _Entry(_ref(model), _ref(composite), fp, eng)
+    weakref.finalize(model, _evict, key)
+    if composite is not None:
+        weakref.finalize(composite, _evict, key)
+    while len(_CACHE) > _MAX:
+        _evict(next(iter(_CACHE)))
     return eng
 
 
-__all__ = ["LRPEngine", "EngineError", "get_engine"]
+def cache_size() -> int:
+    return len(_CACHE)
+
+
+def clear_cache() -> None:
+    for key in list(_CACHE):
+        _evict(key)
+
+
+__all__ = ["LRPEngine", "EngineError", "get_engine", "cache_size", "clear_cache"]

@@ -24,6 +24,7 @@ batch size.
 from __future__ import annotations
 
 import os
+import weakref
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -107,8 +108,10 @@ class EngineError(NotImplementedError):
 class LRPEngine:
     def __init__(self, model: nn.Module, composite, device: Optional[torch.device] = None):
         _capi.load()
-        self.model = model
-        self.composite = composite
+        # no strong references to the model / composite: the plan owns prepared copies of what it
+        # needs, and get_engine's cache is keyed by weak references (engine/__init__.py)
+        self._model_ref = weakref.ref(model)
+        self._composite_ref = (lambda: None) if composite is None else weakref.ref(composite)
         p0 = next(model.parameters())
         self.device = device or p0.device
         if self.device.type != "cuda":
@@ -124,6 +127,22 @@ class LRPEngine:
         self._buffers: Dict[tuple, dict] = {}
         self.last: Optional[dict] = None
         self.trace: Optional[list] = None      # set to [] to record (tag, start_event, end_event)
+
+    @property
+    def model(self):
+        return self._model_ref()
+
+    @property
+    def composite(self):
+        return self._composite_ref()
+
+    def release(self) -> None:
+        """Free the cached activation/relevance buffers and prepared per-shape state."""
+        self._buffers.clear()
+        self._cur_bufs = {}
+        for st in self.stages:
+            st.den_maps.clear()
+        self.last = None
 
     def _call(self, tag: str, name: str, *args) -> None:
         if self.trace is None:

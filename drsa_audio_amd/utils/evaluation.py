@@ -10,18 +10,20 @@
 These read and write the caller's own files (the formats ``drsa.main`` / ``SubspaceOptimizer``
 write here and in the reference).  Checkpoints are loaded with ``weights_only=True``; the
 reference's RNG-state entries are admitted through an explicit allowlist of numpy types.
-``projection_matrix.pkl`` is a pickle: only load files you produced.
+``projection_matrix.pkl`` is read with a restricted unpickler that admits only arrays
+(``utils/safe_pickle.py``).
 """
 from __future__ import annotations
 
 import os
-import pickle
 import random
 from typing import List, Tuple
 
 import numpy as np
 import pandas as pd
 import torch
+
+from . import safe_pickle
 
 
 def get_run_stats(path: str) -> Tuple[float, List[float], List[float]]:
@@ -47,7 +49,7 @@ def get_best_run(path: str):
 def load_projection_matrix(genre: str, layer_idx: int, path: str, device=torch.device("cpu")) -> torch.Tensor:
     _, _, _, best, _ = get_best_run(os.path.join(path, f"{genre}/layer{layer_idx}"))
     with open(os.path.join(best, "projection_matrix.pkl"), "rb") as fh:
-        U = pickle.load(fh)
+        U = safe_pickle.load(fh)
     return torch.tensor(U, device=device)
 
 

@@ -6,8 +6,8 @@
                                  ``normalize_vectors`` on A and C separately (HIP kernel)
 
 These read and write the caller's own dataset files (the reference's format, so datasets made
-by either side load in the other).  Loading a pickle executes code from the file: only load
-files you produced.
+by either side load in the other).  ``load_and_normalize_data`` reads the file with a restricted
+unpickler that admits only numpy arrays / torch tensors (``utils/safe_pickle.py``).
 """
 from __future__ import annotations
 
@@ -17,6 +17,7 @@ import pickle
 import numpy as np
 import torch
 
+from ....utils import safe_pickle
 from ..preprocessing import normalize_vectors
 
 
@@ -37,8 +38,10 @@ def save_data(activation_vectors, context_vectors, layer=None, sample_class=None
 
 def load_and_normalize_data(filepath, device):
     with open(filepath, "rb") as fh:
-        dataset = pickle.load(fh)
+        dataset = safe_pickle.load(fh)
     a, c = zip(*dataset)
-    a = torch.tensor(np.array(a), device=device, dtype=torch.float32).contiguous()
-    c = torch.tensor(np.array(c), device=device, dtype=torch.float32).contiguous()
+    a = torch.tensor(np.array([np.asarray(v.cpu() if torch.is_tensor(v) else v) for v in a]), device=device,
+                     dtype=torch.float32).contiguous()
+    c = torch.tensor(np.array([np.asarray(v.cpu() if torch.is_tensor(v) else v) for v in c]), device=device,
+                     dtype=torch.float32).contiguous()
     return normalize_vectors(a), normalize_vectors(c)

@@ -71,6 +71,11 @@ class AlphaBeta(BasicHook):
     kind = "alphabeta"
 
     def __init__(self, alpha=2.0, beta=1.0, stabilizer=1e-6, zero_params=None):
+        # zennit 0.5.1 refuses these configurations (conservation needs alpha - beta = 1)
+        if alpha < 0 or beta < 0:
+            raise ValueError("Both alpha and beta parameters must be non-negative!")
+        if (alpha - beta) != 1.0:
+            raise ValueError("The difference of parameters alpha - beta must equal 1!")
         super().__init__(zero_params)
         self.alpha, self.beta = float(alpha), float(beta)
         self.stabilizer = Stabilizer.ensure(stabilizer).epsilon

@@ -97,3 +97,12 @@ def test_c_abi_argument_validation_without_gpu():
     assert lib.drsa_amd_drsa_slab_floats(100, 4) == 128 * 128 + 4
     assert lib.drsa_amd_drsa_slab_floats(64, 4) == 64 * 64 + 4
     assert lib.drsa_amd_drsa_workspace_bytes(100, 128, 3) == 0
+
+
+def test_alphabeta_parameter_checks_like_zennit():
+    from drsa_audio_amd.zennit.rules import AlphaBeta
+    AlphaBeta(2.0, 1.0)
+    AlphaBeta(1.0, 0.0)
+    for a, b in ((-1.0, -2.0), (1.0, -0.0 - 1.0), (2.0, 0.5), (0.5, 0.0)):
+        with pytest.raises(ValueError):
+            AlphaBeta(a, b)
