@@ -83,46 +83,77 @@ def kernel_macs(eng, B, K):
 
 
 # --------------------------------------------------------------------------- CPU baseline
-def cpu_baseline(budget_s=15.0):
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import lrp_ref
-    from drsa_audio_amd.model.modify_model import ProjectionModel
-    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "64")), 16)
-    torch.set_num_threads(threads)
-    nm = {"features.0": ("wsquare", 1e-7), "features.3": ("gamma", 0.4, 1e-7), "features.6": ("gamma", 0.4, 1e-7),
-          "features.9": ("gamma", 0.2, 1e-7), "features.12": ("gamma", 0.1, 1e-7),
-          "classifier.0": ("epsilon", 1e-7), "classifier.3": ("epsilon", 1e-7), "classifier.6": ("epsilon", 1e-7)}
-    pm = ProjectionModel(gtzan128(), 7, load_u(), 4).eval()
-    chunk = 16
-    lrp_ref.subspace_heatmaps(pm, nm, 4, synthetic_logmel(1, seed=98), class_idx=3, mode="zennit")  # warm-up
-    n, dt, i = 0, 0.0, 0
-    while dt < budget_s and n < 1024:
-        x = synthetic_logmel(chunk, seed=100 + i)
-        t0 = time.perf_counter()
-        lrp_ref.subspace_heatmaps(pm, nm, 4, x, class_idx=3, mode="zennit")
-        dt += time.perf_counter() - t0
-        n += chunk
-        i += 1
+def _cpu_model_name():
     cpu = platform.processor() or platform.machine()
     try:
         with open("/proc/cpuinfo") as fh:
             for line in fh:
                 if line.startswith("model name"):
-                    cpu = line.split(":", 1)[1].strip()
-                    break
+                    return line.split(":", 1)[1].strip()
     except OSError:
         pass
-    return {"value": n / dt, "unit": "explained samples/s", "cores": threads, "kind": "port",
-            "sample": f"{n} samples x (K+1=5 replicated rows), GTZAN-128 j=7 K=4, oracle zennit-structured "
-                      f"mode (5-pass Gamma + autograd like zennit.BasicHook), torch {torch.__version__} CPU, "
-                      f"{threads} threads, {cpu}, {dt:.1f} s"}
+    return cpu
+
+
+def _cpu_threads():
+    """torch.set_num_threads(len(os.sched_getaffinity(0))), reported with the count."""
+    n = len(os.sched_getaffinity(0))
+    torch.set_num_threads(n)
+    return n
+
+
+def _median_timed(fn, warmup=2, reps=5):
+    for _ in range(warmup):
+        fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), ts
+
+
+def cpu_baseline(chunk=8, reps=5):
+    """The reference's CPU path, restated op for op (oracle zennit-structured mode: 5-pass Gamma +
+    autograd like zennit.BasicHook, K+1 batch replication like explainer.py:92), timed per SURVEY
+    8(d): all affinity cores, 2 warm-ups, median of >= 5 timed chunks of `chunk` samples."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import lrp_ref
+    from drsa_audio_amd.model.modify_model import ProjectionModel
+    threads = _cpu_threads()
+    nm = {"features.0": ("wsquare", 1e-7), "features.3": ("gamma", 0.4, 1e-7), "features.6": ("gamma", 0.4, 1e-7),
+          "features.9": ("gamma", 0.2, 1e-7), "features.12": ("gamma", 0.1, 1e-7),
+          "classifier.0": ("epsilon", 1e-7), "classifier.3": ("epsilon", 1e-7), "classifier.6": ("epsilon", 1e-7)}
+    pm = ProjectionModel(gtzan128(), 7, load_u(), 4).eval()
+    x = synthetic_logmel(chunk, seed=100)
+    med, ts = _median_timed(lambda: lrp_ref.subspace_heatmaps(pm, nm, 4, x, class_idx=3, mode="zennit"), 2, reps)
+    return {"value": chunk / med, "unit": "explained samples/s", "cores": threads, "kind": "port",
+            "sample": f"median of {reps} timed chunks ({', '.join(f'{t:.2f}' for t in ts)} s) after 2 warm-ups; "
+                      f"chunk = {chunk} samples x (K+1=5 replicated rows), GTZAN-128 j=7 K=4, oracle "
+                      f"zennit-structured mode, torch {torch.__version__} CPU, {threads} threads "
+                      f"(len(sched_getaffinity); OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')}), "
+                      f"{_cpu_model_name()}"}
+
+
+def cpu_drsa_baseline(reps=7):
+    """DRSA CPU leg at C3: oracle/drsa_ref.step (op for op drsa.py:84-106: fp32 obj + autograd, fp64
+    eigh orthogonalize; pinned bit-exact to the reference's own fixtures), median of `reps` steps."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import drsa_ref
+    from gen_fixtures import drsa_inputs
+    threads = _cpu_threads()
+    A, C = (torch.from_numpy(v) for v in drsa_inputs(20000, 64, 3))
+    U = torch.from_numpy(np.load(os.path.join(ROOT, "tests", "golden", "u64_seed42.npy")))
+    med, _ = _median_timed(lambda: drsa_ref.step(A, C, U, 4), 2, reps)
+    return {"config": "C3: N=20000, d=64, K=4", "ms_per_step": med * 1e3, "vector_steps_per_s": 20000 / med,
+            "cores": threads, "kind": "port", "sample": f"median of {reps} steps after 2 warm-ups"}
 
 
 # --------------------------------------------------------------------------- DRSA
 def drsa_bench(device, steps=200):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import drsa_ref
     from gen_fixtures import drsa_inputs
+    from drsa_audio_amd import _capi
     from drsa_audio_amd.xai.drsa.drsa import DrsaWorkspace, drsa_run
     N, d, K = 20000, 64, 4
     A, C = drsa_inputs(N, d, 3)
@@ -137,19 +168,43 @@ def drsa_bench(device, steps=200):
         U, traj = drsa_run(Ag, Cg, Ug, K, steps, ws)
         torch.cuda.synchronize(device)
         dt = time.perf_counter() - t0
+        # the reference's 2000-step C3 run (tests/golden/drsa_long_fixture.npz): max deviation
+        fx = np.load(os.path.join(ROOT, "tests", "golden", "drsa_long_fixture.npz"))
+        _, t2000 = drsa_run(Ag, Cg, Ug, K, 2000, ws)
+        torch.cuda.synchronize(device)
+        ref = fx["c3_traj"]
+        dev2000 = float(np.max(np.abs(t2000.cpu().numpy().astype(np.float64) - ref) / np.abs(ref)))
+        # per-kernel HIP-event timings on this stream: partial (+ slab reduce) and finish (polar)
+        st = s.cuda_stream
+        Un = torch.empty_like(Ug)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        tp, tf = [], []
+        for _ in range(50):
+            ev[0].record(s)
+            _capi.call("drsa_amd_drsa_partial", Ag.data_ptr(), Cg.data_ptr(), N, d, K, Ug.data_ptr(), ws.gs.data_ptr(),
+                       ws.ptr, ws.nbytes, st)
+            ev[1].record(s)
+            _capi.call("drsa_amd_drsa_finish", ws.gs.data_ptr(), N, d, K, Ug.data_ptr(), Un.data_ptr(),
+                       ws.f.data_ptr(), 0, None, st)
+            ev[2].record(s)
+            torch.cuda.synchronize(device)
+            tp.append(ev[0].elapsed_time(ev[1]))
+            tf.append(ev[1].elapsed_time(ev[2]))
     traj = traj.cpu().numpy()
-    # objective vs the CPU restatement of drsa.py for the first 10 steps
-    Ur, ref = torch.from_numpy(U0), []
-    At, Ct = torch.from_numpy(A), torch.from_numpy(C)
-    for _ in range(10):
-        Ur, f, _ = drsa_ref.step(At, Ct, Ur, K)
-        ref.append(f)
-    rel = float(np.max(np.abs(traj[:10] - np.array(ref)) / np.abs(np.array(ref))))
     flop = 8.0 * N * d * d
-    return {"config": "C3: N=20000, d=64, K=4 (synthetic normalised A=|N(0,1)|, C~N(0,1))",
-            "ms_per_step": dt / steps * 1e3, "vector_steps_per_s": N * steps / dt,
-            "tflops_algorithmic": flop * steps / dt / 1e12, "steps": steps,
-            "objective_max_rel_err_vs_oracle_10_steps": rel, "objective_final": float(traj[-1])}
+    ms = dt / steps * 1e3
+    tflops = flop / (ms * 1e-3) / 1e12
+    tp_ms = float(np.median(tp))
+    return {"config": "C3: N=20000, d=64, K=4 (synthetic normalised A=|N(0,1)|, C~N(0,1)), whole S-step loop "
+                      "as one replayed hipGraph", "ms_per_step": ms, "vector_steps_per_s": N * steps / dt,
+            "steps": steps, "objective_final": float(traj[-1]),
+            "traj_dev_2000_vs_reference": dev2000,
+            "roofline": {"bound": "mfma", "kernel": "drsa_partial (+ slab reduce)",
+                         "achieved": flop / (tp_ms * 1e-3) / 1e12, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": flop / (tp_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS,
+                         "whole_step_tflops": tflops, "whole_step_frac": tflops / FP32_MFMA_PEAK_TFLOPS,
+                         "algorithmic_flop_per_step": flop},
+            "event_ms": {"partial_plus_reduce": tp_ms, "finish_polar": float(np.median(tf))}}
 
 
 def frontend_bench(device, n_songs=64, iters=20):
@@ -398,9 +453,25 @@ def main():
     drsa_sharded = None
     if not args.no_drsa and world > 1:
         drsa_sharded = drsa_sharded_bench(device, world, rank)
-    cpu = None
+    # the reference API returns numpy (explainer.py:111): the same steps with the D2H copy of info
+    to_host = None
+    if rank == 0:
+        for _ in range(2):
+            hg.generate_subspace_heatmaps(x, to_host=True)
+        torch.cuda.synchronize(device)
+        t1 = time.perf_counter()
+        nh = 5
+        for _ in range(nh):
+            hg.generate_subspace_heatmaps(x, to_host=True)
+        torch.cuda.synchronize(device)
+        th = (time.perf_counter() - t1) / nh
+        to_host = {"explained_samples_per_s": B / th, "ms_per_step": th * 1e3,
+                   "note": "generate_subspace_heatmaps(to_host=True): info dict as numpy (input + heatmaps + "
+                           "relevances + mask copied D2H each step, PCIe-inclusive)"}
+    cpu = cpu_drsa = None
     if not args.no_cpu_baseline and rank == 0 and world == 1:
         cpu = cpu_baseline()
+        cpu_drsa = cpu_drsa_baseline()
 
     if rank == 0:
         out = {
@@ -429,7 +500,7 @@ def main():
             "secondary": {"standard_lrp_c2_bs64_samples_per_s": c2 * world,
                           "explained_samples_per_s_bs64": bs64 * world, "drsa": drsa,
                           "drsa_sharded": drsa_sharded, "drsa_joint_c5": joint, "vggish_lrp": vgg,
-                          "logmel_frontend": frontend},
+                          "logmel_frontend": frontend, "to_host": to_host, "cpu_baseline_drsa_c3": cpu_drsa},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

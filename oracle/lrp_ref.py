@@ -29,7 +29,7 @@ Rule arithmetic (z = f(x; W, b), Jᵀ_W g = input-gradient of f with weights W):
 Layers without a rule use their plain gradient (ReLU, MaxPool [first max], Dropout
 (eval), BatchNorm (eval), flatten), exactly like zennit's Gradient attributor.
 
-Three execution modes share that arithmetic:
+Four execution modes share that arithmetic:
 * ``mode="analytic"`` — each rule evaluated with explicit conv/conv-transpose calls.
 * ``mode="zennit"``   — each rule evaluated the way zennit's BasicHook does it
   (modified forwards + ``torch.autograd.grad``), and the heatmap generator replicates
@@ -39,7 +39,9 @@ Three execution modes share that arithmetic:
   sequential fp32 fma chain in a pinned order (``oracle/lrp_exact.c``): channel-major /
   tap-minor for convolutions, bias added last.  This is the order the HIP kernels
   accumulate in (f32 MFMA is an exact k-ordered fma chain), so this mode is the
-  bit-exact parity oracle.  The reference path is ill-conditioned with respect to
+  bit-exact parity oracle.
+* ``mode="f64"``      — the analytic structure in float64: the accuracy anchor.  The parity
+  tests bound every fp32 path's distance to it (tests/test_lrp_gpu.py, test_oracle_lrp.py).  The reference path is ill-conditioned with respect to
   rounding (the ProjectionModel's a' = (aU)Uᵀ differs from a at rounding level and the
   ε = 1e-6 stabilisers amplify that at dead ReLU channels: correctly rounded projections
   move subspace relevances by up to ~6 %), so only a pinned order can pin it.
@@ -270,7 +272,9 @@ class ExactOps:
         return out.reshape(lead)
 
 
-OPS = {"analytic": TorchOps, "zennit": TorchOps, "exact": ExactOps}
+# "f64": the analytic structure evaluated in float64 (model and input promoted): the accuracy
+# anchor that fp32 implementations (the reference's own path, the HIP kernels) are measured against
+OPS = {"analytic": TorchOps, "zennit": TorchOps, "exact": ExactOps, "f64": TorchOps}
 
 
 def _aff(L: Layer, x, w, b, ops=TorchOps):
@@ -299,11 +303,11 @@ def _proj_fwd(L: Layer, x, ops):
     if L.kind == "proj":
         b, d = x.size(0), x.size(1)
         vecs = x.reshape(b, d, -1).transpose(1, 2)
-        h = ops.matmul(vecs, m.U.to(torch.float32))
+        h = ops.matmul(vecs, m.U.to(x.dtype))
         return h.reshape(b, vecs.size(1), m.num_concepts, m.d_k)
     b, n = x.size(0), x.size(1)
     side = int(round(n ** 0.5))
-    a = ops.matmul(x.reshape(b, n, m.d), m.U_inv.to(torch.float32).contiguous())
+    a = ops.matmul(x.reshape(b, n, m.d), m.U_inv.to(x.dtype).contiguous())
     return a.transpose(1, 2).reshape(b, m.d, side, side).contiguous()
 
 
@@ -312,11 +316,11 @@ def _proj_jt(L: Layer, x, g, ops):
     m = L.module
     if L.kind == "proj":        # h = a_vec U  ->  J^T g = g_vec U^T (back to [b, d, H, W])
         b, n = g.size(0), g.size(1)
-        t = ops.matmul(g.reshape(b, n, -1), m.U.to(torch.float32).t().contiguous())
+        t = ops.matmul(g.reshape(b, n, -1), m.U.to(g.dtype).t().contiguous())
         return t.transpose(1, 2).reshape(x.shape)
     b, d = g.size(0), g.size(1)     # a' = h U^T  ->  J^T g = g_vec U
     gv = g.reshape(b, d, -1).transpose(1, 2)
-    return ops.matmul(gv, m.U_inv.to(torch.float32).t().contiguous()).reshape(x.shape)
+    return ops.matmul(gv, m.U_inv.to(g.dtype).t().contiguous()).reshape(x.shape)
 
 
 # ----------------------------------------------------------------------------
@@ -510,10 +514,13 @@ def lrp(model: nn.Module, rules: Dict[str, RuleSpec], x: torch.Tensor, class_idx
         num_classes=None, one_hot_encoded=False, mode: str = "analytic",
         capture: Optional[str] = None):
     """Returns (logits, R_input[, (act, rel) at layer ``capture``])."""
+    if mode == "f64":
+        import copy
+        model = copy.deepcopy(model).double()
     layers = sequential_layers(model)
     ops = OPS[mode]
     acts: List[Tuple[torch.Tensor, torch.Tensor, object]] = []
-    h = x.detach().to(torch.float32)
+    h = x.detach().to(torch.float64 if mode == "f64" else torch.float32)
     for L in layers:
         aux = None
         if L.kind == "maxpool":
