@@ -95,11 +95,35 @@ def _cpu_model_name():
     return cpu
 
 
+def _cgroup_cpus():
+    """CPUs this process may actually use under a cgroup v2/v1 quota (None: no quota)."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+            if q != "max":
+                return max(1, int(-(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as fq, open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fp:
+            q, per = int(fq.read()), int(fp.read())
+            if q > 0:
+                return max(1, -(-q // per))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def _cpu_threads():
-    """torch.set_num_threads(len(os.sched_getaffinity(0))), reported with the count."""
-    n = len(os.sched_getaffinity(0))
+    """torch.set_num_threads(len(os.sched_getaffinity(0))) -- capped at the cgroup CPU
+    quota when one is set (the affinity mask can list the whole machine while the process is
+    granted a share of it; threads beyond the share only contend).  Returns (threads, affinity,
+    quota)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = _cgroup_cpus()
+    n = min(aff, quota) if quota else aff
     torch.set_num_threads(n)
-    return n
+    return n, aff, quota
 
 
 def _median_timed(fn, warmup=2, reps=5):
@@ -120,7 +144,8 @@ def cpu_baseline(chunk=8, reps=5):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import lrp_ref
     from drsa_audio_amd.model.modify_model import ProjectionModel
-    threads = _cpu_threads()
+    threads, aff, quota = _cpu_threads()
+    log(f"[bench] CPU baseline (LRP+DRSA explained samples): {threads} threads (affinity {aff}, cgroup quota {quota})")
     nm = {"features.0": ("wsquare", 1e-7), "features.3": ("gamma", 0.4, 1e-7), "features.6": ("gamma", 0.4, 1e-7),
           "features.9": ("gamma", 0.2, 1e-7), "features.12": ("gamma", 0.1, 1e-7),
           "classifier.0": ("epsilon", 1e-7), "classifier.3": ("epsilon", 1e-7), "classifier.6": ("epsilon", 1e-7)}
@@ -131,8 +156,7 @@ def cpu_baseline(chunk=8, reps=5):
             "sample": f"median of {reps} timed chunks ({', '.join(f'{t:.2f}' for t in ts)} s) after 2 warm-ups; "
                       f"chunk = {chunk} samples x (K+1=5 replicated rows), GTZAN-128 j=7 K=4, oracle "
                       f"zennit-structured mode, torch {torch.__version__} CPU, {threads} threads "
-                      f"(len(sched_getaffinity); OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')}), "
-                      f"{_cpu_model_name()}"}
+                      f"(len(sched_getaffinity) = {aff}, cgroup CPU quota = {quota}), {_cpu_model_name()}"}
 
 
 def cpu_drsa_baseline(reps=7):
@@ -141,7 +165,8 @@ def cpu_drsa_baseline(reps=7):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import drsa_ref
     from gen_fixtures import drsa_inputs
-    threads = _cpu_threads()
+    threads, aff, quota = _cpu_threads()
+    log(f"[bench] CPU baseline (DRSA C3 step): {threads} threads")
     A, C = (torch.from_numpy(v) for v in drsa_inputs(20000, 64, 3))
     U = torch.from_numpy(np.load(os.path.join(ROOT, "tests", "golden", "u64_seed42.npy")))
     med, _ = _median_timed(lambda: drsa_ref.step(A, C, U, 4), 2, reps)
@@ -363,6 +388,7 @@ def main():
     hg = HeatmapGenerator(model, load_u(), LRP_NAME_MAP_GTZAN, "blues", num_concepts=K, layer_idx=7, device=device)
     x = synthetic_logmel(B, seed=1 + rank, device=device)
 
+    log(f"[bench] rank {rank}/{world}: headline B={B}, {args.warmup} warm-up + {args.steps} timed steps")
     for _ in range(args.warmup):
         hg.generate_subspace_heatmaps(x, to_host=False)
     torch.cuda.synchronize(device)
@@ -420,6 +446,7 @@ def main():
             traffic = None
     total_macs = sum(macs.values())
 
+    log(f"[bench] headline {value:.0f} explained samples/s ({ms:.3f} ms/step); secondaries next")
     # ---- secondary: standard LRP (C2, bs=64) ----
     from drsa_audio_amd.zennit.composites import NameMapComposite
     from drsa_audio_amd.xai.explain.attribute import compute_relevances
@@ -446,7 +473,9 @@ def main():
 
     drsa = None
     if not args.no_drsa and rank == 0:
+        log("[bench] DRSA C3")
         drsa = drsa_bench(device)
+    log("[bench] log-mel front end, DRSA C5 joint, VGGish")
     frontend = frontend_bench(device) if rank == 0 else None
     joint = drsa_joint_bench(device) if (rank == 0 and not args.no_drsa) else None
     vgg = vggish_lrp_bench(device) if (rank == 0 and not args.no_drsa) else None
@@ -456,6 +485,7 @@ def main():
     # the reference API returns numpy (explainer.py:111): the same steps with the D2H copy of info
     to_host = None
     if rank == 0:
+        log("[bench] to_host rate")
         for _ in range(2):
             hg.generate_subspace_heatmaps(x, to_host=True)
         torch.cuda.synchronize(device)

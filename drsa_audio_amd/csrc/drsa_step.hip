@@ -725,6 +725,10 @@ int drsa_amd_drsa_run(const float* A, const float* C, int64_t N, int d, int K, f
   DRSA_REQUIRE(A && C && U_io && U_tmp && f_traj && counter, "drsa_run: null pointer");
   hipStream_t s = (hipStream_t)stream;
   float* gs = ws_gs(ws, N, g);
+  if (use_graph && s) {   // already inside a stream capture (e.g. a torch CUDA graph): record the plain sequence
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) use_graph = 0;
+  }
   DRSA_HIP(hipMemsetAsync(counter, 0, sizeof(int), s));
   auto one = [&](const float* Uin, float* Uout) -> int {
     int rc = drsa_amd_drsa_partial(A, C, N, d, K, Uin, gs, ws, ws_size, stream);

@@ -59,9 +59,19 @@ class HeatmapGenerator:
         out = eng.subspace_heatmaps(x, cls=cls, one_hot=one_hot_encoded)
         self.info_device = out
         if to_host:
-            self.info = {"input": input_batch.detach().cpu().numpy()}
+            # the reference returns numpy (explainer.py:111): D2H into fresh pinned buffers (torch's
+            # caching host allocator), all copies queued on the stream, one wait
+            info = {}
+            if input_batch.device.type == "cpu":
+                info["input"] = input_batch.detach().numpy()
+            else:
+                info["input"] = torch.empty(input_batch.shape, dtype=input_batch.dtype, pin_memory=True)
+                info["input"].copy_(input_batch.detach(), non_blocking=True)
             for k, v in out.items():
-                self.info[k] = v.cpu().numpy()
+                info[k] = torch.empty(v.shape, dtype=v.dtype, pin_memory=True)
+                info[k].copy_(v, non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+            self.info = {k: (v.numpy() if torch.is_tensor(v) else v) for k, v in info.items()}
 
     def obtain_heatmaps(self, input_batch: torch.Tensor, one_hot_encoded: bool = False,
                         flip_all_classes: bool = False) -> torch.Tensor:
