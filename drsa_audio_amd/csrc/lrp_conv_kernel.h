@@ -35,6 +35,12 @@
 #ifndef DRSA_CONV_BWD_WPE
 #define DRSA_CONV_BWD_WPE 3
 #endif
+#ifndef DRSA_CONV_PRE_D
+#define DRSA_CONV_PRE_D 0
+#endif
+#ifndef DRSA_CONV_BWDC_WPE
+#define DRSA_CONV_BWDC_WPE 2
+#endif
 #ifndef DRSA_CONV_FWD_WPE
 #define DRSA_CONV_FWD_WPE 3
 #endif
@@ -57,7 +63,8 @@ constexpr int halo_stride(int hx, int mw) {
 }
 
 enum AMode { A_DENSE = 0, A_POOLSPARSE = 1 };
-enum Epi { EPI_FWD_POOL = 0, EPI_FWD_RELU = 1, EPI_BWD = 2 };
+// EPI_BWDC: backward with all clones of a sample in one workgroup (lrp_conv_clones.h)
+enum Epi { EPI_FWD_POOL = 0, EPI_FWD_RELU = 1, EPI_BWD = 2, EPI_BWDC = 3 };
 
 // halo column c (pixel tx0 - 1 + c) lives at LDS column c + XO, so the tile interior starts
 // 16-byte aligned (float4 staging stores) and pool cells cover aligned float2 pairs.
@@ -71,8 +78,11 @@ struct ConvCfg {
   static constexpr int RS = halo_stride(HX + XO, MW);
   static constexpr int PLANE_RAW = HY * RS;
   static constexpr int PLANE = PLANE_RAW + ((PLANE_RAW % 32) == 0 ? 4 : 0);
-  static constexpr int MTH = 16 / MW;      // M-tile height (pixels)
-  static constexpr int MTW = 2 * MW;       // M-tile width (pixels)
+  // M-tile = the 32 pixels of one MFMA B operand: window-major 2x2 pool windows (MTH = 16/MW rows
+  // x 2*MW), or for EPI_BWDC row-major MTH x MTW with MTW = min(TW, 32), so that register r of
+  // the accumulator holds 32 consecutive pixels of a row (epilogue straight to global memory)
+  static constexpr int MTW = EPI == EPI_BWDC ? (TW < 32 ? TW : 32) : 2 * MW;
+  static constexpr int MTH = 32 / MTW;
   static constexpr int MTX = TW / MTW;     // M-tiles per tile row
   static constexpr int MT = (TH / MTH) * MTX;
   static constexpr int NT = COUT / 32;
@@ -92,12 +102,13 @@ struct ConvCfg {
   static constexpr int TCH = WN * 32 / ES;                     // channels staged per epilogue pass
   static constexpr size_t staging_floats = (size_t)CIC * PLANE + (size_t)NG * KCP * COUT;
   static constexpr size_t epi_floats = (size_t)TCH * TH * TWP;
-  static constexpr size_t lds_floats = staging_floats > epi_floats ? staging_floats : epi_floats;
+  static constexpr size_t lds_floats =
+      (EPI == EPI_BWDC || staging_floats > epi_floats) ? staging_floats : epi_floats;
   // minimum waves per SIMD the register allocation must allow (1 block = 1 wave per SIMD)
-  static constexpr int WPE = (EPI == EPI_BWD && NG == 1) ? (SMALL_BWD ? 4 : DRSA_CONV_BWD_WPE)
+  static constexpr int WPE = EPI == EPI_BWDC ? DRSA_CONV_BWDC_WPE : (EPI == EPI_BWD && NG == 1) ? (SMALL_BWD ? 4 : DRSA_CONV_BWD_WPE)
                              : (EPI != EPI_BWD && CIC <= 8 && COUT <= 32 && NG <= 2 ? DRSA_CONV_FWD_WPE : 1);
   // operand prefetch distance of the MFMA loop (k-steps)
-  static constexpr int PD = DRSA_CONV_PD_BWD > 0 && EPI == EPI_BWD ? DRSA_CONV_PD_BWD : 1;
+  static constexpr int PD = DRSA_CONV_PD_BWD > 0 && EPI >= EPI_BWD ? DRSA_CONV_PD_BWD : 1;
   static_assert(TH % MTH == 0 && TW % MTW == 0, "tile must be a multiple of the M-tile");
   static_assert(COUT % 32 == 0, "COUT must be padded to 32");
   static_assert(CIN % CIC == 0, "CIN must be a multiple of the chunk");
@@ -351,7 +362,7 @@ __device__ __forceinline__ void mfma_chunk(const float* halo, const float* wl, c
           float x = xr[cur][u];
           // NG == 2 is the Gamma forward on a non-negative input (ABI contract): x+ = x, so both
           // sets read the same operand with no per-k-step transform
-          if constexpr (EPI != EPI_BWD && NG == 3) {
+          if constexpr (EPI < EPI_BWD && NG == 3) {
             x = (g == 0) ? x : (g == 1 ? fmaxf(x, 0.f) : fminf(x, 0.f));
           }
           acc[g][u][v] = mfma32(wr[cur][g][v], x, acc[g][u][v]);
@@ -408,17 +419,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[g][u][v][r] = 0.f;
 
-  Stager<Cfg> stg;
-  stg.load(a, 0, tid, ty0, tx0, bq, bs);
-  for (int chunk = 0; chunk < Cfg::NCHUNK; ++chunk) {
-    __syncthreads();
-    stg.store(halo, wl, tid);
-    __syncthreads();
-    if (chunk + 1 < Cfg::NCHUNK) stg.load(a, (chunk + 1) * CIC, tid, ty0, tx0, bq, bs);
-    if (!active || (a.dbg & 4)) continue;
-    mfma_chunk<Cfg, Cfg::PD>(halo, wl, pix_off, lane, wn, acc);
-  }
-
   // ---- epilogue, staged through LDS so global I/O is coalesced float4 rows ----
   // pass (v, kind): every active wave writes its 32-channel slice (n-tile wn*NPW + v) of its
   // m-tiles into T[TCH][TH][TWP] (lane = pixel, register = channel: conflict-free rows),
@@ -453,6 +453,57 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
   auto gch = [&](int cl, int v) { return ((cl >> 5) * NPW + v) * 32 + (cl & 31); };   // global channel
   // global channel of staged row cl in pass sub (ES = 2 implies WN = 1)
   auto gchs = [&](int cl, int v, int sub) { return ES == 1 ? gch(cl, v) : v * 32 + sub * TCH + cl; };
+  constexpr int Q = TH * TW / 4, CS = kThreads / Q;
+  static_assert(kThreads % Q == 0, "float4 groups per tile must divide the block");
+  const int cl0 = tid / Q, rem = tid % Q;
+  const int py = rem / (TW / 4), px = (rem % (TW / 4)) * 4;
+  const bool pix_ok = ty0 + py < H && tx0 + px < W;
+  const int HW = H * W;
+  const size_t pix = pix_ok ? (size_t)(ty0 + py) * W + tx0 + px : 0;
+  const float* xs = a.x ? a.x + (size_t)bs * a.cout * HW + pix : nullptr;
+  const float* ds = a.den ? a.den + (size_t)bs * a.cout * HW + pix : nullptr;
+  float* oqp = a.out + (size_t)bq * a.cout * HW + pix;
+  // x and den come from clamped, always valid addresses (den falls back to x or out when the
+  // mode does not use it) and are ALL issued before any arithmetic; the rule / post modes are
+  // uniform selects, not branches (a branch around the division would put each den load in
+  // its own basic block, one full memory round trip after another)
+  const bool need_x = (a.xmode != XM_NONE || a.post != POST_NONE) && !(a.dbg & 2);
+  const bool mul_x = a.xmode != XM_NONE && !(a.dbg & 2), split_x = a.xmode == XM_SPLIT && !(a.dbg & 2);
+  const bool post_div = a.post == POST_DIV, post_any = a.post != POST_NONE;
+  const float* xsrc = xs ? xs : oqp;
+  const float* dsrc = (ds && post_div) ? ds : xsrc;
+  const float eps = a.eps;
+  // epilogue x/den loads of (n-tile v, pass sub); (0, 0) is issued before the last chunk's MFMAs
+  auto epi_loads = [&](int v, int sub, float4 (&xk)[V4T], float4 (&dk)[V4T], bool lx = true, bool ld = true) {
+#pragma unroll
+    for (int it = 0; it < V4T; ++it) {
+      const int cl = cl0 + it * CS;
+      const int co = gchs(cl, v, sub);
+      const bool ok = cl < TCH && co < a.cout;
+      const int coc = ok ? co : 0;
+      if (lx) xk[it] = *reinterpret_cast<const float4*>(xsrc + (size_t)coc * HW);
+      if (ld) dk[it] = *reinterpret_cast<const float4*>(dsrc + (size_t)coc * HW);
+    }
+  };
+  float4 pre_x[V4T], pre_d[V4T];
+  Stager<Cfg> stg;
+  stg.load(a, 0, tid, ty0, tx0, bq, bs);
+  for (int chunk = 0; chunk + 1 < Cfg::NCHUNK; ++chunk) {
+    __syncthreads();
+    stg.store(halo, wl, tid);
+    __syncthreads();
+    stg.load(a, (chunk + 1) * CIC, tid, ty0, tx0, bq, bs);
+    if (!active || (a.dbg & 4)) continue;
+    mfma_chunk<Cfg, Cfg::PD>(halo, wl, pix_off, lane, wn, acc);
+  }
+  // last chunk, peeled: the staging registers are free, so the backward epilogue's first x/den
+  // loads go out here and their latency hides under the MFMAs
+  __syncthreads();
+  stg.store(halo, wl, tid);
+  __syncthreads();
+  if constexpr (EPI == EPI_BWD) epi_loads(0, 0, pre_x, pre_d, true, DRSA_CONV_PRE_D);
+  if (active && !(a.dbg & 4)) mfma_chunk<Cfg, Cfg::PD>(halo, wl, pix_off, lane, wn, acc);
+
 #pragma unroll
   for (int v = 0; v < NPW; ++v) {
     if constexpr (EPI == EPI_FWD_POOL || EPI == EPI_FWD_RELU) {
@@ -593,40 +644,56 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
       // a channel offset.  Loads come from clamped (always valid) addresses and the arithmetic
       // runs unconditionally (no exec branches that would serialise the load latency); only the
       // store is masked.  x is loaded once for the rule and the division.
-      constexpr int Q = TH * TW / 4, CS = kThreads / Q;
-      static_assert(kThreads % Q == 0, "float4 groups per tile must divide the block");
-      const int cl0 = tid / Q, rem = tid % Q;
-      const int py = rem / (TW / 4), px = (rem % (TW / 4)) * 4;
-      const bool pix_ok = ty0 + py < H && tx0 + px < W;
-      const int HW = H * W;
-      const size_t pix = pix_ok ? (size_t)(ty0 + py) * W + tx0 + px : 0;
-      const float* xs = a.x ? a.x + (size_t)bs * a.cout * HW + pix : nullptr;
-      const float* ds = a.den ? a.den + (size_t)bs * a.cout * HW + pix : nullptr;
-      float* oqp = a.out + (size_t)bq * a.cout * HW + pix;
-      const bool need_x = (a.xmode != XM_NONE || a.post != POST_NONE) && !(a.dbg & 2);
+#pragma unroll
      for (int sub = 0; sub < ES; ++sub) {
-      float4 Rk[V4T], xk[V4T];
+      float4 Rk[V4T], xk[V4T], dk[V4T];
+      if (v == 0 && sub == 0) {
+#pragma unroll
+        for (int it = 0; it < V4T; ++it) xk[it] = pre_x[it];
+        if (DRSA_CONV_PRE_D) {
+#pragma unroll
+          for (int it = 0; it < V4T; ++it) dk[it] = pre_d[it];
+        } else {
+          epi_loads(v, sub, xk, dk, false, true);
+        }
+      } else {
+        epi_loads(v, sub, xk, dk);
+      }
       stage(v, [&](int u, int r) { return acc[0][u][v][r]; }, sub);
+      // the common mode (Epsilon-type rule: R = x * J^T g, then the next layer's division)
+      // specialised: the loads above are already in flight, this branch is uniform
+      if (NG == 1 && a.xmode == XM_MUL && post_div && !(a.dbg & 2)) {
+#pragma unroll
+        for (int it = 0; it < V4T; ++it) {
+          const int cl = cl0 + it * CS;
+          const int co = gchs(cl, v, sub);
+          const bool ok = cl < TCH && co < a.cout;
+          const int clc = ok ? cl : 0, coc = ok ? co : 0;
+          const float4 t = *reinterpret_cast<const float4*>(T + (clc * TH + py) * TWP + px);
+          const float4 x = xk[it], d = dk[it];
+          auto f = [&](float tt, float xx, float dd) {
+            const float q = div_nb(xx * tt, stab(dd, eps));
+            return (xx > 0.f) ? q : 0.f;
+          };
+          const float4 R = make_float4(f(t.x, x.x, d.x), f(t.y, x.y, d.y), f(t.z, x.z, d.z), f(t.w, x.w, d.w));
+          if (ok && pix_ok) *reinterpret_cast<float4*>(oqp + (size_t)coc * HW) = R;
+        }
+        continue;
+      }
 #pragma unroll
       for (int it = 0; it < V4T; ++it) {
         const int cl = cl0 + it * CS;
         const int co = gchs(cl, v, sub);
-        const bool ok = cl < TCH && co < a.cout;
-        const int clc = ok ? cl : 0, coc = ok ? co : 0;
+        const int clc = (cl < TCH && co < a.cout) ? cl : 0;
         const float4 t = *reinterpret_cast<const float4*>(T + (clc * TH + py) * TWP + px);
-        xk[it] = need_x ? *reinterpret_cast<const float4*>(xs + (size_t)coc * HW) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (!need_x) xk[it] = make_float4(0.f, 0.f, 0.f, 0.f);
         const float4 x = xk[it];
-        if (a.xmode == XM_NONE || (a.dbg & 2)) {
-          Rk[it] = t;
-        } else if (a.xmode == XM_MUL) {
-          Rk[it] = make_float4(x.x * t.x, x.y * t.y, x.z * t.z, x.w * t.w);
-        } else {
-          Rk[it] = make_float4(fmaxf(x.x, 0.f) * t.x, fmaxf(x.y, 0.f) * t.y, fmaxf(x.z, 0.f) * t.z,
-                               fmaxf(x.w, 0.f) * t.w);
-        }
+        // XM_NONE: 1 * t = t;  XM_MUL: x * t;  XM_SPLIT: max(x, 0) * t
+        auto xm = [&](float xx) { const float m = split_x ? fmaxf(xx, 0.f) : xx; return mul_x ? m : 1.f; };
+        Rk[it] = make_float4(xm(x.x) * t.x, xm(x.y) * t.y, xm(x.z) * t.z, xm(x.w) * t.w);
       }
       if constexpr (NG >= 2) {
-        if (a.xmode == XM_SPLIT) {
+        if (split_x) {
           stage(v, [&](int u, int r) { return acc[1][u][v][r]; }, sub);
 #pragma unroll
           for (int it = 0; it < V4T; ++it) {
@@ -653,23 +720,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
           if (ok && pix_ok && R.x == 12345.f) oqp[(size_t)coc * HW] = 1.f;
           continue;
         }
-        if (a.post == POST_DIV) {
-          const float4 x = xk[it];
-          const float4 d = *reinterpret_cast<const float4*>(ds + (size_t)coc * HW);
-          // quotients first (evaluated for every lane), then the ReLU-backward select
-          const float qx = div_nb(R.x, stab(d.x, a.eps)), qy = div_nb(R.y, stab(d.y, a.eps));
-          const float qz = div_nb(R.z, stab(d.z, a.eps)), qw = div_nb(R.w, stab(d.w, a.eps));
-          R.x = (x.x > 0.f) ? qx : 0.f;
-          R.y = (x.y > 0.f) ? qy : 0.f;
-          R.z = (x.z > 0.f) ? qz : 0.f;
-          R.w = (x.w > 0.f) ? qw : 0.f;
-        } else if (a.post == POST_MASK) {
-          const float4 x = xk[it];
-          R.x = (x.x > 0.f) ? R.x : 0.f;
-          R.y = (x.y > 0.f) ? R.y : 0.f;
-          R.z = (x.z > 0.f) ? R.z : 0.f;
-          R.w = (x.w > 0.f) ? R.w : 0.f;
-        }
+        // POST_DIV: x > 0 ? R / stab(den) : 0;  POST_MASK: x > 0 ? R : 0 (quotients evaluated for
+        // every lane and mode, then selected)
+        const float4 x = xk[it], d = dk[it];
+        auto post = [&](float rr, float xx, float dd) {
+          const float q = div_nb(rr, stab(dd, eps));
+          const float y = post_div ? q : rr;
+          return (post_any && !(xx > 0.f)) ? 0.f : y;
+        };
+        R = make_float4(post(R.x, x.x, d.x), post(R.y, x.y, d.y), post(R.z, x.z, d.z), post(R.w, x.w, d.w));
         if (ok && pix_ok) *reinterpret_cast<float4*>(oqp + (size_t)coc * HW) = R;
       }
      }

@@ -163,37 +163,55 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(LinArgs a) {
 
 // ===========================================================================
 // projection forward: h = a_vec U, a' = h U^T, optional 2x2 max-pool of a'
-//   a [B][D][H][W] -> h [B][D][H*W] (channel-major), ap [B][D][H][W], pooled + argmax
+//   a [B][d][H][W] -> h [B][d][H*W] (channel-major), ap [B][d][H][W], pooled + argmax
 //   tile = 2 rows x 32 cols (64 pixels); a workgroup stages U once and walks PT tiles.
 //   MFMA orientation D[channel][pixel]: lanes = pixels (coalesced I/O).
+// Any d <= DP (DP = 16, 32, 64, 128): U and a are embedded in DP x DP / DP rows with zeros;
+// the k chains run over d4 = round_up(d, 4) terms only, so for d % 4 == 0 (VGGish d = 100, 96)
+// every value is the d-term chain of the unpadded product, bit for bit; outputs past d are
+// computed (zeros) but not stored.
 // ===========================================================================
 constexpr int PT = 4;   // row-pair tiles per workgroup
 
-template <int D>
+template <int DP>
+__device__ __forceinline__ void stage_u_padded(float* Us, const float* __restrict__ U, int d, int tid) {
+  constexpr int LD = DP + 1;
+  for (int i = tid; i < DP * DP; i += 256) {
+    const int c = i / DP, j = i % DP;
+    const bool ok = c < d && j < d;
+    const float v = U[ok ? c * d + j : 0];
+    Us[c * LD + j] = ok ? v : 0.f;
+  }
+}
+
+template <int DP>
 __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __restrict__ a, const float* __restrict__ U,
                                                             float* __restrict__ h, float* __restrict__ ap,
                                                             float* __restrict__ pooled, uint8_t* __restrict__ amax,
-                                                            int H, int W, int pool) {
-  constexpr int P = 64, LD = D + 1, PL = P + 4;
+                                                            int d, int H, int W, int pool) {
+  constexpr int P = 64, LD = DP + 1, PL = P + 4;
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* Us = sm;               // [D][LD]   U[c][j]
-  float* as = Us + D * LD;      // [D][PL]   a tile, then a' tile
-  float* hs = as + D * PL;      // [D][PL]   h tile
+  float* Us = sm;               // [DP][LD]   U[c][j]
+  float* as = Us + DP * LD;     // [DP][PL]   a tile, then a' tile
+  float* hs = as + DP * PL;     // [DP][PL]   h tile
   const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
   const int b = blockIdx.y;
   const int TW = W < 32 ? W : 32, RPT = P / TW;      // tile = RPT rows x TW cols
   const int HW = H * W, xt = W / TW;
-  for (int i = tid; i < D * D; i += 256) Us[(i / D) * LD + i % D] = U[i];
-  constexpr int NB = D / 16;
+  const int d4 = (d + 3) & ~3;
+  stage_u_padded<DP>(Us, U, d, tid);
+  constexpr int NB = DP / 16;
   static_assert(P / 16 == 4, "one 16-pixel block per wave");
   for (int t = 0; t < PT; ++t) {
     const int tile = blockIdx.x * PT + t;
     if (tile >= (H / RPT) * xt) break;
     const int y0 = (tile / xt) * RPT, x0 = (tile % xt) * TW;
     __syncthreads();
-    for (int i = tid; i < D * P; i += 256) {
+    for (int i = tid; i < DP * P; i += 256) {
       const int c = i / P, p = i % P;
-      as[c * PL + p] = a[((size_t)b * D + c) * HW + (y0 + p / TW) * W + x0 + p % TW];
+      const bool ok = c < d;
+      const float v = a[((size_t)b * d + (ok ? c : 0)) * HW + (y0 + p / TW) * W + x0 + p % TW];
+      as[c * PL + p] = ok ? v : 0.f;
     }
     __syncthreads();
     // h[j][p] = sum_c U[c][j] a[c][p]: wave w owns pixel block w and runs the NB output blocks
@@ -203,7 +221,7 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
 #pragma unroll
       for (int jb = 0; jb < NB; ++jb) acc[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
-      for (int k0 = 0; k0 < D; k0 += 4) {
+      for (int k0 = 0; k0 < d4; k0 += 4) {
         const int c = k0 + (lane >> 4);
         const float bv = as[c * PL + w * 16 + (lane & 15)];
 #pragma unroll
@@ -215,7 +233,7 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
         for (int r = 0; r < 4; ++r) {
           const int j = jb * 16 + (lane >> 4) * 4 + r, p = w * 16 + (lane & 15);
           hs[j * PL + p] = acc[jb][r];
-          if (h) h[((size_t)b * D + j) * HW + (y0 + p / TW) * W + x0 + p % TW] = acc[jb][r];
+          if (h && j < d) h[((size_t)b * d + j) * HW + (y0 + p / TW) * W + x0 + p % TW] = acc[jb][r];
         }
     }
     __syncthreads();
@@ -225,7 +243,7 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
 #pragma unroll
       for (int cb = 0; cb < NB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
-      for (int k0 = 0; k0 < D; k0 += 4) {
+      for (int k0 = 0; k0 < d4; k0 += 4) {
         const int j = k0 + (lane >> 4);
         const float bv = hs[j * PL + w * 16 + (lane & 15)];
 #pragma unroll
@@ -237,14 +255,14 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
         for (int r = 0; r < 4; ++r) {
           const int c = cb * 16 + (lane >> 4) * 4 + r, p = w * 16 + (lane & 15);
           as[c * PL + p] = acc[cb][r];   // a tile no longer needed: holds a' now
-          if (ap) ap[((size_t)b * D + c) * HW + (y0 + p / TW) * W + x0 + p % TW] = acc[cb][r];
+          if (ap && c < d) ap[((size_t)b * d + c) * HW + (y0 + p / TW) * W + x0 + p % TW] = acc[cb][r];
         }
     }
     if (pool) {
       __syncthreads();
       const int H2 = H / 2, W2 = W / 2;
       const int CXN = TW / 2;
-      for (int i = tid; i < D * 16; i += 256) {
+      for (int i = tid; i < d * 16; i += 256) {
         const int c = i / 16, cell = i % 16, cy = cell / CXN, cx = cell % CXN;
         const int p00 = (2 * cy) * TW + 2 * cx;
         const float v[4] = {as[c * PL + p00], as[c * PL + p00 + 1], as[c * PL + p00 + TW],
@@ -253,7 +271,7 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
         float m = v[0];
         for (int s4 = 1; s4 < 4; ++s4)
           if (v[s4] > m || (v[s4] != v[s4] && m == m)) { m = v[s4]; am = s4; }
-        const size_t o = ((size_t)b * D + c) * H2 * W2 + (y0 / 2 + cy) * W2 + x0 / 2 + cx;
+        const size_t o = ((size_t)b * d + c) * H2 * W2 + (y0 / 2 + cy) * W2 + x0 / 2 + cx;
         pooled[o] = m;
         amax[o] = (uint8_t)am;
       }
@@ -282,26 +300,27 @@ constexpr int PT_BWD = DRSA_PT_BWD;   // tiles per workgroup (backward)
 #define PROJ_CLONE_UNROLL 1
 #endif
 
-template <int D>
+template <int DP>
 __global__ __launch_bounds__(256) void projection_bwd_kernel(
     const float* __restrict__ gp, const uint8_t* __restrict__ amax, const float* __restrict__ ap,
     const float* __restrict__ h, const float* __restrict__ a, const float* __restrict__ den,
-    const float* __restrict__ U, float* __restrict__ G, int H, int W, int K, float eps_proj, float eps_den,
+    const float* __restrict__ U, float* __restrict__ G, int d, int H, int W, int K, float eps_proj, float eps_den,
     int sparse, int has_den, int fanout) {
-  constexpr int P = 64, LD = D + 1, PL = P + 4;
-  constexpr int NB = D / 16, TILES = NB * (P / 16), QW = TILES / 4;   // 16x16 blocks; per wave
+  constexpr int P = 64, LD = DP + 1, PL = P + 4;
+  constexpr int NB = DP / 16, TILES = NB * (P / 16), QW = TILES / 4;   // 16x16 blocks; per wave
   // Per wave: pixel block pb = wave, channel blocks cb = 0..NB-1 (q = wave + 4 i).  Its h, a,
   // den values (MFMA output layout) are prefetched at the start, with the staging loads.
-  constexpr bool PF = D <= 64;
+  // Rows c >= d (padded embedding) are zero in U and g1 and never stored.
+  constexpr bool PF = DP <= 64;
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* Us = sm;               // [D][LD]
-  float* g1 = Us + D * LD;      // [D][PL]
-  float* g2 = g1 + D * PL;      // [D][PL]
+  float* Us = sm;               // [DP][LD]
+  float* g1 = Us + DP * LD;     // [DP][PL]
+  float* g2 = g1 + DP * PL;     // [DP][PL]
   const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
   const int b = blockIdx.y;
   const int TW = W < 32 ? W : 32, RPT = P / TW;
   const int HW = H * W, xt = W / TW;
-  const int dk = D / K;
+  const int dk = d / K, d4 = (d + 3) & ~3;
   const int nq = fanout ? (K + 1) : 1;
   for (int t = 0; t < PT_BWD; ++t) {
     const int tile = blockIdx.x * PT_BWD + t;
@@ -317,29 +336,33 @@ __global__ __launch_bounds__(256) void projection_bwd_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int c = i * 16 + (lane >> 4) * 4 + r;
-          const size_t os = ((size_t)b * D + c) * HW + pixl;
-          hv[i * 4 + r] = h[os];
-          av[i * 4 + r] = a[os];
-          dv[i * 4 + r] = has_den ? den[os] : 1.f;
+          const bool ok = c < d;
+          const size_t os = ((size_t)b * d + (ok ? c : 0)) * HW + pixl;
+          const float hh = h[os], aa = a[os], dd = has_den ? den[os] : 1.f;
+          hv[i * 4 + r] = ok ? hh : 0.f;
+          av[i * 4 + r] = ok ? aa : 0.f;
+          dv[i * 4 + r] = dd;
         }
     }
     __syncthreads();
-    if (t == 0)
-      for (int i = tid; i < D * D; i += 256) Us[(i / D) * LD + i % D] = U[i];
+    if (t == 0) stage_u_padded<DP>(Us, U, d, tid);
 #pragma unroll PROJ_STAGE_UNROLL
-    for (int i = tid; i < D * P; i += 256) {
+    for (int i = tid; i < DP * P; i += 256) {
       const int c = i / P, p = i % P;
       const int y = y0 + p / TW, x = x0 + p % TW;
+      const bool ok = c < d;
+      const int cc = ok ? c : 0;
       float R;
       if (sparse) {
         const int H2 = H / 2, W2 = W / 2;
-        const size_t q = ((size_t)b * D + c) * H2 * W2 + (y >> 1) * W2 + (x >> 1);
+        const size_t q = ((size_t)b * d + cc) * H2 * W2 + (y >> 1) * W2 + (x >> 1);
         const float gv = gp[q];
         R = (amax[q] == (((y & 1) << 1) | (x & 1))) ? gv : 0.f;
       } else {
-        R = gp[((size_t)b * D + c) * HW + y * W + x];
+        R = gp[((size_t)b * d + cc) * HW + y * W + x];
       }
-      g1[c * PL + p] = R / stab(ap[((size_t)b * D + c) * HW + y * W + x], eps_proj);
+      const float v = R / stab(ap[((size_t)b * d + cc) * HW + y * W + x], eps_proj);
+      g1[c * PL + p] = ok ? v : 0.f;
     }
     __syncthreads();
     // t[j][p] = sum_c U[c][j] g1[c][p];  R_h = h (.) t;  g2 = R_h / stab(h)
@@ -348,7 +371,7 @@ __global__ __launch_bounds__(256) void projection_bwd_kernel(
       const int jb = i, pb = w;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
-      for (int k0 = 0; k0 < D; k0 += 4) {
+      for (int k0 = 0; k0 < d4; k0 += 4) {
         const int c = k0 + (lane >> 4);
         acc = mfma16(Us[c * LD + jb * 16 + (lane & 15)], g1[c * PL + pb * 16 + (lane & 15)], acc);
       }
@@ -356,8 +379,12 @@ __global__ __launch_bounds__(256) void projection_bwd_kernel(
       for (int r = 0; r < 4; ++r) {
         const int j = jb * 16 + (lane >> 4) * 4 + r, p = pb * 16 + (lane & 15);
         float hx;
-        if constexpr (PF) hx = hv[i * 4 + r];
-        else hx = h[((size_t)b * D + j) * HW + pixl];
+        if constexpr (PF) {
+          hx = hv[i * 4 + r];
+        } else {
+          const float hh = h[((size_t)b * d + (j < d ? j : 0)) * HW + pixl];
+          hx = j < d ? hh : 0.f;
+        }
         const float Rh = hx * acc[r];
         g2[j * PL + p] = Rh / stab(hx, eps_proj);
       }
@@ -365,7 +392,7 @@ __global__ __launch_bounds__(256) void projection_bwd_kernel(
     __syncthreads();
     for (int qi = 0; qi < nq; ++qi) {
       const int q = fanout ? qi : b % (K + 1);
-      const int j0 = q == 0 ? 0 : (q - 1) * dk, j1 = q == 0 ? D : q * dk;
+      const int j0 = q == 0 ? 0 : (q - 1) * dk, j1 = q == 0 ? d : q * dk;
       const size_t orow = fanout ? (size_t)b * (K + 1) + q : (size_t)b;
 #pragma unroll
       for (int i = 0; i < QW; ++i) {
@@ -382,7 +409,8 @@ __global__ __launch_bounds__(256) void projection_bwd_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int c = cb * 16 + (lane >> 4) * 4 + r;
-          const size_t os = ((size_t)b * D + c) * HW + pixl;
+          const bool cok = c < d;
+          const size_t os = ((size_t)b * d + (cok ? c : 0)) * HW + pixl;
           float ax, dx;
           if constexpr (PF) { ax = av[i * 4 + r]; dx = dv[i * 4 + r]; }
           else { ax = a[os]; dx = has_den ? den[os] : 1.f; }
@@ -394,7 +422,7 @@ __global__ __launch_bounds__(256) void projection_bwd_kernel(
           } else {
             gq = (ax > 0.f) ? Rv : 0.f;
           }
-          G[(orow * D + c) * HW + pixl] = gq;
+          if (cok) G[(orow * d + c) * HW + pixl] = gq;
         }
       }
     }
@@ -407,7 +435,7 @@ __global__ __launch_bounds__(256) void projection_bwd_kernel(
 // as projection_fwd_kernel (h, a') and projection_bwd_kernel (t, clones), so every value is
 // bit-identical to the stored-buffer path.  Each wave owns one 16-pixel block of the 64-pixel
 // tile end to end, so after U is staged no workgroup barrier is needed:
-//   region A [D][16]: a, then g1;  region B [D][16]: h, then g2   (wave-private LDS)
+//   region A [DP][16]: a, then g1;  region B [DP][16]: h, then g2   (wave-private LDS)
 // ===========================================================================
 #ifndef DRSA_PT_RC
 #define DRSA_PT_RC 4
@@ -417,25 +445,25 @@ constexpr int PT_RC = DRSA_PT_RC;   // tiles per workgroup (U staged once)
 #define DRSA_PROJ_RC_WPE 3
 #endif
 
-template <int D>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? DRSA_PROJ_RC_WPE : 1))) void projection_bwd_rc_kernel(
+template <int DP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? DRSA_PROJ_RC_WPE : 1))) void projection_bwd_rc_kernel(
     const float* __restrict__ gp, const uint8_t* __restrict__ amax, const float* __restrict__ a,
-    const float* __restrict__ den, const float* __restrict__ U, float* __restrict__ G, int H, int W, int K,
+    const float* __restrict__ den, const float* __restrict__ U, float* __restrict__ G, int d, int H, int W, int K,
     float eps_proj, float eps_den, int sparse, int has_den, int fanout) {
-  constexpr int P = 64, LD = D + 1, PW = 16, NB = D / 16;
-  constexpr bool PF = D <= 64;   // keep a / den of the output rows in registers
+  constexpr int P = 64, LD = DP + 1, PW = 16, NB = DP / 16;
+  constexpr bool PF = DP <= 64;   // keep a / den of the output rows in registers
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
-  float* Us = sm;                                   // [D][LD]
-  float* RA = Us + D * LD + w * 2 * D * PW;         // [D][PW]
-  float* RB = RA + D * PW;                          // [D][PW]
+  float* Us = sm;                                   // [DP][LD]
+  float* RA = Us + DP * LD + w * 2 * DP * PW;       // [DP][PW]
+  float* RB = RA + DP * PW;                         // [DP][PW]
   const int b = blockIdx.y;
   const int TW = W < 32 ? W : 32, RPT = P / TW;
   const int HW = H * W, xt = W / TW, H2 = H / 2, W2 = W / 2;
-  const int dk = D / K;
+  const int dk = d / K, d4 = (d + 3) & ~3;
   const int nq = fanout ? (K + 1) : 1;
   const int pc = lane & 15, rg = lane >> 4;         // pixel column / row group of the MFMA layouts
-  for (int i = tid; i < D * D; i += 256) Us[(i / D) * LD + i % D] = U[i];
+  stage_u_padded<DP>(Us, U, d, tid);
   __syncthreads();
   for (int t = 0; t < PT_RC; ++t) {
     const int tile = blockIdx.x * PT_RC + t;
@@ -451,8 +479,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? D
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int c = i * 16 + rg * 4 + r;
-        const size_t os = ((size_t)b * D + c) * HW + pixl;
-        av[i * 4 + r] = a[os];
+        const bool ok = c < d;
+        const size_t os = ((size_t)b * d + (ok ? c : 0)) * HW + pixl;
+        const float aa = a[os];
+        av[i * 4 + r] = ok ? aa : 0.f;
         if constexpr (PF) dv[i * 4 + r] = has_den ? den[os] : 1.f;
       }
     __builtin_amdgcn_wave_barrier();
@@ -467,7 +497,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? D
 #pragma unroll
       for (int jb = 0; jb < NB; ++jb) acc[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
-      for (int k0 = 0; k0 < D; k0 += 4) {
+      for (int k0 = 0; k0 < d4; k0 += 4) {
         const int c = k0 + rg;
         const float bv = RA[c * PW + pc];
 #pragma unroll
@@ -485,7 +515,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? D
 #pragma unroll
       for (int cb = 0; cb < NB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
-      for (int k0 = 0; k0 < D; k0 += 4) {
+      for (int k0 = 0; k0 < d4; k0 += 4) {
         const int j = k0 + rg;
         const float bv = RB[j * PW + pc];
 #pragma unroll
@@ -496,15 +526,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? D
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int c = cb * 16 + rg * 4 + r;
+          const bool ok = c < d;
+          const int cc = ok ? c : 0;
           float R;
           if (sparse) {
-            const size_t q = ((size_t)b * D + c) * H2 * W2 + (py >> 1) * W2 + (px >> 1);
+            const size_t q = ((size_t)b * d + cc) * H2 * W2 + (py >> 1) * W2 + (px >> 1);
             const float gv = gp[q];   // unconditional load, then the argmax select
             R = (amax[q] == (((py & 1) << 1) | (px & 1))) ? gv : 0.f;
           } else {
-            R = gp[((size_t)b * D + c) * HW + pixl];
+            R = gp[((size_t)b * d + cc) * HW + pixl];
           }
-          RA[c * PW + pc] = R / stab(acc[cb][r], eps_proj);
+          const float v = R / stab(acc[cb][r], eps_proj);
+          RA[c * PW + pc] = ok ? v : 0.f;
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -514,7 +547,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? D
 #pragma unroll
       for (int jb = 0; jb < NB; ++jb) acc[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
-      for (int k0 = 0; k0 < D; k0 += 4) {
+      for (int k0 = 0; k0 < d4; k0 += 4) {
         const int c = k0 + rg;
         const float bv = RA[c * PW + pc];
 #pragma unroll
@@ -532,7 +565,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? D
     __builtin_amdgcn_wave_barrier();
     for (int qi = 0; qi < nq; ++qi) {
       const int q = fanout ? qi : b % (K + 1);
-      const int j0 = q == 0 ? 0 : (q - 1) * dk, j1 = q == 0 ? D : q * dk;
+      const int j0 = q == 0 ? 0 : (q - 1) * dk, j1 = q == 0 ? d : q * dk;
       const size_t orow = fanout ? (size_t)b * (K + 1) + q : (size_t)b;
       f32x4 acc[NB];
 #pragma unroll
@@ -549,7 +582,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? D
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int c = cb * 16 + rg * 4 + r;
-          const size_t os = ((size_t)b * D + c) * HW + pixl;
+          const bool cok = c < d;
+          const size_t os = ((size_t)b * d + (cok ? c : 0)) * HW + pixl;
           const float ax = av[cb * 4 + r];
           float dx = 1.f;
           if constexpr (PF) dx = dv[cb * 4 + r];
@@ -562,7 +596,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? D
           } else {
             gq = (ax > 0.f) ? Rv : 0.f;
           }
-          G[(orow * D + c) * HW + pixl] = gq;
+          if (cok) G[(orow * d + c) * HW + pixl] = gq;
         }
     }
   }
@@ -858,6 +892,9 @@ int with_lds(F* fn, size_t lds) {
   return drsa::ensure_smem((const void*)fn, lds);   // per device, thread-safe
 }
 
+// padded projection width: the smallest instantiated DP >= d (0 = unsupported)
+int proj_dp(int d) { return d < 1 ? 0 : d <= 16 ? 16 : d <= 32 ? 32 : d <= 64 ? 64 : d <= 128 ? 128 : 0; }
+
 template <int D>
 size_t proj_fwd_lds() { return ((size_t)D * (D + 1) + 2 * (size_t)D * 68) * sizeof(float); }
 template <int D>
@@ -910,12 +947,12 @@ int drsa_amd_projection_fwd(const float* a, const float* U, float* h, float* ap,
   hipStream_t s = (hipStream_t)stream;
   const int tiles = (H / (64 / TW)) * (W / TW);
   const dim3 grid((tiles + PT - 1) / PT, B);
-  switch (D) {
+  switch (proj_dp(D)) {
 #define PF(DD)                                                                                        \
   case DD: {                                                                                          \
     { int rc = with_lds(projection_fwd_kernel<DD>, proj_fwd_lds<DD>()); if (rc) return rc; }                                  \
     hipLaunchKernelGGL(projection_fwd_kernel<DD>, grid, dim3(256), proj_fwd_lds<DD>(), s, a, U, h, ap, pooled, amax, \
-                       H, W, pool);                                                                   \
+                       D, H, W, pool);                                                                \
     break;                                                                                            \
   }
     PF(16) PF(32) PF(64) PF(128)
@@ -940,12 +977,12 @@ int drsa_amd_projection_bwd(const float* gp, const uint8_t* amax, const float* a
   const int sparse = amax != nullptr, has_den = den != nullptr;
   if (!ap || !h) {   // recompute h and a' from a
     const dim3 grid((tiles + PT_RC - 1) / PT_RC, B);
-    switch (D) {
+    switch (proj_dp(D)) {
 #define PR(DD)                                                                                        \
   case DD: {                                                                                          \
     { int rc = with_lds(projection_bwd_rc_kernel<DD>, proj_bwd_rc_lds<DD>()); if (rc) return rc; }                                  \
     hipLaunchKernelGGL(projection_bwd_rc_kernel<DD>, grid, dim3(256), proj_bwd_rc_lds<DD>(), s, gp, amax, a, den, U, G, \
-                       H, W, K, eps_proj, eps_den, sparse, has_den, fanout);                         \
+                       D, H, W, K, eps_proj, eps_den, sparse, has_den, fanout);                      \
     break;                                                                                            \
   }
       PR(16) PR(32) PR(64) PR(128)
@@ -958,12 +995,12 @@ int drsa_amd_projection_bwd(const float* gp, const uint8_t* amax, const float* a
     return DRSA_OK;
   }
   const dim3 grid((tiles + PT_BWD - 1) / PT_BWD, B);
-  switch (D) {
+  switch (proj_dp(D)) {
 #define PB(DD)                                                                                        \
   case DD: {                                                                                          \
     { int rc = with_lds(projection_bwd_kernel<DD>, proj_bwd_lds<DD>()); if (rc) return rc; }                                  \
     hipLaunchKernelGGL(projection_bwd_kernel<DD>, grid, dim3(256), proj_bwd_lds<DD>(), s, gp, amax, ap, h, a, den, U, \
-                       G, H, W, K, eps_proj, eps_den, sparse, has_den, fanout);                               \
+                       G, D, H, W, K, eps_proj, eps_den, sparse, has_den, fanout);                            \
     break;                                                                                            \
   }
     PB(16) PB(32) PB(64) PB(128)

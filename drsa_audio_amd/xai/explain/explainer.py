@@ -31,7 +31,10 @@ from .attribute import SubspaceHook, compute_relevances
 class HeatmapGenerator:
     def __init__(self, model: nn.Module, U: torch.Tensor, name_map: List[Tuple[List[str], object]],
                  sample_class: str, num_concepts: int = 4, layer_idx: int = 10,
-                 device: str | torch.device = torch.device("cuda")) -> None:
+                 device: str | torch.device = torch.device("cuda"), canonizers=None) -> None:
+        """``canonizers`` (extension, default None = the reference's composite) is passed to the
+        class composite, e.g. ``[SequentialMergeBatchNorm()]`` for the VGGish-BN models of the
+        reference's DRSA scripts (getdrsadata.py:113), whose layer 19 has d = 100."""
         self.device = torch.device(device) if isinstance(device, str) else device
         self.num_concepts = int(num_concepts)
         case = "toy" if sample_class.endswith("1") or sample_class.endswith("2") else "gtzan"
@@ -39,7 +42,7 @@ class HeatmapGenerator:
         self.class_idx = mapper[sample_class]
         self.num_classes = len(mapper)
         self.projectionmodel = ProjectionModel(model, layer_idx, U.to(self.device), self.num_concepts, case=case)
-        self.composite = get_class_composite(name_map, self.num_concepts, device=device)
+        self.composite = get_class_composite(name_map, self.num_concepts, device=device, canonizers=canonizers)
         self.info = {}
         self.info_device = {}
 
@@ -92,13 +95,14 @@ class HeatmapGenerator:
 
 
 def get_class_composite(name_map: List[Tuple[List[str], object]], num_concepts: int,
-                        device: str | torch.device = torch.device("cpu")) -> Composite:
-    """name_map + Epsilon() on (inv)projection + SubspaceHook on the filter."""
+                        device: str | torch.device = torch.device("cpu"), canonizers=None) -> Composite:
+    """name_map + Epsilon() on (inv)projection + SubspaceHook on the filter (``canonizers``:
+    extension, see HeatmapGenerator)."""
     nm = list(name_map)
     nm.append((["features.invprojection"], Epsilon()))
     nm.append((["features.subspacefilter"], SubspaceHook(num_concepts, device=device)))
     nm.append((["features.projection"], Epsilon()))
-    return NameMapComposite(name_map=nm)
+    return NameMapComposite(name_map=nm, canonizers=canonizers)
 
 
 def compute_subspace_relevances(act_vecs: torch.Tensor, ctx_vecs: torch.Tensor, U: torch.Tensor,

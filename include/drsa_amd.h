@@ -129,7 +129,9 @@ int drsa_amd_linear_bwd(const float* R, const int* seed_cls, int one_hot, const 
                         float eps_post, float* out, int M, int Nout, int Kin, void* stream);
 
 /* ProjectionModel forward (modify_model.py:75-123): h = a_vec U, a' = h U^T [, 2x2 pool].
- * h and ap may be NULL (not stored); ap is required when pool == 0 (it is the output). */
+ * h and ap may be NULL (not stored); ap is required when pool == 0 (it is the output).
+ * Any D <= 128 (VGGish layer 19: D = 100): zero-padded embedding in the kernel; for D % 4 == 0
+ * every value is the unpadded D-term chain. */
 int drsa_amd_projection_fwd(const float* a, const float* U, float* h, float* ap, float* pooled, uint8_t* amax, int B,
                             int D, int H, int W, int pool, void* stream);
 

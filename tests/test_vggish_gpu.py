@@ -12,7 +12,7 @@ import torch
 
 import drsa_ref
 import lrp_ref
-from lrp_common import logmel, spec, vggish
+from lrp_common import logmel, ortho, spec, vggish
 from drsa_audio_amd.utils.constants import LRP_NAME_MAP_VGGISH
 from drsa_audio_amd.zennit.canonizers import SequentialMergeBatchNorm
 from drsa_audio_amd.zennit.composites import NameMapComposite
@@ -79,3 +79,24 @@ def test_vggish_capture_at_wide_pool_layer(small):
                                    mode="exact", capture="features.5")
     a, r = get_intermediate(copy.deepcopy(small).to(DEV), x.to(DEV), _comp(), 5, 0)
     assert torch.equal(a.cpu(), act) and torch.equal(r.cpu(), rel)
+
+
+@pytest.mark.parametrize("layer_idx", [19, 16])
+def test_vggish_d100_heatmap_generator_bit_exact(small, layer_idx):
+    """d = 100 projection (j = 19: 2x2 pool after it; j = 16: a conv after it, a' is the stage
+    output) fanned out to K+1 = 5 clones, bit-identical to the exact oracle on the merged model."""
+    import copy
+    from drsa_audio_amd.model.modify_model import ProjectionModel
+    from drsa_audio_amd.xai.explain.explainer import HeatmapGenerator
+    U = ortho(100, 7 + layer_idx)
+    x = logmel(2, 64, 128, seed=40 + layer_idx)
+    pm = ProjectionModel(lrp_ref.merge_batch_norm(small), layer_idx, U, 4).eval()
+    ref = lrp_ref.subspace_heatmaps(pm, spec(LRP_NAME_MAP_VGGISH), 4, x, class_idx=2, mode="exact")
+    hg = HeatmapGenerator(copy.deepcopy(small).to(DEV), U, LRP_NAME_MAP_VGGISH, "disco", num_concepts=4,
+                          layer_idx=layer_idx, device="cuda", canonizers=[SequentialMergeBatchNorm()])
+    hg.generate_subspace_heatmaps(x)
+    for k in ("standard_heatmaps", "standard_relevance", "subspace_heatmaps", "subspace_relevances", "mask"):
+        assert np.array_equal(hg.info[k], ref[k]), k
+    # the K subspace heatmaps sum to the standard one (up to fp32 rounding of the sum)
+    np.testing.assert_allclose(hg.info["subspace_heatmaps"].sum(1), hg.info["standard_heatmaps"][:, 0],
+                               rtol=1e-3, atol=1e-6 * np.abs(hg.info["standard_heatmaps"]).max())
