@@ -488,21 +488,32 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
   float4 pre_x[V4T], pre_d[V4T];
   Stager<Cfg> stg;
   stg.load(a, 0, tid, ty0, tx0, bq, bs);
-  for (int chunk = 0; chunk + 1 < Cfg::NCHUNK; ++chunk) {
+  if constexpr (EPI == EPI_BWD) {
+    for (int chunk = 0; chunk + 1 < Cfg::NCHUNK; ++chunk) {
+      __syncthreads();
+      stg.store(halo, wl, tid);
+      __syncthreads();
+      stg.load(a, (chunk + 1) * CIC, tid, ty0, tx0, bq, bs);
+      if (!active || (a.dbg & 4)) continue;
+      mfma_chunk<Cfg, Cfg::PD>(halo, wl, pix_off, lane, wn, acc);
+    }
+    // last chunk, peeled: the staging registers are free, so the epilogue's first x loads go
+    // out here and their latency hides under the MFMAs (den too would spill: measured slower)
     __syncthreads();
     stg.store(halo, wl, tid);
     __syncthreads();
-    stg.load(a, (chunk + 1) * CIC, tid, ty0, tx0, bq, bs);
-    if (!active || (a.dbg & 4)) continue;
-    mfma_chunk<Cfg, Cfg::PD>(halo, wl, pix_off, lane, wn, acc);
+    epi_loads(0, 0, pre_x, pre_d, true, DRSA_CONV_PRE_D);
+    if (active && !(a.dbg & 4)) mfma_chunk<Cfg, Cfg::PD>(halo, wl, pix_off, lane, wn, acc);
+  } else {
+    for (int chunk = 0; chunk < Cfg::NCHUNK; ++chunk) {
+      __syncthreads();
+      stg.store(halo, wl, tid);
+      __syncthreads();
+      if (chunk + 1 < Cfg::NCHUNK) stg.load(a, (chunk + 1) * CIC, tid, ty0, tx0, bq, bs);
+      if (!active || (a.dbg & 4)) continue;
+      mfma_chunk<Cfg, Cfg::PD>(halo, wl, pix_off, lane, wn, acc);
+    }
   }
-  // last chunk, peeled: the staging registers are free, so the backward epilogue's first x/den
-  // loads go out here and their latency hides under the MFMAs
-  __syncthreads();
-  stg.store(halo, wl, tid);
-  __syncthreads();
-  if constexpr (EPI == EPI_BWD) epi_loads(0, 0, pre_x, pre_d, true, DRSA_CONV_PRE_D);
-  if (active && !(a.dbg & 4)) mfma_chunk<Cfg, Cfg::PD>(halo, wl, pix_off, lane, wn, acc);
 
 #pragma unroll
   for (int v = 0; v < NPW; ++v) {

@@ -184,11 +184,12 @@ __device__ __forceinline__ void stage_u_padded(float* Us, const float* __restric
   }
 }
 
-template <int DP>
+template <int DP, bool PAD>
 __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __restrict__ a, const float* __restrict__ U,
                                                             float* __restrict__ h, float* __restrict__ ap,
                                                             float* __restrict__ pooled, uint8_t* __restrict__ amax,
-                                                            int d, int H, int W, int pool) {
+                                                            int d_in, int H, int W, int pool) {
+  const int d = PAD ? d_in : DP;   // PAD = false: d == DP at compile time (no padding code)
   constexpr int P = 64, LD = DP + 1, PL = P + 4;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* Us = sm;               // [DP][LD]   U[c][j]
@@ -300,12 +301,13 @@ constexpr int PT_BWD = DRSA_PT_BWD;   // tiles per workgroup (backward)
 #define PROJ_CLONE_UNROLL 1
 #endif
 
-template <int DP>
+template <int DP, bool PAD>
 __global__ __launch_bounds__(256) void projection_bwd_kernel(
     const float* __restrict__ gp, const uint8_t* __restrict__ amax, const float* __restrict__ ap,
     const float* __restrict__ h, const float* __restrict__ a, const float* __restrict__ den,
-    const float* __restrict__ U, float* __restrict__ G, int d, int H, int W, int K, float eps_proj, float eps_den,
+    const float* __restrict__ U, float* __restrict__ G, int d_in, int H, int W, int K, float eps_proj, float eps_den,
     int sparse, int has_den, int fanout) {
+  const int d = PAD ? d_in : DP;
   constexpr int P = 64, LD = DP + 1, PL = P + 4;
   constexpr int NB = DP / 16, TILES = NB * (P / 16), QW = TILES / 4;   // 16x16 blocks; per wave
   // Per wave: pixel block pb = wave, channel blocks cb = 0..NB-1 (q = wave + 4 i).  Its h, a,
@@ -445,11 +447,12 @@ constexpr int PT_RC = DRSA_PT_RC;   // tiles per workgroup (U staged once)
 #define DRSA_PROJ_RC_WPE 3
 #endif
 
-template <int DP>
+template <int DP, bool PAD>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? DRSA_PROJ_RC_WPE : 1))) void projection_bwd_rc_kernel(
     const float* __restrict__ gp, const uint8_t* __restrict__ amax, const float* __restrict__ a,
-    const float* __restrict__ den, const float* __restrict__ U, float* __restrict__ G, int d, int H, int W, int K,
+    const float* __restrict__ den, const float* __restrict__ U, float* __restrict__ G, int d_in, int H, int W, int K,
     float eps_proj, float eps_den, int sparse, int has_den, int fanout) {
+  const int d = PAD ? d_in : DP;
   constexpr int P = 64, LD = DP + 1, PW = 16, NB = DP / 16;
   constexpr bool PF = DP <= 64;   // keep a / den of the output rows in registers
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -950,8 +953,9 @@ int drsa_amd_projection_fwd(const float* a, const float* U, float* h, float* ap,
   switch (proj_dp(D)) {
 #define PF(DD)                                                                                        \
   case DD: {                                                                                          \
-    { int rc = with_lds(projection_fwd_kernel<DD>, proj_fwd_lds<DD>()); if (rc) return rc; }                                  \
-    hipLaunchKernelGGL(projection_fwd_kernel<DD>, grid, dim3(256), proj_fwd_lds<DD>(), s, a, U, h, ap, pooled, amax, \
+    auto kf = D == DD ? projection_fwd_kernel<DD, false> : projection_fwd_kernel<DD, true>;        \
+    { int rc = with_lds(kf, proj_fwd_lds<DD>()); if (rc) return rc; }                               \
+    hipLaunchKernelGGL(kf, grid, dim3(256), proj_fwd_lds<DD>(), s, a, U, h, ap, pooled, amax,       \
                        D, H, W, pool);                                                                \
     break;                                                                                            \
   }
@@ -980,8 +984,9 @@ int drsa_amd_projection_bwd(const float* gp, const uint8_t* amax, const float* a
     switch (proj_dp(D)) {
 #define PR(DD)                                                                                        \
   case DD: {                                                                                          \
-    { int rc = with_lds(projection_bwd_rc_kernel<DD>, proj_bwd_rc_lds<DD>()); if (rc) return rc; }                                  \
-    hipLaunchKernelGGL(projection_bwd_rc_kernel<DD>, grid, dim3(256), proj_bwd_rc_lds<DD>(), s, gp, amax, a, den, U, G, \
+    auto kr = D == DD ? projection_bwd_rc_kernel<DD, false> : projection_bwd_rc_kernel<DD, true>;  \
+    { int rc = with_lds(kr, proj_bwd_rc_lds<DD>()); if (rc) return rc; }                            \
+    hipLaunchKernelGGL(kr, grid, dim3(256), proj_bwd_rc_lds<DD>(), s, gp, amax, a, den, U, G,        \
                        D, H, W, K, eps_proj, eps_den, sparse, has_den, fanout);                      \
     break;                                                                                            \
   }
@@ -998,8 +1003,9 @@ int drsa_amd_projection_bwd(const float* gp, const uint8_t* amax, const float* a
   switch (proj_dp(D)) {
 #define PB(DD)                                                                                        \
   case DD: {                                                                                          \
-    { int rc = with_lds(projection_bwd_kernel<DD>, proj_bwd_lds<DD>()); if (rc) return rc; }                                  \
-    hipLaunchKernelGGL(projection_bwd_kernel<DD>, grid, dim3(256), proj_bwd_lds<DD>(), s, gp, amax, ap, h, a, den, U, \
+    auto kb = D == DD ? projection_bwd_kernel<DD, false> : projection_bwd_kernel<DD, true>;        \
+    { int rc = with_lds(kb, proj_bwd_lds<DD>()); if (rc) return rc; }                               \
+    hipLaunchKernelGGL(kb, grid, dim3(256), proj_bwd_lds<DD>(), s, gp, amax, ap, h, a, den, U,      \
                        G, D, H, W, K, eps_proj, eps_den, sparse, has_den, fanout);                            \
     break;                                                                                            \
   }
