@@ -50,7 +50,15 @@ def _cin_pad(c: int) -> int:
 
 
 def _kind(rule) -> Optional[str]:
-    return None if rule is None else getattr(rule, "kind", type(rule).__name__)
+    k = None if rule is None else getattr(rule, "kind", type(rule).__name__)
+    # zennit Norm(stabilizer) on a conv/dense layer is Epsilon(epsilon=stabilizer): same
+    # input/output modifiers, parameters unmodified (NoMod with no keys), gradient mapper
+    # out_grad / stabilize(z) and reducer x * grad
+    return "epsilon" if k == "norm" else k
+
+
+def _eps_of(rule) -> float:
+    return float(getattr(rule, "epsilon", getattr(rule, "stabilizer", 0.0)))
 
 
 @dataclass
@@ -198,7 +206,7 @@ class LRPEngine:
                 if r_f is not None and type(r_f).__name__ != "SubspaceHook":
                     raise EngineError("engine: only SubspaceHook is supported on the subspace filter")
                 U = pm.U.detach().to(self.device, torch.float32).contiguous()
-                proj = ProjGroup(U=U, K=int(pm.num_concepts), eps_inv=r_i.epsilon, eps_proj=r_p.epsilon,
+                proj = ProjGroup(U=U, K=int(pm.num_concepts), eps_inv=_eps_of(r_i), eps_proj=_eps_of(r_p),
                                  mask=r_f is not None, pool_after=False)
                 if r_f is not None and int(r_f.num_concepts) != proj.K:
                     raise EngineError("engine: SubspaceHook num_concepts differs from the projection")
@@ -220,7 +228,7 @@ class LRPEngine:
             kind = _kind(rule)
             if kind not in (None, "epsilon", "gamma", "wsquare", "flat", "zplus"):
                 raise EngineError(f"engine: rule {type(rule).__name__} on conv features.{name} is not supported yet")
-            eps = {None: 0.0, "epsilon": getattr(rule, "epsilon", 0.0), "gamma": getattr(rule, "stabilizer", 0.0),
+            eps = {None: 0.0, "epsilon": _eps_of(rule), "gamma": getattr(rule, "stabilizer", 0.0),
                    "wsquare": getattr(rule, "stabilizer", 0.0), "flat": getattr(rule, "stabilizer", 0.0),
                    "zplus": getattr(rule, "stabilizer", 0.0)}[kind]
             st = ConvStage(name=f"features.{name}", cin=m.in_channels, cout=m.out_channels, rule_kind=kind,
@@ -263,7 +271,7 @@ class LRPEngine:
                 raise EngineError("engine: zero_params on dense layers is not supported yet")
             self.dense.append(DenseStage(name=f"classifier.{name}", W=W.contiguous(),
                                          b=None if b is None else b.contiguous(), rule_kind=kind,
-                                         eps=float(getattr(rule, "epsilon", 0.0)), relu_after=relu))
+                                         eps=_eps_of(rule) if kind else 0.0, relu_after=relu))
             i = j
         if not self.stages or not self.dense:
             raise EngineError("engine: model must have a conv trunk and a dense head")

@@ -52,4 +52,6 @@ class Gradient(Attributor):
         else:
             seed = torch.as_tensor(fn, device=out.device, dtype=out.dtype).expand_as(out).contiguous()
         relevance = self.engine.backward(seed=seed.contiguous())
-        return out, relevance
+        # the engine's output buffers are reused by its next call: hand out copies (the
+        # reference returns fresh tensors; results of consecutive calls must not alias)
+        return out.clone(), relevance.clone()

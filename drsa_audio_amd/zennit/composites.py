@@ -89,3 +89,17 @@ class SpecialFirstLayerMapComposite(LayerMapComposite):
 
     def rule_for(self, name, module):
         raise RuntimeError("SpecialFirstLayerMapComposite resolves rules per model; use .rules(model)")
+
+
+class NameLayerMapComposite(Composite):
+    """zennit NameLayerMapComposite (used at reference pf.py:219-227): a module's rule comes from
+    ``name_map`` if its name is listed there, else from ``layer_map`` (first matching type)."""
+
+    def __init__(self, name_map=None, layer_map=None, canonizers=None):
+        super().__init__(canonizers=canonizers)
+        self.name_map_composite = NameMapComposite(name_map or [])
+        self.layer_map_composite = LayerMapComposite(layer_map or [])
+
+    def rule_for(self, name: str, module: nn.Module):
+        r = self.name_map_composite.rule_for(name, module)
+        return r if r is not None else self.layer_map_composite.rule_for(name, module)

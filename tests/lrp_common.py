@@ -36,6 +36,9 @@ def spec(name_map):
             t = ("gamma", r.gamma, r.stabilizer)
         elif k in ("wsquare", "flat", "zplus"):
             t = (k, r.stabilizer)
+        elif k == "norm":
+            # zennit Norm(stabilizer) on conv/dense = Epsilon(stabilizer) (see engine/plan.py _kind)
+            t = ("epsilon", r.stabilizer)
         elif k == "pass":
             t = ("pass",)
         else:
