@@ -45,6 +45,8 @@ SIGNATURES = {
     "drsa_amd_projection_fwd": (_i32, [_fp, _fp, _fp, _fp, _fp, _vp, _i32, _i32, _i32, _i32, _i32, _vp]),
     "drsa_amd_projection_bwd": (_i32, [_fp, _vp, _fp, _fp, _fp, _fp, _fp, _fp, _i32, _i32, _i32, _i32, _i32,
                                        _f32, _f32, _i32, _vp]),
+    "drsa_amd_ab_split": (_i32, [_fp, _fp, _fp, _fp, _fp, _i32, _i32, _i64, _f32, _vp]),
+    "drsa_amd_ab_combine": (_i32, [_fp, _fp, _f32, _f32, _fp, _fp, _fp, _i32, _i32, _i64, _i32, _f32, _vp]),
     "drsa_amd_first_layer_bwd": (_i32, [_fp, _vp, _fp, _fp, _i32, _i32, _i32, _i32, _i32, _vp]),
     "drsa_amd_first_layer_den": (_i32, [_fp, _fp, _fp, _i32, _i32, _i32, _i32, _vp]),
     "drsa_amd_heatmap_sort": (_i32, [_fp, _i32, _i32, _i32, _fp, _fp, _fp, _fp, _vp, _vp]),

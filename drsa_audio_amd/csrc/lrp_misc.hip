@@ -890,6 +890,52 @@ __global__ __launch_bounds__(256) void heatmap_sort_kernel(const float* __restri
   }
 }
 
+// ===========================================================================
+// AlphaBeta (zennit 0.5.1 AlphaBeta, reference pf.py:289) on a conv with non-negative input,
+// around two plain backward convs (the x- terms vanish):
+//   split:   gp = R / stab(den_p), gn = R / stab(den_n)          (per element of the conv output;
+//            den per sample, R rows are sample*clones + clone)
+//   combine: R_in = alpha * (x J^T_{W+} gp) - beta * (x J^T_{W-} gn)   (two roundings each, no fma)
+//            then the post step of the layer below, as the conv epilogue: x > 0 ? R / stab(den) : 0
+//            (POST_DIV), x > 0 ? R : 0 (POST_MASK) or R.
+// ===========================================================================
+__global__ __launch_bounds__(256) void ab_split_kernel(const float* __restrict__ g, const float* __restrict__ dp,
+                                                       const float* __restrict__ dn, float* __restrict__ gp,
+                                                       float* __restrict__ gn, long n, int clones, long total,
+                                                       float eps) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long bq = i / n, j = i - bq * n;
+    const long o = (bq / clones) * n + j;
+    const float r = g[i];
+    gp[i] = div_nb(r, stab(dp[o], eps));
+    gn[i] = div_nb(r, stab(dn[o], eps));
+  }
+}
+
+__global__ __launch_bounds__(256) void ab_combine_kernel(const float* __restrict__ pos, const float* __restrict__ neg,
+                                                         float alpha, float beta, const float* __restrict__ x,
+                                                         const float* __restrict__ den, float* __restrict__ out,
+                                                         long n, int clones, long total, int post, float eps) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long bq = i / n, j = i - bq * n;
+    const long o = (bq / clones) * n + j;
+    const float a = alpha * pos[i];
+    const float b = beta * neg[i];
+    float R = a - b;
+    if (post != POST_NONE) {
+      const float xv = x[o];
+      if (post == POST_DIV) R = div_nb(R, stab(den[o], eps));
+      R = (xv > 0.f) ? R : 0.f;
+    }
+    out[i] = R;
+  }
+}
+
+unsigned ew_grid(long total) {
+  const long g = (total + 255) / 256;
+  return (unsigned)(g < 65536 ? (g > 0 ? g : 1) : 65536);
+}
+
 template <typename F>
 int with_lds(F* fn, size_t lds) {
   return drsa::ensure_smem((const void*)fn, lds);   // per device, thread-safe
@@ -1053,6 +1099,29 @@ int drsa_amd_heatmap_sort(const float* hm, int B, int K, int HW, float* std_out,
   DRSA_REQUIRE(HW % 4 == 0, "heatmap_sort: H*W must be a multiple of 4");
   hipLaunchKernelGGL(heatmap_sort_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, hm, K, HW, std_out, std_rel,
                      sub_out, rel, mask);
+  DRSA_LAUNCH_CHECK();
+  return DRSA_OK;
+}
+
+int drsa_amd_ab_split(const float* g, const float* den_p, const float* den_n, float* gp, float* gn, int Bq,
+                      int clones, long n, float eps, void* stream) {
+  DRSA_REQUIRE(g && den_p && den_n && gp && gn, "ab_split: null pointer");
+  DRSA_REQUIRE(Bq > 0 && clones > 0 && Bq % clones == 0 && n > 0, "ab_split: bad shape");
+  const long total = (long)Bq * n;
+  hipLaunchKernelGGL(ab_split_kernel, dim3(ew_grid(total)), dim3(256), 0, (hipStream_t)stream, g, den_p, den_n, gp, gn,
+                     n, clones, total, eps);
+  DRSA_LAUNCH_CHECK();
+  return DRSA_OK;
+}
+
+int drsa_amd_ab_combine(const float* pos, const float* neg, float alpha, float beta, const float* x, const float* den,
+                        float* out, int Bq, int clones, long n, int post, float eps, void* stream) {
+  DRSA_REQUIRE(pos && neg && out, "ab_combine: null pointer");
+  DRSA_REQUIRE(Bq > 0 && clones > 0 && Bq % clones == 0 && n > 0, "ab_combine: bad shape");
+  DRSA_REQUIRE(post == POST_NONE || (x && (den || post == POST_MASK)), "ab_combine: post needs x (and den)");
+  const long total = (long)Bq * n;
+  hipLaunchKernelGGL(ab_combine_kernel, dim3(ew_grid(total)), dim3(256), 0, (hipStream_t)stream, pos, neg, alpha,
+                     beta, x, den, out, n, clones, total, post, eps);
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;
 }

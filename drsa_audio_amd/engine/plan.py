@@ -88,7 +88,13 @@ class ConvStage:
     ng_fwd: int = 1
     wts_fwd: torch.Tensor = None
     bias3: torch.Tensor = None
-    den_kind: Optional[str] = None       # "gamma" | "eps" | "map" | None
+    den_kind: Optional[str] = None       # "gamma" | "eps" | "map" | "ab" | None
+    # AlphaBeta: second forward (W, W-) for den_n, and the two backward weight sets
+    wts_fwd_n: torch.Tensor = None
+    bias3_n: torch.Tensor = None
+    wts_bwd_n: torch.Tensor = None
+    alpha: float = 1.0
+    beta: float = 0.0
     ng_bwd: int = 1
     wts_bwd: torch.Tensor = None
     xmode_bwd: int = XM_NONE
@@ -226,11 +232,14 @@ class LRPEngine:
                     raise EngineError("engine: a ProjectionModel layer must be followed by MaxPool2d(2) or no pool")
             rule = rules.get(f"features.{name}")
             kind = _kind(rule)
-            if kind not in (None, "epsilon", "gamma", "wsquare", "flat", "zplus"):
+            if kind not in (None, "epsilon", "gamma", "wsquare", "flat", "zplus", "alphabeta"):
                 raise EngineError(f"engine: rule {type(rule).__name__} on conv features.{name} is not supported yet")
+            if kind == "alphabeta" and (not prev_nonneg or (pool and pool_k != (2, 2))):
+                raise EngineError(f"engine: AlphaBeta on features.{name} needs a non-negative input (not the first "
+                                  "conv) and a 2x2 or no max-pool after it")
             eps = {None: 0.0, "epsilon": _eps_of(rule), "gamma": getattr(rule, "stabilizer", 0.0),
                    "wsquare": getattr(rule, "stabilizer", 0.0), "flat": getattr(rule, "stabilizer", 0.0),
-                   "zplus": getattr(rule, "stabilizer", 0.0)}[kind]
+                   "zplus": getattr(rule, "stabilizer", 0.0), "alphabeta": getattr(rule, "stabilizer", 0.0)}[kind]
             st = ConvStage(name=f"features.{name}", cin=m.in_channels, cout=m.out_channels, rule_kind=kind,
                            eps=float(eps), pool=pool, proj=proj, input_nonneg=prev_nonneg, W=W, b=b, rule=rule,
                            relu_name=relu_name, pool_name=pool_name, pool_k=pool_k)
@@ -347,6 +356,21 @@ class LRPEngine:
                 st.ng_bwd, st.xmode_bwd, bsets = 1, XM_MUL, [Wp]
             else:
                 st.ng_bwd, st.xmode_bwd, bsets = 2, XM_SPLIT, [Wp, Wn]
+        elif k == "alphabeta":
+            # zennit AlphaBeta on a non-negative input (oracle lrp_ref.py alphabeta): positive set
+            # (x, W+, b+) and negative set (x, W-, b-), the x- terms vanish; den_p and den_n come
+            # from two Gamma-form forwards (den = (conv(x; W+-) + b+-) + 0)
+            Wp, Wn = W.clamp(min=0), W.clamp(max=0)
+            bias3[1, :st.cout] = bd.clamp(min=0)
+            bias3n = torch.zeros(3, cout_p, device=dev)
+            bias3n[0, :st.cout] = b
+            bias3n[1, :st.cout] = bd.clamp(max=0)
+            sets, st.ng_fwd, st.den_kind = [W, Wp], 2, "ab"
+            st.wts_fwd_n = torch.stack([fwd_layout(s_) for s_ in (W, Wn)]).contiguous()
+            st.bias3_n = bias3n.contiguous()
+            st.ng_bwd, st.xmode_bwd, bsets = 1, XM_MUL, [Wp]
+            st.wts_bwd_n = torch.stack([bwd_layout(Wn)]).contiguous()
+            st.alpha, st.beta = float(st.rule.alpha), float(st.rule.beta)
         elif k == "epsilon":
             bias3[1, :st.cout] = bd
             sets, st.ng_fwd, st.den_kind = [W], 1, "eps"
@@ -409,6 +433,8 @@ class LRPEngine:
             rec = {"in": cur, "H": h, "W": w}
             den_map = self._den_map(st, h, w) if st.den_kind == "map" else None
             need_den = st.den_kind is not None
+            if st.den_kind == "ab" and li == capture and st.pool:
+                raise EngineError("engine: capture at the ReLU of an AlphaBeta conv is not supported")
             if st.proj is None and st.pool and (li == capture or st.pool_k != (2, 2)):
                 a = self._buf((li, "a"), (B, st.cout, h, w))
                 den_full = self._buf((li, "den_full"), (B, st.cout, h, w)) if need_den else None
@@ -430,6 +456,12 @@ class LRPEngine:
                            st.bias3.data_ptr(), _capi.ptr(den_map), out.data_ptr(), amax.data_ptr(), _capi.ptr(den), B, st.cin, st.cout,
                            h, w, st.ng_fwd, 1, s)
                 rec.update(y=out, amax=amax, den=den, Hout=h // 2, Wout=w // 2)
+                if st.den_kind == "ab":   # second pass: den_n (y and argmax rewritten with the same values)
+                    den_n = self._buf((li, "den_n"), (B, st.cout, h // 2, w // 2))
+                    self._call(f"conv_fwd_n:{st.name}", "drsa_amd_conv_fwd", cur.data_ptr(), st.wts_fwd_n.data_ptr(),
+                               st.bias3_n.data_ptr(), None, out.data_ptr(), amax.data_ptr(), den_n.data_ptr(), B, st.cin,
+                               st.cout, h, w, 2, 1, s)
+                    rec.update(den_n=den_n)
                 cur, h, w = out, h // 2, w // 2
             else:
                 a = self._buf((li, "a"), (B, st.cout, h, w))
@@ -438,6 +470,12 @@ class LRPEngine:
                            st.bias3.data_ptr(), _capi.ptr(den_map), a.data_ptr(), None, _capi.ptr(den), B, st.cin, st.cout, h, w,
                            st.ng_fwd, 0, s)
                 rec.update(a=a, den=den)
+                if st.den_kind == "ab":
+                    den_n = self._buf((li, "den_n"), (B, st.cout, h, w))
+                    self._call(f"conv_fwd_n:{st.name}", "drsa_amd_conv_fwd", cur.data_ptr(), st.wts_fwd_n.data_ptr(),
+                               st.bias3_n.data_ptr(), None, a.data_ptr(), None, den_n.data_ptr(), B, st.cin, st.cout, h, w,
+                               2, 0, s)
+                    rec.update(den_n=den_n)
                 if st.proj is not None:
                     P = st.proj
                     # h and a' are recomputed by projection_bwd from a (no HBM round trip); a' is
@@ -487,7 +525,7 @@ class LRPEngine:
         rec = self.last["stages"][li]
         if st.proj is not None:
             return POST_NONE, None, 0.0
-        if st.den_kind is None:
+        if st.den_kind is None or st.den_kind == "ab":
             return POST_MASK, None, 0.0
         return POST_DIV, rec["den"], st.eps
 
@@ -550,7 +588,8 @@ class LRPEngine:
                 fan = fanout and P.mask
                 nq = (K + 1) if fan else 1
                 G = self._buf((li, "G"), (B * nq, st.cout, h, w))
-                post, den, eps = (POST_DIV, rec["den"], st.eps) if st.den_kind is not None else (POST_MASK, None, 0.0)
+                post, den, eps = ((POST_DIV, rec["den"], st.eps) if st.den_kind not in (None, "ab")
+                                  else (POST_MASK, None, 0.0))
                 if not P.mask:
                     raise EngineError("engine: projection without SubspaceHook is not supported yet")
                 self._call("projection_bwd", "drsa_amd_projection_bwd", g.data_ptr(), _capi.ptr(rec["amax"] if P.pool_after else None),
@@ -578,6 +617,23 @@ class LRPEngine:
                 out = self._buf((li, "R"), (Bq, 1, h, w))
                 self._call(f"first_layer_bwd:{st.name}", "drsa_amd_first_layer_bwd", g.data_ptr(), _capi.ptr(amax_in), st.w2_first.data_ptr(),
                            out.data_ptr(), Bq, clones, st.cout, h, w, s)
+            elif st.den_kind == "ab":
+                # R (ReLU-masked) at the conv output -> gp, gn -> two backward convs -> combine + post
+                n_out = g.numel() // Bq
+                gp = self._buf((li, "ab_gp"), tuple(g.shape))
+                gn = self._buf((li, "ab_gn"), tuple(g.shape))
+                self._call(f"ab_split:{st.name}", "drsa_amd_ab_split", g.data_ptr(), rec["den"].data_ptr(),
+                           rec["den_n"].data_ptr(), gp.data_ptr(), gn.data_ptr(), Bq, clones, n_out, float(st.eps), s)
+                pos = self._buf((li, "ab_pos"), (Bq, st.cin, h, w))
+                neg = self._buf((li, "ab_neg"), (Bq, st.cin, h, w))
+                for gg, wts, dst in ((gp, st.wts_bwd, pos), (gn, st.wts_bwd_n, neg)):
+                    self._call(f"conv_bwd:{st.name}", "drsa_amd_conv_bwd", gg.data_ptr(), _capi.ptr(amax_in),
+                               wts.data_ptr(), x_in.data_ptr(), None, dst.data_ptr(), Bq, clones, st.cout, st.cin, h, w,
+                               1, XM_MUL, POST_NONE, 0.0, s)
+                out = self._buf((li, "R"), (Bq, st.cin, h, w))
+                self._call(f"ab_combine:{st.name}", "drsa_amd_ab_combine", pos.data_ptr(), neg.data_ptr(), st.alpha,
+                           st.beta, x_in.data_ptr() if post != POST_NONE else None, _capi.ptr(den), out.data_ptr(), Bq,
+                           clones, st.cin * h * w, post, float(eps), s)
             else:
                 out = self._buf((li, "R"), (Bq, st.cin, h, w))
                 self._call(f"conv_bwd:{st.name}", "drsa_amd_conv_bwd", g.data_ptr(), _capi.ptr(amax_in), st.wts_bwd.data_ptr(),

@@ -145,6 +145,16 @@ int drsa_amd_projection_bwd(const float* gp, const uint8_t* amax, const float* a
                             const float* den, const float* U, float* G, int B, int D, int H, int W, int K,
                             float eps_proj, float eps_den, int fanout, void* stream);
 
+/* AlphaBeta on a conv with non-negative input (zennit AlphaBeta as configured at pf.py:285-289,
+ * restated in oracle/lrp_ref.py): split R at the conv output into gp = R / stab(den_p) and
+ * gn = R / stab(den_n) (den per sample, R rows = sample*clones + clone, n elements per row) ... */
+int drsa_amd_ab_split(const float* g, const float* den_p, const float* den_n, float* gp, float* gn, int Bq,
+                      int clones, long n, float eps, void* stream);
+/* ... and after the two backward convs pos = x J^T_{W+} gp, neg = x J^T_{W-} gn:
+ * R_in = alpha*pos - beta*neg, then the post step of the layer below (post as conv_bwd). */
+int drsa_amd_ab_combine(const float* pos, const float* neg, float alpha, float beta, const float* x, const float* den,
+                        float* out, int Bq, int clones, long n, int post, float eps, void* stream);
+
 /* First-layer (one input channel) WSquare / Flat backward: R = J^T_{W2} g. */
 int drsa_amd_first_layer_bwd(const float* g, const uint8_t* amax, const float* w2, float* out, int Bq, int clones,
                              int C, int H, int W, void* stream);

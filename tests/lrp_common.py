@@ -39,6 +39,8 @@ def spec(name_map):
         elif k == "norm":
             # zennit Norm(stabilizer) on conv/dense = Epsilon(stabilizer) (see engine/plan.py _kind)
             t = ("epsilon", r.stabilizer)
+        elif k == "alphabeta":
+            t = ("alphabeta", r.alpha, r.beta, r.stabilizer)
         elif k == "pass":
             t = ("pass",)
         else:

@@ -215,13 +215,35 @@ def test_zplus_rule_bit_exact(net):
         assert np.array_equal(hg9.info[k], ref9[k]), k
 
 
-def test_alphabeta_refused_loudly(net):
-    """AlphaBeta is restated in the oracle only; the engine must refuse it, not fall back."""
+def test_alphabeta_rule_bit_exact(net):
+    """AlphaBeta (reference pf.py:285-289) on the post-ReLU convs, also inside
+    the ProjectionModel layer (j = 10, K+1 clones through it): two Gamma-form forwards for
+    den_p / den_n, split -> two backward convs -> alpha*pos - beta*neg, bit-exact vs the oracle."""
+    from drsa_audio_amd.zennit.rules import AlphaBeta
+    nm = [(["features.0"], WSquare(stabilizer=1e-7)), (["features.3", "features.6"], AlphaBeta(alpha=2.0, beta=1.0)),
+          (["features.9"], AlphaBeta(alpha=1.0, beta=0.0, stabilizer=1e-7)),
+          (["features.12"], Gamma(gamma=0.2, stabilizer=1e-7)),
+          (["classifier.0", "classifier.3", "classifier.6"], Epsilon(epsilon=1e-7))]
+    x = logmel(2, seed=31)
+    _, R = _exact(net, nm, x, class_idx=6)
+    Rg = compute_relevances(_gpu_model(net), x.to(DEV), NameMapComposite(nm), class_idx=6)
+    assert torch.equal(Rg.cpu(), R)
+    pm = ProjectionModel(net, 10, u64(), 4).eval()
+    ref = lrp_ref.subspace_heatmaps(pm, spec(nm), 4, x, class_idx=6, mode="exact")
+    hg = HeatmapGenerator(_gpu_model(net), u64(), nm, "rock", num_concepts=4, layer_idx=10, device="cuda")
+    hg.generate_subspace_heatmaps(x)
+    for k in ("standard_heatmaps", "subspace_heatmaps", "mask"):
+        assert np.array_equal(hg.info[k], ref[k]), k
+
+
+def test_alphabeta_refused_where_unsupported(net):
+    """AlphaBeta on the signed-input first conv or on a dense layer is refused loudly (no fallback)."""
     from drsa_audio_amd.engine.plan import EngineError
     from drsa_audio_amd.zennit.rules import AlphaBeta
-    nm = [(["features.3"], AlphaBeta(alpha=2.0, beta=1.0)), (["classifier.0"], Epsilon(epsilon=1e-7))]
-    with pytest.raises(EngineError):
-        compute_relevances(_gpu_model(net), logmel(1, seed=3).to(DEV), NameMapComposite(nm), class_idx=0)
+    for nm in ([(["features.0"], AlphaBeta(alpha=2.0, beta=1.0))],
+               [(["features.3"], Gamma(gamma=0.2)), (["classifier.0"], AlphaBeta(alpha=2.0, beta=1.0))]):
+        with pytest.raises(EngineError):
+            compute_relevances(_gpu_model(net), logmel(1, seed=3).to(DEV), NameMapComposite(nm), class_idx=0)
 
 
 def test_gradient_attributor_with_tensor_output_relevance(net):

@@ -33,6 +33,8 @@ def _spec_rule(r):
         return (k, r.stabilizer)
     if k == "pass":
         return ("pass",)
+    if k == "alphabeta":
+        return ("alphabeta", r.alpha, r.beta, r.stabilizer)
     raise ValueError(k)
 
 
@@ -51,6 +53,7 @@ def _check_order(order_dev, R, ps):
 CONFIGS = [
     {"convolutional": ("gamma", 0.25), "dense": ("epsilon", 1e-7), "first_layer": ("wsquare",)},
     {"convolutional": ("zplus",), "dense": ("norm",), "first_layer": ("flat",)},
+    {"convolutional": ("alphabeta", 2.0), "dense": ("epsilon", 1e-7), "first_layer": ("wsquare",)},
     {"convolutional": ("epsilon", 1e-6), "dense": ("epsilon", 1e-7), "first_layer": ("wsquare",),
      "name_map": [(["features.3"], Gamma(gamma=0.5, stabilizer=1e-7))]},
 ]
