@@ -488,7 +488,7 @@ __global__ __launch_bounds__(fin_threads<polar_dim<DP>()>()) void drsa_finish_ke
     const float v = ip < d ? rv : ((jp == pad_col(ip - d, K, dk, DKP)) ? 1.f : 0.f);
     if (e < PD * PD) X[ip * LD + jp] = v;
   }
-  const int it = polar_ns<PD>(X, T, red, scr, tol, max_iter);
+  const int it = polar_run<PD>(X, T, red, scr, tol, max_iter);
   for (int e = tid; e < d * d; e += NT) {
     const int i = e / d, j = e % d;
     U_out[e] = X[i * LD + (j / dk) * DKP + j % dk];
@@ -518,7 +518,7 @@ __global__ __launch_bounds__(fin_threads<DP>()) void polar_kernel(const float* _
     const float v = keep_or_zero(V[real ? (size_t)i * d + j : 0], real);
     if (e < DP * DP) X[i * LD + j] = (i < d && j < d) ? v : (i == j ? 1.f : 0.f);
   }
-  const int it = polar_ns<DP>(X, T, red, scr, tol, max_iter);
+  const int it = polar_run<DP>(X, T, red, scr, tol, max_iter);
   for (int e = threadIdx.x; e < d * d; e += NT) U_out[e] = X[(e / d) * LD + e % d];
   if (iters_out && threadIdx.x == 0) *iters_out = it;
 }

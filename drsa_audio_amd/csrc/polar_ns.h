@@ -7,6 +7,9 @@
 #pragma once
 #include "common.h"
 
+#ifndef DRSA_NS16
+#define DRSA_NS16 1
+#endif
 #ifndef DRSA_NS_STAMP
 #define DRSA_NS_STAMP(slot)
 #endif
@@ -204,6 +207,104 @@ __device__ int polar_ns(float* X, float* T, float* red, float* scr, float tol, i
   }
   __syncthreads();
   return it;
+}
+
+// DP <= 64: the same iteration on 16x16x4 MFMA tiles, one output tile per wave (no k-split, so no
+// LDS scratch round trip and no extra barrier per product).  16x16 D layout: lane l, reg r ->
+// row 4(l>>4) + r, col l&15; A/B operands: lane l holds k = k0 + (l>>4), row/col l&15.
+template <int DP>
+__device__ int polar_ns16(float* X, float* T, float* red, float tol, int max_iter) {
+  constexpr int NT = fin_threads<DP>(), LD = ns_ld<DP>(), NB = DP / 16, NWV = NT / 64;
+  constexpr int NSYM = NB * (NB + 1) / 2, NFULL = NB * NB;
+  constexpr int TPR = NT / DP;
+  static_assert(DP == 32 || DP == 64, "polar_ns16: DP 32 or 64");
+  static_assert(NFULL <= NWV && NSYM <= NWV, "one tile per wave");
+  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int lo = lane & 15, hi = lane >> 4;
+  int sib = 0, sjb = 0;            // this wave's upper-triangle tile of P
+  {
+    int rem = w;
+    while (sib < NB && rem >= NB - sib) { rem -= NB - sib; ++sib; }
+    sjb = sib + rem;
+  }
+  const int fib = w / NB, fjb = w % NB;   // this wave's tile of X T
+  auto put_p = [&](int it, int row, int col, float v, float& err) {
+    if (it > 0) {
+      const bool dg = row == col;
+      err = fmaxf(err, fabsf(v - (dg ? 1.f : 0.f)));
+      v = (dg ? 1.5f : 0.f) - 0.5f * v;
+    }
+    T[row * LD + col] = v;
+    if (row / 16 != col / 16) T[col * LD + row] = v;
+  };
+  int it = 0;
+  float err_prev = 1.f;
+  for (;; ++it) {
+    __syncthreads();   // X complete
+    DRSA_NS_STAMP(4 * it + 0);
+    float err = 0.f;
+    if (w < NSYM) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k0 = 0; k0 < DP; k0 += 4) {
+        const int k = k0 + hi;
+        acc = mfma16(X[k * LD + 16 * sib + lo], X[k * LD + 16 * sjb + lo], acc);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) put_p(it, 16 * sib + 4 * hi + r, 16 * sjb + lo, acc[r], err);
+    }
+    if (it == 0) {
+      __syncthreads();
+      DRSA_NS_STAMP(4 * it + 1);
+      float tr = 0.f;
+      for (int i = lane; i < DP; i += 64) tr += T[i * LD + i];
+      for (int m = 32; m >= 1; m >>= 1) tr += shfl_xor(tr, m);
+      const int row = tid / TPR, part = tid % TPR;
+      float rs = 0.f;
+      for (int c = part; c < DP; c += TPR) rs += fabsf(T[row * LD + c]);
+      for (int m = 1; m < TPR; m <<= 1) rs += shfl_xor(rs, m);
+      const float rowmax = block_max<NT>(rs, red);
+      float a2 = (float)DP / tr;
+      if (a2 * rowmax >= 2.9f) a2 = 1.f / rowmax;
+      const float a = sqrtf(a2);
+      for (int e = tid; e < DP * DP; e += NT) {
+        const int r = e / DP, c = e % DP;
+        X[r * LD + c] *= a;
+        const float pv = T[r * LD + c] * a2;
+        err = fmaxf(err, fabsf(pv - (r == c ? 1.f : 0.f)));
+        T[r * LD + c] = (r == c ? 1.5f : 0.f) - 0.5f * pv;
+      }
+    }
+    err = block_max1<NT>(err, red + 32 + 16 * (it & 1));
+    DRSA_NS_STAMP(4 * it + 2);
+    if (err < tol || it >= max_iter) break;
+    const bool last = (float)DP * err < 1e-4f || (it > 0 && err_prev < 1e-4f && err > 0.25f * err_prev);
+    err_prev = err;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (w < NFULL) {
+#pragma unroll
+      for (int k0 = 0; k0 < DP; k0 += 4) {
+        const int k = k0 + hi;
+        acc = mfma16(X[(16 * fib + lo) * LD + k], T[k * LD + 16 * fjb + lo], acc);
+      }
+    }
+    __syncthreads();   // every read of X done
+    DRSA_NS_STAMP(4 * it + 3);
+    if (w < NFULL) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) X[(16 * fib + 4 * hi + r) * LD + 16 * fjb + lo] = acc[r];
+    }
+    if (last) { ++it; break; }
+  }
+  __syncthreads();
+  return it;
+}
+
+// the production polar: 16x16 tiles below DP = 128, 32x32 (k-split where needed) otherwise
+template <int DP>
+__device__ int polar_run(float* X, float* T, float* red, float* scr, float tol, int max_iter) {
+  if constexpr (DP <= 64 && DRSA_NS16) return polar_ns16<DP>(X, T, red, tol, max_iter);
+  else return polar_ns<DP>(X, T, red, scr, tol, max_iter);
 }
 
 }  // namespace

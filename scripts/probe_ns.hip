@@ -19,7 +19,7 @@ __global__ __launch_bounds__(fin_threads<DP>()) void probe_kernel(const float* V
   __syncthreads();
   float* X = smem; float* T = X + DP * LD; float* red = T + DP * LD; float* scr = red + 64;
   for (int e = threadIdx.x; e < DP * DP; e += NT) X[(e / DP) * LD + e % DP] = V[e];
-  int it = polar_ns<DP>(X, T, red, scr, 4e-7f, 40);
+  int it = polar_run<DP>(X, T, red, scr, 4e-7f, 40);
   for (int e = threadIdx.x; e < DP * DP; e += NT) U[e] = X[(e / DP) * LD + e % DP];
   if (threadIdx.x == 0) { *iters = it; st[198] = wall_clock64(); }
 }
@@ -45,7 +45,18 @@ void run() {
     float ms; hipEventElapsedTime(&ms, e0, e1);
     unsigned long long h[200]; int hit;
     hipMemcpy(h, st, 200 * 8, hipMemcpyDeviceToHost); hipMemcpy(&hit, it, 4, hipMemcpyDeviceToHost);
-    printf("DP=%d rep %d: event %.2f us, iters %d, kernel ticks %llu\n", DP, rep, ms * 1e3, hit, h[198] - h[199]);
+    float* hU = (float*)malloc(DP * DP * 4);
+    hipMemcpy(hU, U, DP * DP * 4, hipMemcpyDeviceToHost);
+    double orth = 0;
+    for (int i = 0; i < DP; ++i)
+      for (int j = 0; j < DP; ++j) {
+        double acc = 0;
+        for (int k = 0; k < DP; ++k) acc += (double)hU[k * DP + i] * hU[k * DP + j];
+        orth = fmax(orth, fabs(acc - (i == j ? 1.0 : 0.0)));
+      }
+    free(hU);
+    printf("DP=%d rep %d: event %.2f us, iters %d, kernel ticks %llu, max|U^T U - I| %.2e\n", DP, rep, ms * 1e3, hit,
+           h[198] - h[199], orth);
     unsigned long long prev = h[199];
     for (int s = 0; s < 4 * (hit + 1) && s < 196; ++s) {
       if (!h[s]) continue;
