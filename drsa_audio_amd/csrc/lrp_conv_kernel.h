@@ -38,6 +38,9 @@
 #ifndef DRSA_CONV_PRE_D
 #define DRSA_CONV_PRE_D 0
 #endif
+#ifndef DRSA_CONV_PRE_N
+#define DRSA_CONV_PRE_N 64
+#endif
 #ifndef DRSA_CONV_BWDC_WPE
 #define DRSA_CONV_BWDC_WPE 2
 #endif
@@ -453,6 +456,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
   auto gch = [&](int cl, int v) { return ((cl >> 5) * NPW + v) * 32 + (cl & 31); };   // global channel
   // global channel of staged row cl in pass sub (ES = 2 implies WN = 1)
   auto gchs = [&](int cl, int v, int sub) { return ES == 1 ? gch(cl, v) : v * 32 + sub * TCH + cl; };
+  Stager<Cfg> stg;
+  stg.load(a, 0, tid, ty0, tx0, bq, bs);
+  // backward: all chunks but the last here, the last one peeled below (after the epilogue
+  // addressing is set up, so that none of it is live across the loop)
+  for (int chunk = 0; chunk + (EPI == EPI_BWD ? 1 : 0) < Cfg::NCHUNK; ++chunk) {
+    __syncthreads();
+    stg.store(halo, wl, tid);
+    __syncthreads();
+    if (chunk + 1 < Cfg::NCHUNK) stg.load(a, (chunk + 1) * CIC, tid, ty0, tx0, bq, bs);
+    if (!active || (a.dbg & 4)) continue;
+    mfma_chunk<Cfg, Cfg::PD>(halo, wl, pix_off, lane, wn, acc);
+  }
   constexpr int Q = TH * TW / 4, CS = kThreads / Q;
   static_assert(kThreads % Q == 0, "float4 groups per tile must divide the block");
   const int cl0 = tid / Q, rem = tid % Q;
@@ -474,9 +489,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
   const float* dsrc = (ds && post_div) ? ds : xsrc;
   const float eps = a.eps;
   // epilogue x/den loads of (n-tile v, pass sub); (0, 0) is issued before the last chunk's MFMAs
-  auto epi_loads = [&](int v, int sub, float4 (&xk)[V4T], float4 (&dk)[V4T], bool lx = true, bool ld = true) {
+  auto epi_loads = [&](int v, int sub, float4 (&xk)[V4T], float4 (&dk)[V4T], bool lx = true, bool ld = true,
+                       int i0 = 0, int i1 = -1) {
+    if (i1 < 0) i1 = V4T;
 #pragma unroll
-    for (int it = 0; it < V4T; ++it) {
+    for (int it = i0; it < i1; ++it) {
       const int cl = cl0 + it * CS;
       const int co = gchs(cl, v, sub);
       const bool ok = cl < TCH && co < a.cout;
@@ -485,34 +502,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
       if (ld) dk[it] = *reinterpret_cast<const float4*>(dsrc + (size_t)coc * HW);
     }
   };
+  // x groups prefetched before the last chunk's MFMAs (all of them spill a few registers)
+  constexpr int kPreN = DRSA_CONV_PRE_N < V4T ? DRSA_CONV_PRE_N : V4T;
   float4 pre_x[V4T], pre_d[V4T];
-  Stager<Cfg> stg;
-  stg.load(a, 0, tid, ty0, tx0, bq, bs);
   if constexpr (EPI == EPI_BWD) {
-    for (int chunk = 0; chunk + 1 < Cfg::NCHUNK; ++chunk) {
-      __syncthreads();
-      stg.store(halo, wl, tid);
-      __syncthreads();
-      stg.load(a, (chunk + 1) * CIC, tid, ty0, tx0, bq, bs);
-      if (!active || (a.dbg & 4)) continue;
-      mfma_chunk<Cfg, Cfg::PD>(halo, wl, pix_off, lane, wn, acc);
-    }
     // last chunk, peeled: the staging registers are free, so the epilogue's first x loads go
     // out here and their latency hides under the MFMAs (den too would spill: measured slower)
     __syncthreads();
     stg.store(halo, wl, tid);
     __syncthreads();
-    epi_loads(0, 0, pre_x, pre_d, true, DRSA_CONV_PRE_D);
+    epi_loads(0, 0, pre_x, pre_d, true, DRSA_CONV_PRE_D, 0, kPreN);
     if (active && !(a.dbg & 4)) mfma_chunk<Cfg, Cfg::PD>(halo, wl, pix_off, lane, wn, acc);
-  } else {
-    for (int chunk = 0; chunk < Cfg::NCHUNK; ++chunk) {
-      __syncthreads();
-      stg.store(halo, wl, tid);
-      __syncthreads();
-      if (chunk + 1 < Cfg::NCHUNK) stg.load(a, (chunk + 1) * CIC, tid, ty0, tx0, bq, bs);
-      if (!active || (a.dbg & 4)) continue;
-      mfma_chunk<Cfg, Cfg::PD>(halo, wl, pix_off, lane, wn, acc);
-    }
   }
 
 #pragma unroll
@@ -660,7 +660,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
       float4 Rk[V4T], xk[V4T], dk[V4T];
       if (v == 0 && sub == 0) {
 #pragma unroll
-        for (int it = 0; it < V4T; ++it) xk[it] = pre_x[it];
+        for (int it = 0; it < kPreN; ++it) xk[it] = pre_x[it];
+        epi_loads(v, sub, xk, dk, true, false, kPreN, V4T);
         if (DRSA_CONV_PRE_D) {
 #pragma unroll
           for (int it = 0; it < V4T; ++it) dk[it] = pre_d[it];
