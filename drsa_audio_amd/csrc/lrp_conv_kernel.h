@@ -52,6 +52,9 @@ namespace drsa_conv {
 
 constexpr int kThreads = 256;
 
+// bias3 of a forward call without bias ([3][COUT], COUT <= 128)
+__device__ const float g_zero_bias3[3 * 128] = {};
+
 template <int V, int M>
 constexpr int round_up() { return (V + M - 1) / M * M; }
 
@@ -518,10 +521,23 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
 #pragma unroll
   for (int v = 0; v < NPW; ++v) {
     if constexpr (EPI == EPI_FWD_POOL || EPI == EPI_FWD_RELU) {
+      // the lane's 16 channels' biases, loaded unconditionally (bias3 is [3][COUT]; a missing bias
+      // reads a zero table) and all issued before any use: a branch around each load had put
+      // every one of them in its own basic block behind its own wait
+      const float* bb = a.bias ? a.bias : g_zero_bias3;
+      float b0[16], b1[16], b2[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = gch(wn * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, v);
+        const bool cok = co < a.cout;
+        const float x0 = bb[co], x1 = bb[COUT + co], x2 = bb[2 * COUT + co];
+        b0[r] = cok ? x0 : 0.f;
+        b1[r] = cok ? x1 : 0.f;
+        b2[r] = cok ? x2 : 0.f;
+      }
       // pass 0: y = relu(z)
       stage(v, [&](int u, int r) {
-        const int co = gch(wn * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, v);
-        const float z = acc[0][u][v][r] + ((a.bias && co < a.cout) ? a.bias[co] : 0.f);
+        const float z = acc[0][u][v][r] + b0[r];
         float y = z > 0.f ? z : 0.f;
         if (z != z) y = z;   // relu(NaN) = NaN (torch semantics)
         return y;
@@ -604,18 +620,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
       } else if (a.out_den) {
         // pass 1: the rule's denominator
         stage(v, [&](int u, int r) {
-          const int co = gch(wn * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, v);
-          const bool cok = co < a.cout;
           if constexpr (NG >= 2) {
-            const float bp = (a.bias && cok) ? a.bias[COUT + co] : 0.f;
-            const float bn = (a.bias && cok) ? a.bias[2 * COUT + co] : 0.f;
-            const float z0 = acc[1][u][v][r] + bp;
-            float z1 = bn;
-            if constexpr (NG == 3) z1 = acc[2][u][v][r] + bn;
+            const float z0 = acc[1][u][v][r] + b1[r];
+            float z1 = b2[r];
+            if constexpr (NG == 3) z1 = acc[2][u][v][r] + b2[r];
             return z0 + z1;
           }
           // Epsilon: den = conv(x; W) + b_den (b_den = b, or 0 under zero_params=['bias'])
-          return acc[0][u][v][r] + ((a.bias && cok) ? a.bias[COUT + co] : 0.f);
+          return acc[0][u][v][r] + b1[r];
         });
         if constexpr (EPI == EPI_FWD_POOL) {
           const int H2 = H >> 1, W2 = W >> 1;

@@ -691,12 +691,16 @@ constexpr int FQ_Y = 16, FQ_X = 64, FQ_C = DRSA_FQ_C;
 constexpr int FQ_RY = FQ_Y + 2, FQ_RX = FQ_X + 2;            // cells incl. halo
 constexpr int FQ_PY = 2 * FQ_RY, FQ_PX = 2 * FQ_RX + 4;      // pixel image (row pad 4)
 constexpr int FQ_KR = (FQ_RY + 3) / 4;                       // row passes of 4 waves
+// image column of the halo origin: 3 puts every thread's 6-pixel window (starting at 4tx + 4) on
+// a 16-byte boundary, so a row of it is one ds_read_b128 + one ds_read_b64 over consecutive lanes
+// (bank-conflict free; the former origin 1 gave 8-byte reads at a 16-byte lane stride)
+constexpr int FQ_C0 = 3;
 constexpr int FQ_NS = FQ_C * FQ_KR + 1;                      // staged cells per thread
 
 typedef float fq2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ void fq_put(float* img, int ci, int ry, int rx, float v, int sb) {
-  float* d = img + (ci * FQ_PY + 2 * ry) * FQ_PX + 2 * rx + 1;
+  float* d = img + (ci * FQ_PY + 2 * ry) * FQ_PX + 2 * rx + FQ_C0;
   d[0] = sb == 0 ? v : 0.f;
   d[1] = sb == 1 ? v : 0.f;
   d[FQ_PX] = sb == 2 ? v : 0.f;
@@ -775,18 +779,20 @@ __global__ __launch_bounds__(256) void first_layer_bwd_pooled_kernel(const float
       float wv[9];
 #pragma unroll
       for (int t = 0; t < 9; ++t) wv[t] = (c < C) ? w2[c * 9 + t] : 0.f;
-      // patch P[i][j] = pixel (2qy0 + 4ty - 1 + i, 2qx0 + 4tx - 1 + j) = img[4ty + 1 + i][4tx + 2 + j];
+      // patch P[i][j] = pixel (2qy0 + 4ty - 1 + i, 2qx0 + 4tx - 1 + j) = img[4ty + 1 + i][4tx + FQ_C0 + 1 + j];
       // pair q (q = 0..4) = (P[i][q], P[i][q + 1])
       fq2 pr[6][5];
-      const float* base = img + (ci * FQ_PY + 4 * ty + 1) * FQ_PX + 4 * tx + 2;
+      const float* base = img + (ci * FQ_PY + 4 * ty + 1) * FQ_PX + 4 * tx + FQ_C0 + 1;
 #pragma unroll
       for (int i = 0; i < 6; ++i) {
         const float* r = base + i * FQ_PX;
-        pr[i][0] = *reinterpret_cast<const fq2*>(r);
-        pr[i][2] = *reinterpret_cast<const fq2*>(r + 2);
-        pr[i][4] = *reinterpret_cast<const fq2*>(r + 4);
-        pr[i][1] = fq2{r[1], r[2]};
-        pr[i][3] = fq2{r[3], r[4]};
+        const float4 q4 = *reinterpret_cast<const float4*>(r);
+        const fq2 q2 = *reinterpret_cast<const fq2*>(r + 4);
+        pr[i][0] = fq2{q4.x, q4.y};
+        pr[i][1] = fq2{q4.y, q4.z};
+        pr[i][2] = fq2{q4.z, q4.w};
+        pr[i][3] = fq2{q4.w, q2.x};
+        pr[i][4] = q2;
       }
 #pragma unroll
       for (int py = 0; py < 4; ++py)
