@@ -372,10 +372,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N > 1 path on a one-GPU box (tests only): every rank on cuda:0, gloo
+    if os.environ.get("DRSA_BENCH_ONE_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("DRSA_BENCH_BACKEND", "nccl")   # nccl = RCCL on ROCm
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
