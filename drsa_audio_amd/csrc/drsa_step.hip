@@ -117,7 +117,10 @@ constexpr int partial_threads() { return PCfg<DP, DKP>::NT; }
 // Workgroup g owns row blocks [rb0, rb1) (16 rows each), staged RT rows at a time into LDS by
 // all threads (the next tile is prefetched into registers while the current one is computed);
 // wave w owns column group w % CG and the tile's row blocks w / CG, w / CG + NW / CG, ...
-template <int DP, int DKP, bool BF>
+// VEC (d % 4 == 0): float4 row loads.  A compile-time choice: a runtime branch per prefetch slot
+// made the compiler wait for every outstanding load at each join, which serialised the slots and
+// defeated the prefetch of the next tile.
+template <int DP, int DKP, bool BF, bool VEC>
 __global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_kernel(
     const void* __restrict__ A_, const void* __restrict__ C_, int64_t N, int d, int K, int dk,
     const float* __restrict__ U, float* __restrict__ partials, int64_t rb_total) {
@@ -135,7 +138,6 @@ __global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_ker
   const float* C = reinterpret_cast<const float*>(C_);
   const uint16_t* Ab = reinterpret_cast<const uint16_t*>(A_);
   const uint16_t* Cb = reinterpret_cast<const uint16_t*>(C_);
-  const bool vec = (d & 3) == 0;
 
   const int64_t rb0 = (int64_t)blockIdx.x * rb_total / gridDim.x;
   const int64_t rb1 = (int64_t)(blockIdx.x + 1) * rb_total / gridDim.x;
@@ -158,7 +160,7 @@ __global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_ker
       const size_t off = ok ? (size_t)(r0 + row) * d + col : 0;
       float4 a, c;
       if constexpr (BF) {   // 4 bf16 -> 4 fp32 (exact)
-        if (vec) {
+        if constexpr (VEC) {
           const uint2 ua = *reinterpret_cast<const uint2*>(Ab + off);
           const uint2 uc = *reinterpret_cast<const uint2*>(Cb + off);
           a = make_float4(__uint_as_float(ua.x << 16), __uint_as_float(ua.x & 0xffff0000u),
@@ -178,7 +180,7 @@ __global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_ker
           c = make_float4(vc[0], vc[1], vc[2], vc[3]);
         }
       } else {
-        if (vec) {
+        if constexpr (VEC) {
           a = *reinterpret_cast<const float4*>(A + off);
           c = *reinterpret_cast<const float4*>(C + off);
         } else {
@@ -543,9 +545,10 @@ template <int DP, int DKP, bool BF>
 int launch_partial(const void* A, const void* C, int64_t N, const Geom& g, const float* U, float* partials,
                    const PartialPlan& pl, hipStream_t s) {
   using Cfg = PCfg<DP, DKP>;
-  DRSA_SMEM((drsa_partial_kernel<DP, DKP, BF>), Cfg::lds_bytes);
-  hipLaunchKernelGGL((drsa_partial_kernel<DP, DKP, BF>), dim3(pl.grid), dim3(Cfg::NT), Cfg::lds_bytes, s, A, C,
-                     N, g.d, g.K, g.dk, U, partials, pl.rb_total);
+  auto kern = (g.d & 3) == 0 ? drsa_partial_kernel<DP, DKP, BF, true> : drsa_partial_kernel<DP, DKP, BF, false>;
+  DRSA_SMEM(kern, Cfg::lds_bytes);
+  hipLaunchKernelGGL(kern, dim3(pl.grid), dim3(Cfg::NT), Cfg::lds_bytes, s, A, C, N, g.d, g.K, g.dk, U, partials,
+                     pl.rb_total);
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;
 }
