@@ -297,11 +297,22 @@ def drsa_joint_bench(device, steps=200):
         out16 = drsa_run_joint(probs16, steps)
         torch.cuda.synchronize(device)
         dt16 = time.perf_counter() - t0
+        # fp16 inputs + fp16 MFMA projection (C5 "fp16 MFMA projection")
+        probsh = [(A.to(torch.float16), C.to(torch.float16), U0, K_) for A, C, U0, K_ in probs]
+        drsa_run_joint(probsh, 4)
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        outh = drsa_run_joint(probsh, steps)
+        torch.cuda.synchronize(device)
+        dth = time.perf_counter() - t0
     flop = 2 * 8.0 * N * d * d
     rel16 = max(abs(float(a[1][-1]) - float(b[1][-1])) / abs(float(b[1][-1])) for a, b in zip(out16, out))
+    relh = max(abs(float(a[1][-1]) - float(b[1][-1])) / abs(float(b[1][-1])) for a, b in zip(outh, out))
     return {"config": "C5 joint: 2 problems (VGGish j=26, j=33) x N=20000, d=128, K=16, one graph",
             "ms_per_joint_step": dt / steps * 1e3, "ms_per_step_sequential_runs": dt_seq / steps * 1e3,
             "bf16": {"ms_per_joint_step": dt16 / steps * 1e3, "objective_rel_diff_vs_fp32_after_steps": rel16,
+                     "tolerance": 1e-2},
+            "fp16": {"ms_per_joint_step": dth / steps * 1e3, "objective_rel_diff_vs_fp32_after_steps": relh,
                      "tolerance": 1e-2},
             "vector_steps_per_s": 2 * N * steps / dt, "tflops_algorithmic": flop * steps / dt / 1e12,
             "objective_final": [float(t[-1]) for _, t in out]}

@@ -80,6 +80,12 @@ __device__ __forceinline__ f32x4 mfma16_bf16(u16x8 a, u16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
                                                  0, 0, 0);
 }
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+// the same layout on v_mfma_f32_16x16x32_f16 (fp16 bit patterns)
+__device__ __forceinline__ f32x4 mfma16_f16(u16x8 a, u16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c,
+                                                0, 0, 0);
+}
 
 // zennit Stabilizer: t + eps * (sign(t) + [t == 0]).  sign(t) + [t == 0] is exactly +1 for
 // t >= 0 (including -0), -1 for t < 0, and 0 for NaN (where t + 0 = NaN = t - eps), so the

@@ -107,12 +107,35 @@ struct PCfg {
   static constexpr size_t lds_bytes = (tile_floats > red_floats ? tile_floats : red_floats) * sizeof(float);
 };
 
+// 16-bit A/C element (DT 1 bf16, DT 2 fp16 bit patterns) -> fp32 (exact), fp32 that came from
+// such an element -> its bits (exact), and fp32 -> 16-bit with round-to-nearest-even (U)
+template <int DT>
+__device__ __forceinline__ float wid16(uint32_t b) {
+  if constexpr (DT == 1) return __uint_as_float(b << 16);
+  else return (float)__builtin_bit_cast(_Float16, (uint16_t)b);
+}
+template <int DT>
+__device__ __forceinline__ uint16_t nar16(float v) {
+  if constexpr (DT == 1) return (uint16_t)(__float_as_uint(v) >> 16);
+  else return __builtin_bit_cast(uint16_t, (_Float16)v);
+}
+template <int DT>
+__device__ __forceinline__ uint16_t rne16(float v) {
+  if constexpr (DT == 1) {
+    const uint32_t u = __float_as_uint(v);
+    return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+  } else {
+    return __builtin_bit_cast(uint16_t, (_Float16)v);   // v_cvt_f16_f32: RNE
+  }
+}
+
 template <int DP, int DKP>
 constexpr int partial_threads() { return PCfg<DP, DKP>::NT; }
 
-// BF: A and C are bf16 in HBM (C5: "bf16 MFMA projection with fp32 accumulate"); GEMM1
-// (XA = A U, XC = C U) runs on v_mfma_f32_16x16x32_bf16 with U rounded to bf16 (RNE) once per
-// launch; everything after it (relu, S, the gradient GEMM on the exactly widened A/C, slab) is fp32.
+// DT 1 / 2: A and C are bf16 / fp16 in HBM (C5: "bf16 CNN ... fp16 MFMA projection", fp32
+// accumulate); GEMM1 (XA = A U, XC = C U) runs on v_mfma_f32_16x16x32_{bf16,f16} with U rounded
+// to the 16-bit type (RNE) once per launch; everything after it (relu, S, the gradient GEMM on the
+// exactly widened A/C, slab) is fp32.  DT 0: fp32 throughout.
 //
 // Workgroup g owns row blocks [rb0, rb1) (16 rows each), staged RT rows at a time into LDS by
 // all threads (the next tile is prefetched into registers while the current one is computed);
@@ -120,11 +143,12 @@ constexpr int partial_threads() { return PCfg<DP, DKP>::NT; }
 // VEC (d % 4 == 0): float4 row loads.  A compile-time choice: a runtime branch per prefetch slot
 // made the compiler wait for every outstanding load at each join, which serialised the slots and
 // defeated the prefetch of the next tile.
-template <int DP, int DKP, bool BF, bool VEC>
+template <int DP, int DKP, int DT, bool VEC>
 __global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_kernel(
     const void* __restrict__ A_, const void* __restrict__ C_, int64_t N, int d, int K, int dk,
     const float* __restrict__ U, float* __restrict__ partials, int64_t rb_total) {
   using Cfg = PCfg<DP, DKP>;
+  constexpr bool BF = DT != 0;   // 16-bit A/C (bf16 or fp16)
   constexpr int CW = Cfg::CW, CG = Cfg::CG, NCB = Cfg::NCB, NIB = Cfg::NIB, NW = Cfg::NW, NT = Cfg::NT;
   constexpr int KP = Cfg::KP, RT = Cfg::RT, LDA = Cfg::LDA, NV = Cfg::NV, PFN = Cfg::PFN;
   constexpr int WPG = NW / CG, NQ = DP / 16, NQ2 = DP / 32 > 0 ? DP / 32 : 1;
@@ -159,22 +183,22 @@ __global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_ker
       const bool ok = i < NV && r0 + row < rmax && col < d;
       const size_t off = ok ? (size_t)(r0 + row) * d + col : 0;
       float4 a, c;
-      if constexpr (BF) {   // 4 bf16 -> 4 fp32 (exact)
+      if constexpr (BF) {   // 4 x 16-bit -> 4 fp32 (exact)
         if constexpr (VEC) {
           const uint2 ua = *reinterpret_cast<const uint2*>(Ab + off);
           const uint2 uc = *reinterpret_cast<const uint2*>(Cb + off);
-          a = make_float4(__uint_as_float(ua.x << 16), __uint_as_float(ua.x & 0xffff0000u),
-                          __uint_as_float(ua.y << 16), __uint_as_float(ua.y & 0xffff0000u));
-          c = make_float4(__uint_as_float(uc.x << 16), __uint_as_float(uc.x & 0xffff0000u),
-                          __uint_as_float(uc.y << 16), __uint_as_float(uc.y & 0xffff0000u));
+          a = make_float4(wid16<DT>(ua.x & 0xffffu), wid16<DT>(ua.x >> 16), wid16<DT>(ua.y & 0xffffu),
+                          wid16<DT>(ua.y >> 16));
+          c = make_float4(wid16<DT>(uc.x & 0xffffu), wid16<DT>(uc.x >> 16), wid16<DT>(uc.y & 0xffffu),
+                          wid16<DT>(uc.y >> 16));
         } else {
           float va[4], vc[4];
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const size_t o = (ok && col + u < d) ? off + u : 0;
             const uint32_t xa = Ab[o], xc = Cb[o];
-            va[u] = keep_or_zero(__uint_as_float(xa << 16), col + u < d);
-            vc[u] = keep_or_zero(__uint_as_float(xc << 16), col + u < d);
+            va[u] = keep_or_zero(wid16<DT>(xa), col + u < d);
+            vc[u] = keep_or_zero(wid16<DT>(xc), col + u < d);
           }
           a = make_float4(va[0], va[1], va[2], va[3]);
           c = make_float4(vc[0], vc[1], vc[2], vc[3]);
@@ -245,8 +269,7 @@ __global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_ker
         for (int jj = 0; jj < 8; ++jj) {
           const int k = 32 * q2 + 8 * lg + jj;
           const float v = U[(size_t)(k < d ? k : 0) * d + j];
-          const uint32_t u = __float_as_uint(keep_or_zero(v, real && k < d));
-          ubf[cb][q2][jj] = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+          ubf[cb][q2][jj] = rne16<DT>(keep_or_zero(v, real && k < d));
         }
     }
   }
@@ -298,19 +321,20 @@ __global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_ker
           const float* pc8 = Cr + l15 * LDA + 32 * q2 + 8 * lg;
           const float4 a0 = *reinterpret_cast<const float4*>(pa8), a1 = *reinterpret_cast<const float4*>(pa8 + 4);
           const float4 c0 = *reinterpret_cast<const float4*>(pc8), c1 = *reinterpret_cast<const float4*>(pc8 + 4);
-          u16x8 ab, cbv;   // widened bf16 values: the top 16 bits are exact
-          ab[0] = __float_as_uint(a0.x) >> 16; ab[1] = __float_as_uint(a0.y) >> 16;
-          ab[2] = __float_as_uint(a0.z) >> 16; ab[3] = __float_as_uint(a0.w) >> 16;
-          ab[4] = __float_as_uint(a1.x) >> 16; ab[5] = __float_as_uint(a1.y) >> 16;
-          ab[6] = __float_as_uint(a1.z) >> 16; ab[7] = __float_as_uint(a1.w) >> 16;
-          cbv[0] = __float_as_uint(c0.x) >> 16; cbv[1] = __float_as_uint(c0.y) >> 16;
-          cbv[2] = __float_as_uint(c0.z) >> 16; cbv[3] = __float_as_uint(c0.w) >> 16;
-          cbv[4] = __float_as_uint(c1.x) >> 16; cbv[5] = __float_as_uint(c1.y) >> 16;
-          cbv[6] = __float_as_uint(c1.z) >> 16; cbv[7] = __float_as_uint(c1.w) >> 16;
+          u16x8 ab, cbv;   // the widened 16-bit values narrow back exactly
+          ab[0] = nar16<DT>(a0.x); ab[1] = nar16<DT>(a0.y); ab[2] = nar16<DT>(a0.z); ab[3] = nar16<DT>(a0.w);
+          ab[4] = nar16<DT>(a1.x); ab[5] = nar16<DT>(a1.y); ab[6] = nar16<DT>(a1.z); ab[7] = nar16<DT>(a1.w);
+          cbv[0] = nar16<DT>(c0.x); cbv[1] = nar16<DT>(c0.y); cbv[2] = nar16<DT>(c0.z); cbv[3] = nar16<DT>(c0.w);
+          cbv[4] = nar16<DT>(c1.x); cbv[5] = nar16<DT>(c1.y); cbv[6] = nar16<DT>(c1.z); cbv[7] = nar16<DT>(c1.w);
 #pragma unroll
           for (int cb = 0; cb < NCB; ++cb) {
-            xa[cb] = mfma16_bf16(ab, ubf[cb][q2], xa[cb]);
-            xc[cb] = mfma16_bf16(cbv, ubf[cb][q2], xc[cb]);
+            if constexpr (DT == 1) {
+              xa[cb] = mfma16_bf16(ab, ubf[cb][q2], xa[cb]);
+              xc[cb] = mfma16_bf16(cbv, ubf[cb][q2], xc[cb]);
+            } else {
+              xa[cb] = mfma16_f16(ab, ubf[cb][q2], xa[cb]);
+              xc[cb] = mfma16_f16(cbv, ubf[cb][q2], xc[cb]);
+            }
           }
         }
       }
@@ -541,11 +565,11 @@ PartialPlan plan_partial(int64_t N) {
   return {(int)grid, rbt};
 }
 
-template <int DP, int DKP, bool BF>
+template <int DP, int DKP, int DT>
 int launch_partial(const void* A, const void* C, int64_t N, const Geom& g, const float* U, float* partials,
                    const PartialPlan& pl, hipStream_t s) {
   using Cfg = PCfg<DP, DKP>;
-  auto kern = (g.d & 3) == 0 ? drsa_partial_kernel<DP, DKP, BF, true> : drsa_partial_kernel<DP, DKP, BF, false>;
+  auto kern = (g.d & 3) == 0 ? drsa_partial_kernel<DP, DKP, DT, true> : drsa_partial_kernel<DP, DKP, DT, false>;
   DRSA_SMEM(kern, Cfg::lds_bytes);
   hipLaunchKernelGGL(kern, dim3(pl.grid), dim3(Cfg::NT), Cfg::lds_bytes, s, A, C, N, g.d, g.K, g.dk, U, partials,
                      pl.rb_total);
@@ -553,17 +577,17 @@ int launch_partial(const void* A, const void* C, int64_t N, const Geom& g, const
   return DRSA_OK;
 }
 
-template <int DP, bool BF>
+template <int DP, int DT>
 int dispatch_partial_dp(const void* A, const void* C, int64_t N, const Geom& g, const float* U, float* partials,
                         const PartialPlan& pl, hipStream_t s) {
   switch (g.DKp) {
-    case 1: return launch_partial<DP, 1, BF>(A, C, N, g, U, partials, pl, s);
-    case 2: return launch_partial<DP, 2, BF>(A, C, N, g, U, partials, pl, s);
-    case 4: return launch_partial<DP, 4, BF>(A, C, N, g, U, partials, pl, s);
-    case 8: return launch_partial<DP, 8, BF>(A, C, N, g, U, partials, pl, s);
-    case 16: return launch_partial<DP, 16, BF>(A, C, N, g, U, partials, pl, s);
-    case 32: if constexpr (DP >= 32) return launch_partial<DP, 32, BF>(A, C, N, g, U, partials, pl, s); break;
-    case 64: if constexpr (DP >= 64) return launch_partial<DP, 64, BF>(A, C, N, g, U, partials, pl, s); break;
+    case 1: return launch_partial<DP, 1, DT>(A, C, N, g, U, partials, pl, s);
+    case 2: return launch_partial<DP, 2, DT>(A, C, N, g, U, partials, pl, s);
+    case 4: return launch_partial<DP, 4, DT>(A, C, N, g, U, partials, pl, s);
+    case 8: return launch_partial<DP, 8, DT>(A, C, N, g, U, partials, pl, s);
+    case 16: return launch_partial<DP, 16, DT>(A, C, N, g, U, partials, pl, s);
+    case 32: if constexpr (DP >= 32) return launch_partial<DP, 32, DT>(A, C, N, g, U, partials, pl, s); break;
+    case 64: if constexpr (DP >= 64) return launch_partial<DP, 64, DT>(A, C, N, g, U, partials, pl, s); break;
     default: break;
   }
   drsa::set_error("drsa_partial: unsupported d=%d K=%d", g.d, g.K);
@@ -571,19 +595,22 @@ int dispatch_partial_dp(const void* A, const void* C, int64_t N, const Geom& g, 
 }
 
 int dispatch_partial(const void* A, const void* C, int64_t N, const Geom& g, const float* U, float* partials,
-                     const PartialPlan& pl, hipStream_t s, bool bf) {
+                     const PartialPlan& pl, hipStream_t s, int dt) {
   switch (g.DP) {
     case 16:
-      if (bf) break;
-      return dispatch_partial_dp<16, false>(A, C, N, g, U, partials, pl, s);
-    case 32: return bf ? dispatch_partial_dp<32, true>(A, C, N, g, U, partials, pl, s)
-                       : dispatch_partial_dp<32, false>(A, C, N, g, U, partials, pl, s);
-    case 64: return bf ? dispatch_partial_dp<64, true>(A, C, N, g, U, partials, pl, s)
-                       : dispatch_partial_dp<64, false>(A, C, N, g, U, partials, pl, s);
-    case 128: return bf ? dispatch_partial_dp<128, true>(A, C, N, g, U, partials, pl, s)
-                        : dispatch_partial_dp<128, false>(A, C, N, g, U, partials, pl, s);
+      if (dt) break;
+      return dispatch_partial_dp<16, 0>(A, C, N, g, U, partials, pl, s);
+    case 32: return dt == 1 ? dispatch_partial_dp<32, 1>(A, C, N, g, U, partials, pl, s)
+                  : dt == 2 ? dispatch_partial_dp<32, 2>(A, C, N, g, U, partials, pl, s)
+                            : dispatch_partial_dp<32, 0>(A, C, N, g, U, partials, pl, s);
+    case 64: return dt == 1 ? dispatch_partial_dp<64, 1>(A, C, N, g, U, partials, pl, s)
+                  : dt == 2 ? dispatch_partial_dp<64, 2>(A, C, N, g, U, partials, pl, s)
+                            : dispatch_partial_dp<64, 0>(A, C, N, g, U, partials, pl, s);
+    case 128: return dt == 1 ? dispatch_partial_dp<128, 1>(A, C, N, g, U, partials, pl, s)
+                   : dt == 2 ? dispatch_partial_dp<128, 2>(A, C, N, g, U, partials, pl, s)
+                             : dispatch_partial_dp<128, 0>(A, C, N, g, U, partials, pl, s);
   }
-  drsa::set_error("drsa_partial: unsupported d=%d K=%d%s", g.d, g.K, bf ? " (bf16)" : "");
+  drsa::set_error("drsa_partial: unsupported d=%d K=%d%s", g.d, g.K, dt == 1 ? " (bf16)" : dt == 2 ? " (fp16)" : "");
   return DRSA_EUNSUPPORTED;
 }
 
@@ -625,7 +652,8 @@ int partial_impl(const void* A, const void* C, int64_t N, int d, int K, const fl
   DRSA_REQUIRE(g.ok, "drsa_partial: unsupported d=%d K=%d (need d <= 128, K | d, padded concept width <= 64 and "
                "K * padded width <= 128)", d, K);
   DRSA_REQUIRE(N >= 0, "drsa_partial: N < 0");
-  DRSA_REQUIRE(dtype == 0 || (dtype == 1 && g.DP >= 32), "drsa_partial: bf16 needs a padded d >= 32");
+  DRSA_REQUIRE(dtype == 0 || ((dtype == 1 || dtype == 2) && g.DP >= 32),
+               "drsa_partial: dtype must be 0 (fp32) or 1/2 (bf16/fp16, padded d >= 32)");
   DRSA_REQUIRE(A && C && U && gs_out, "drsa_partial: null pointer");
   hipStream_t s = (hipStream_t)stream;
   const size_t E = slab_floats(g);
@@ -637,7 +665,7 @@ int partial_impl(const void* A, const void* C, int64_t N, int d, int K, const fl
   DRSA_REQUIRE(((uintptr_t)A % 16) == 0 && ((uintptr_t)C % 16) == 0, "drsa_partial: A/C must be 16B aligned");
   const PartialPlan pl = plan_partial(N);
   float* partials = (float*)ws;
-  int rc = dispatch_partial(A, C, N, g, U, partials, pl, s, dtype == 1);
+  int rc = dispatch_partial(A, C, N, g, U, partials, pl, s, dtype);
   if (rc) return rc;
   const size_t ES = slab_stride(g);
   hipLaunchKernelGGL(drsa_reduce_kernel, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, s, partials, pl.grid, (int)E,
@@ -676,6 +704,11 @@ int drsa_amd_drsa_partial(const float* A, const float* C, int64_t N, int d, int 
 int drsa_amd_drsa_partial_bf16(const uint16_t* A, const uint16_t* C, int64_t N, int d, int K, const float* U,
                                float* gs_out, void* ws, size_t ws_size, void* stream) {
   return partial_impl(A, C, N, d, K, U, gs_out, ws, ws_size, stream, 1);
+}
+
+int drsa_amd_drsa_partial_f16(const uint16_t* A, const uint16_t* C, int64_t N, int d, int K, const float* U,
+                              float* gs_out, void* ws, size_t ws_size, void* stream) {
+  return partial_impl(A, C, N, d, K, U, gs_out, ws, ws_size, stream, 2);
 }
 
 int drsa_amd_drsa_finish(const float* gs, int64_t N_total, int d, int K, const float* U, float* U_out,
@@ -791,8 +824,8 @@ int drsa_amd_drsa_run_multi(int P, const drsa_amd_problem_t* probs, int steps, i
     DRSA_REQUIRE(q.N > 0 && q.A && q.C && q.U_io && q.U_tmp && q.f_traj && q.counter && q.ws,
                  "drsa_run_multi: problem %d has null pointers or N <= 0", p);
     DRSA_REQUIRE(q.ws_size >= ws_bytes(q.N, g), "drsa_run_multi: problem %d workspace too small", p);
-    DRSA_REQUIRE(q.dtype == 0 || (q.dtype == 1 && g.DP >= 32), "drsa_run_multi: problem %d: dtype must be 0 (fp32) "
-                 "or 1 (bf16, padded d >= 32)", p);
+    DRSA_REQUIRE(q.dtype == 0 || ((q.dtype == 1 || q.dtype == 2) && g.DP >= 32),
+                 "drsa_run_multi: problem %d: dtype must be 0 (fp32) or 1/2 (bf16/fp16, padded d >= 32)", p);
   }
   bool all_f32 = true;
   for (int p = 0; p < P; ++p) all_f32 = all_f32 && probs[p].dtype == 0;

@@ -74,7 +74,7 @@ class DrsaWorkspace:
 
 
 def _check_problem(A: torch.Tensor, C: torch.Tensor, U: torch.Tensor, K: int):
-    dt = torch.bfloat16 if A.dtype == torch.bfloat16 else torch.float32
+    dt = A.dtype if A.dtype in (torch.bfloat16, torch.float16) else torch.float32
     _capi.require_gpu(A, "activation_vecs", dtype=dt)
     _capi.require_gpu(C, "context_vecs", dtype=dt)
     _capi.require_gpu(U, "U")
@@ -111,10 +111,10 @@ def drsa_step(A, C, U, K, ws: Optional[DrsaWorkspace] = None):
 
 def drsa_run(A, C, U0, K: int, steps: int, ws: Optional[DrsaWorkspace] = None,
              use_graph: bool = True):
-    """S steps natively. Returns (U_S, trajectory tensor [S+1] on device).  bf16 A, C take the
-    bf16-MFMA projection path (drsa_run_joint)."""
+    """S steps natively. Returns (U_S, trajectory tensor [S+1] on device).  bf16 / fp16 A, C take
+    the 16-bit MFMA projection path (drsa_run_joint)."""
     _check_problem(A, C, U0, K)
-    if A.dtype == torch.bfloat16:
+    if A.dtype in (torch.bfloat16, torch.float16):
         return drsa_run_joint([(A, C, U0, K)], steps, use_graph)[0]
     N, d = A.shape
     ws = ws or DrsaWorkspace(N, d, K, A.device)
@@ -133,8 +133,8 @@ def drsa_run_joint(problems, steps: int, use_graph: bool = True):
     """Several independent DRSA problems advanced together (C5: the same model's layers j=26 and
     j=33, K=16 each; the reference optimises them one after another, optsubspaces.py:18-23).
 
-    ``problems``: list of (A, C, U0, K) on one device; A, C fp32, or bf16 (C5: the U-projection
-    GEMM then runs on bf16 MFMA with fp32 accumulation).  One hipGraph holds every problem's step
+    ``problems``: list of (A, C, U0, K) on one device; A, C fp32, or bf16 / fp16 (C5: the
+    U-projection GEMM then runs on bf16 / fp16 MFMA with fp32 accumulation).  One hipGraph holds every problem's step
     on its own forked stream (drsa_amd_drsa_run_multi).  Returns [(U_S, trajectory [S+1])]."""
     import ctypes
     if not problems:
@@ -154,7 +154,7 @@ def drsa_run_joint(problems, steps: int, use_graph: bool = True):
         outs.append((U, traj))
         structs.append(_capi.DrsaProblem(A.data_ptr(), C.data_ptr(), N, d, int(K), U.data_ptr(), U_tmp.data_ptr(),
                                          traj.data_ptr(), ws.counter.data_ptr(), ws.ptr, ws.nbytes,
-                                         1 if A.dtype == torch.bfloat16 else 0))
+                                         {torch.bfloat16: 1, torch.float16: 2}.get(A.dtype, 0)))
     arr = (_capi.DrsaProblem * len(structs))(*structs)
     stream = torch.cuda.current_stream(dev)
     graph = bool(use_graph) and stream.cuda_stream != 0

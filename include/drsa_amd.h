@@ -182,7 +182,8 @@ typedef struct drsa_amd_problem {
   int* counter;
   void* ws;
   size_t ws_size;
-  int dtype; /* 0: A, C fp32; 1: A, C bf16 (uint16 bit patterns), GEMM1 on bf16 MFMA, d >= 32 */
+  int dtype; /* 0: A, C fp32; 1 / 2: A, C bf16 / fp16 (uint16 bit patterns), GEMM1 on bf16 / fp16
+              * MFMA with fp32 accumulation, padded d >= 32 */
 } drsa_amd_problem_t;
 
 /* drsa_amd_drsa_partial with A, C stored as bf16 (C5: bf16 input; the U-projection GEMM runs on
@@ -190,6 +191,10 @@ typedef struct drsa_amd_problem {
  * reduction stay fp32).  No reference bf16 path exists: its tolerance is looser (tests). */
 int drsa_amd_drsa_partial_bf16(const uint16_t* A, const uint16_t* C, int64_t N, int d, int K, const float* U,
                                float* gs_out, void* ws, size_t ws_size, void* stream);
+/* The same with A, C as fp16 (C5's "fp16 MFMA projection": v_mfma_f32_16x16x32_f16, U rounded to
+ * fp16 once per launch, fp32 accumulate; everything after GEMM1 fp32). */
+int drsa_amd_drsa_partial_f16(const uint16_t* A, const uint16_t* C, int64_t N, int d, int K, const float* U,
+                              float* gs_out, void* ws, size_t ws_size, void* stream);
 
 /* P independent problems advanced S steps together (C5: two layers, K=16 each, one graph).
  * Replaces the sequential per-layer loop of optsubspaces.py:18-23 / drsa.main. */

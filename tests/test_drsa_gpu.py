@@ -214,24 +214,28 @@ def test_joint_run_equals_separate_runs_bitwise():
 
 
 @pytest.mark.parametrize("N,d,K", [(3000, 64, 4), (2048, 128, 16), (777, 32, 2), (20000, 64, 8)])
-def test_bf16_partial_matches_bf16_closed_form(N, d, K):
-    """bf16 path (C5): the kernel against the float64 closed form ON THE SAME bf16 inputs (tight:
-    1e-5 relative) — checks the bf16 MFMA operand layout and the widening, not the rounding."""
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+def test_bf16_partial_matches_bf16_closed_form(N, d, K, dt):
+    """16-bit paths (C5: bf16 / fp16 MFMA projection): the kernel against the float64 closed form
+    ON THE SAME 16-bit inputs (tight: 2e-5 relative) — checks the MFMA operand layout and the
+    widening, not the rounding."""
     from drsa_audio_amd.xai.drsa.drsa import DrsaWorkspace
     from drsa_audio_amd import _capi
+    rnd = drsa_ref.bf16_round if dt == "bf16" else drsa_ref.f16_round
+    tdt = torch.bfloat16 if dt == "bf16" else torch.float16
     A, C = drsa_inputs(N, d, 7000 + N)
-    Ab, Cb = drsa_ref.bf16_round(A), drsa_ref.bf16_round(C)
+    Ab, Cb = rnd(A), rnd(C)
     U0 = _u0(d, d + K)
-    At = torch.from_numpy(Ab).to(DEV).to(torch.bfloat16)
-    Ct = torch.from_numpy(Cb).to(DEV).to(torch.bfloat16)
+    At = torch.from_numpy(Ab).to(DEV).to(tdt)
+    Ct = torch.from_numpy(Cb).to(DEV).to(tdt)
     Ut = torch.from_numpy(U0).to(DEV)
     ws = DrsaWorkspace(N, d, K, DEV)
     gs = torch.empty(d * d + K, device=DEV)
-    _capi.call("drsa_amd_drsa_partial_bf16", At.data_ptr(), Ct.data_ptr(), N, d, K, Ut.data_ptr(), gs.data_ptr(),
+    _capi.call(f"drsa_amd_drsa_partial_{dt}", At.data_ptr(), Ct.data_ptr(), N, d, K, Ut.data_ptr(), gs.data_ptr(),
                ws.ptr, ws.nbytes, _capi.stream_ptr(DEV))
     torch.cuda.synchronize()
-    f_ref, G_ref = drsa_ref.closed_form_bf16(Ab, Cb, U0, K)
-    Ud = drsa_ref.bf16_round(U0).astype(np.float64)
+    f_ref, G_ref = drsa_ref.closed_form_bf16(Ab, Cb, U0, K, rounder=rnd)
+    Ud = rnd(U0).astype(np.float64)
     XA, XC = Ab.astype(np.float64) @ Ud, Cb.astype(np.float64) @ Ud
     r = np.maximum((XA * XC).reshape(N, K, d // K).sum(-1), 0)
     S_ref = (r * r).sum(0)
@@ -244,9 +248,11 @@ def test_bf16_partial_matches_bf16_closed_form(N, d, K):
     assert np.abs(Gk - Gt).max() <= 2e-5 * np.abs(Gt).max()
 
 
-def test_bf16_joint_run_objective_within_loosened_tolerance():
-    """C5 bf16 vs the fp32 path on the same (unrounded) data: the DRSA objective trajectory stays
-    within 1e-2 relative (loosened tolerance for a path the reference does not have)."""
+@pytest.mark.parametrize("tdt", [torch.bfloat16, torch.float16])
+def test_bf16_joint_run_objective_within_loosened_tolerance(tdt):
+    """C5 bf16 / fp16 vs the fp32 path on the same (unrounded) data: the DRSA objective
+    trajectory stays within 1e-2 relative (loosened tolerance for a path the reference does not
+    have)."""
     from drsa_audio_amd.xai.drsa.drsa import drsa_run, drsa_run_joint
     probs32, probs16 = [], []
     for N, seed in ((4000, 26), (3000, 33)):
@@ -254,7 +260,7 @@ def test_bf16_joint_run_objective_within_loosened_tolerance():
         U0 = _u0(128, seed)
         A32, C32, U = _gpu(A, C, U0)
         probs32.append((A32, C32, U, 16))
-        probs16.append((A32.to(torch.bfloat16), C32.to(torch.bfloat16), U, 16))
+        probs16.append((A32.to(tdt), C32.to(tdt), U, 16))
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
         j16 = drsa_run_joint(probs16, 20)
