@@ -319,26 +319,42 @@ def drsa_joint_bench(device, steps=200):
 
 
 def vggish_lrp_bench(device, B=32, iters=5):
-    """C5 model: standard LRP (compute_relevances) on VGGish-BN, 128x256 log-mel, fp32."""
+    """C5 model: VGGish-BN, 128x256 log-mel.  Standard LRP (compute_relevances), the engine forward
+    alone, and the C5 CNN leg (DRSA data capture at j = 26: forward + relevance backward to the
+    layer), each on the fp32 plan and on the bf16 plan (model.bfloat16(): conv forwards on
+    v_mfma_f32_32x32x16_bf16, relevance backward fp32; parity tests/test_bf16_gpu.py)."""
+    import copy
+    from drsa_audio_amd.engine import get_engine
     from drsa_audio_amd.model.create_model import VGGType
     from drsa_audio_amd.utils.constants import LRP_NAME_MAP_VGGISH
     from drsa_audio_amd.zennit.canonizers import SequentialMergeBatchNorm
     from drsa_audio_amd.zennit.composites import NameMapComposite
     from drsa_audio_amd.xai.explain.attribute import compute_relevances
+    from drsa_audio_amd.xai.drsa.preprocessing import get_intermediate
     torch.manual_seed(0)
-    m = VGGType(n_filters=(64, 64, 100, 128, 128), n_dense=100, pool_kernels=((2, 4),) + ((2, 2),) * 4, dropout=0.3,
-                input_size=(128, 256), conv_bn=True, dense_bn=True).eval().to(device)
+    m32 = VGGType(n_filters=(64, 64, 100, 128, 128), n_dense=100, pool_kernels=((2, 4),) + ((2, 2),) * 4, dropout=0.3,
+                  input_size=(128, 256), conv_bn=True, dense_bn=True).eval().to(device)
     comp = NameMapComposite(LRP_NAME_MAP_VGGISH, canonizers=[SequentialMergeBatchNorm()])
-    x = synthetic_logmel(B, 128, 256, seed=5, device=device)
-    for _ in range(2):
-        compute_relevances(m, x, comp, class_idx=1)
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    for _ in range(iters):
-        compute_relevances(m, x, comp, class_idx=1)
-    torch.cuda.synchronize(device)
-    return {"config": f"VGGish-BN (64,64,100,128,128), block_depth 2, 128x256, B={B}, standard LRP fp32",
-            "samples_per_s": B * iters / (time.perf_counter() - t0)}
+    x32 = synthetic_logmel(B, 128, 256, seed=5, device=device)
+
+    def timed(fn):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize(device)
+        return B * iters / (time.perf_counter() - t0)
+
+    out = {"config": f"VGGish-BN (64,64,100,128,128), block_depth 2, 128x256, B={B}; samples/s"}
+    for prec, m, x in (("fp32", m32, x32), ("bf16", copy.deepcopy(m32).bfloat16(), x32.bfloat16())):
+        eng = get_engine(m, comp)
+        out[prec] = {"standard_lrp": timed(lambda: compute_relevances(m, x, comp, class_idx=1)),
+                     "forward": timed(lambda: eng.forward(x)),
+                     "capture_j26": timed(lambda: get_intermediate(m, x, comp, 26, 1))}
+    out["samples_per_s"] = out["fp32"]["standard_lrp"]
+    return out
 
 
 def drsa_sharded_bench(device, world, rank, steps=100):

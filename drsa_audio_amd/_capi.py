@@ -38,6 +38,9 @@ SIGNATURES = {
     "drsa_amd_subspace_relevances": (_i32, [_fp, _fp, _i64, _i64, _i32, _i32, _fp, _fp, _vp, _sz, _vp]),
     "drsa_amd_conv_weight_floats": (_sz, [_i32, _i32, _i32]),
     "drsa_amd_conv_fwd": (_i32, [_fp, _fp, _fp, _fp, _fp, _vp, _fp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
+    "drsa_amd_conv_weight_bf16_elems": (_sz, [_i32, _i32, _i32]),
+    "drsa_amd_conv_fwd_bf16": (_i32, [_fp, _vp, _fp, _fp, _fp, _vp, _fp, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
+                                      _vp]),
     "drsa_amd_conv_bwd": (_i32, [_fp, _vp, _fp, _fp, _fp, _fp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
                                  _i32, _f32, _vp]),
     "drsa_amd_linear_fwd": (_i32, [_fp, _fp, _fp, _fp, _fp, _i32, _i32, _i32, _vp]),

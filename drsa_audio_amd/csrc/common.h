@@ -80,6 +80,19 @@ __device__ __forceinline__ f32x4 mfma16_bf16(u16x8 a, u16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
                                                  0, 0, 0);
 }
+// bf16-input MFMA, 32x32x16 (gfx950), fp32 accumulate.
+//   A operand: lane l holds A[i = l&31][k = 8(l>>5) + j], j < 8;  B: B[k = 8(l>>5) + j][col = l&31]
+//   C/D:       as mfma32
+__device__ __forceinline__ f32x16 mfma32_bf16(u16x8 a, u16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
+                                                 0, 0, 0);
+}
+// two floats -> packed bf16x2 (round to nearest even; v_cvt_pk_bf16_f32)
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  const bf16x2_t p = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(uint32_t, p);
+}
 typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
 // the same layout on v_mfma_f32_16x16x32_f16 (fp16 bit patterns)
 __device__ __forceinline__ f32x4 mfma16_f16(u16x8 a, u16x8 b, f32x4 c) {

@@ -10,7 +10,7 @@
 // ---------------------------------------------------------------------------
 namespace drsa_conv {
 extern const Table kTableFwdA, kTableFwdB, kTableFwdC, kTableFwdD, kTableFwdE, kTableBwdA, kTableBwdB, kTableBwdC,
-    kTableBwdcA, kTableBwdcB;
+    kTableBwdcA, kTableBwdcB, kTableFwdBfA, kTableFwdBfB, kTableFwdBfC;
 }
 
 namespace {
@@ -20,7 +20,8 @@ using namespace drsa_conv;
 const drsa_conv::Table* kTables[] = {&drsa_conv::kTableFwdA, &drsa_conv::kTableFwdB, &drsa_conv::kTableFwdC,
                                      &drsa_conv::kTableFwdD, &drsa_conv::kTableFwdE, &drsa_conv::kTableBwdA,
                                      &drsa_conv::kTableBwdB, &drsa_conv::kTableBwdC, &drsa_conv::kTableBwdcA,
-                                     &drsa_conv::kTableBwdcB};
+                                     &drsa_conv::kTableBwdcB, &drsa_conv::kTableFwdBfA, &drsa_conv::kTableFwdBfB,
+                                     &drsa_conv::kTableFwdBfC};
 
 int pad32(int c) { return (c + 31) / 32 * 32; }
 
@@ -29,7 +30,7 @@ int env_int(const char* name, int dflt) {
   return v ? atoi(v) : dflt;
 }
 
-const Entry* find(int cin_p, int cout_p, int W, int ng, int amode, int epi) {
+const Entry* find(int cin_p, int cout_p, int W, int ng, int amode, int epi, int et = 0) {
   int th = 8, tw, mw;
   static const int th16 = env_int("DRSA_AMD_CONV_TH16", 0);
   if (W >= 32) { tw = 32; mw = 8; th = (th16 && cout_p == 32 && ng <= 2 && epi != EPI_BWDC) ? 16 : 8; }
@@ -39,7 +40,7 @@ const Entry* find(int cin_p, int cout_p, int W, int ng, int amode, int epi) {
     for (int i = 0; i < t->n; ++i) {
       const Entry& e = t->entries[i];
       if (e.cin_p == cin_p && e.cout_p == cout_p && e.th == th && e.tw == tw && e.mw == mw && e.ng == ng &&
-          e.amode == amode && e.epi == epi)
+          e.amode == amode && e.epi == epi && e.et == et)
         return &e;
     }
   return nullptr;
@@ -87,6 +88,31 @@ int drsa_amd_conv_fwd(const float* in, const float* wts, const float* bias, cons
   ConvArgs a{};
   a.in = in; a.wts = wts; a.bias = bias; a.den_map = den_map; a.out = out; a.out_amax = out_amax;
   a.out_den = out_den; a.H = H; a.W = W; a.cin = cin; a.cout = cout; a.clones = 1;
+  return launch(e, a, B, (hipStream_t)stream);
+}
+
+size_t drsa_amd_conv_weight_bf16_elems(int cin, int cout, int ng) {
+  return (size_t)ng * 9 * pad32(cin) * pad32(cout);
+}
+
+int drsa_amd_conv_fwd_bf16(const float* in, const uint16_t* wts, const float* bias, const float* den_map, float* out,
+                           uint8_t* out_amax, float* out_den, int B, int cin, int cout, int H, int W, int ng,
+                           int pool, void* stream) {
+  DRSA_REQUIRE(B > 0 && H > 0 && W > 0, "conv_fwd_bf16: bad shape");
+  DRSA_REQUIRE(cin > 1, "conv_fwd_bf16: cin = 1 runs on drsa_amd_conv_fwd (fp32 VALU kernel)");
+  DRSA_REQUIRE(ng >= 1 && ng <= 3, "conv_fwd_bf16: ng must be 1..3");
+  DRSA_REQUIRE(H % 2 == 0 && W % 2 == 0, "conv_fwd_bf16: H and W must be even (got %dx%d)", H, W);
+  DRSA_REQUIRE(!pool || out_amax, "conv_fwd_bf16: pool needs out_amax");
+  DRSA_REQUIRE(pool || W % 4 == 0, "conv_fwd_bf16: an unpooled output needs W %% 4 == 0 (got W=%d)", W);
+  DRSA_REQUIRE(((uintptr_t)wts & 15) == 0, "conv_fwd_bf16: weights must be 16-byte aligned");
+  const Entry* e = find(pad32(cin), pad32(cout), W, ng, A_DENSE, pool ? EPI_FWD_POOL : EPI_FWD_RELU, 1);
+  if (!e) {
+    drsa::set_error("conv_fwd_bf16: no kernel for cin=%d cout=%d W=%d ng=%d pool=%d", cin, cout, W, ng, pool);
+    return DRSA_EUNSUPPORTED;
+  }
+  ConvArgs a{};
+  a.in = in; a.wts = reinterpret_cast<const float*>(wts); a.bias = bias; a.den_map = den_map; a.out = out;
+  a.out_amax = out_amax; a.out_den = out_den; a.H = H; a.W = W; a.cin = cin; a.cout = cout; a.clones = 1;
   return launch(e, a, B, (hipStream_t)stream);
 }
 

@@ -26,6 +26,8 @@
 #include "common.h"
 #include "lrp_conv.h"
 
+#include <type_traits>
+
 #ifndef DRSA_CONV_PD_BWD
 #define DRSA_CONV_PD_BWD 2
 #endif
@@ -76,11 +78,28 @@ enum Epi { EPI_FWD_POOL = 0, EPI_FWD_RELU = 1, EPI_BWD = 2, EPI_BWDC = 3 };
 // 16-byte aligned (float4 staging stores) and pool cells cover aligned float2 pairs.
 constexpr int XO = 3;
 
-template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI>
+// bf16 halo row stride in 16-byte pixels: >= hx and 8 (mod 16), so the two rows of a 2x2-window
+// run of 16 lanes land on disjoint bank halves (ds_read_b128)
+constexpr int bf_stride(int hx) {
+  int r = hx;
+  while (r % 16 != 8) ++r;
+  return r;
+}
+
+// ET (element type of the MFMA operands): 0 = fp32 (v_mfma_f32_32x32x2_f32, the exact k-ordered
+// chain), 1 = bf16 (v_mfma_f32_32x32x16_bf16, forward only: conv inputs and weights rounded to
+// bf16 when staged, fp32 accumulation, fp32 outputs).  The bf16 chunk is 16 input channels = one
+// tap per MFMA (k = tap * 16 + ci); its halo is pixel-major, 8 channels per 16-byte pixel slot.
+template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI, int ET = 0>
 struct ConvCfg {
   static constexpr int CIN_ = CIN, COUT_ = COUT, TH_ = TH, TW_ = TW, MW_ = MW, CIC_ = CIC, NG_ = NG;
   static constexpr int AMODE_ = AMODE, EPI_ = EPI;
+  static constexpr bool BF = ET == 1;
   static constexpr int HY = TH + 2, HX = TW + 2;
+  static constexpr int HXB = bf_stride(HX);
+  // bf16 staging: halo [2 channel halves][HY][HXB] x 16 B, weights [NG][9 taps][2][COUT] x 16 B
+  static constexpr size_t bf_halo_floats = (size_t)2 * HY * HXB * 4;
+  static constexpr size_t bf_w_floats = (size_t)NG * 9 * 2 * COUT * 4;
   static constexpr int RS = halo_stride(HX + XO, MW);
   static constexpr int PLANE_RAW = HY * RS;
   static constexpr int PLANE = PLANE_RAW + ((PLANE_RAW % 32) == 0 ? 4 : 0);
@@ -106,7 +125,8 @@ struct ConvCfg {
   static constexpr bool SMALL_BWD = EPI == EPI_BWD && NG == 1 && CIC <= 8 && COUT <= 32;
   static constexpr int ES = (EPI == EPI_BWD && WN == 1) ? (SMALL_BWD ? 2 : DRSA_CONV_BWD_ES) : 1;
   static constexpr int TCH = WN * 32 / ES;                     // channels staged per epilogue pass
-  static constexpr size_t staging_floats = (size_t)CIC * PLANE + (size_t)NG * KCP * COUT;
+  static constexpr size_t staging_floats =
+      BF ? bf_halo_floats + bf_w_floats : (size_t)CIC * PLANE + (size_t)NG * KCP * COUT;
   static constexpr size_t epi_floats = (size_t)TCH * TH * TWP;
   static constexpr size_t lds_floats =
       (EPI == EPI_BWDC || staging_floats > epi_floats) ? staging_floats : epi_floats;
@@ -119,6 +139,7 @@ struct ConvCfg {
   static_assert(COUT % 32 == 0, "COUT must be padded to 32");
   static_assert(CIN % CIC == 0, "CIN must be a multiple of the chunk");
   static_assert(MT % WM == 0 && NT % WN == 0 && WM * WN <= 4, "wave split");
+  static_assert(!BF || (CIC == 16 && EPI < EPI_BWD && AMODE == A_DENSE), "bf16: dense forward, 16-channel chunks");
 };
 
 // ---- staging of one input-channel chunk: registers <- global (load), LDS <- registers
@@ -375,19 +396,128 @@ __device__ __forceinline__ void mfma_chunk(const float* halo, const float* wl, c
         }
   }
 }
+// ---- bf16 staging (ET = 1) of one 16-channel chunk.  Item (half, hy, hx) = the 8 channels
+//      c0 + 8 half .. +7 of halo pixel (hy, hx): 8 coalesced fp32 loads (consecutive lanes on
+//      consecutive pixels), rounded and packed at store time into one 16-byte LDS slot.  Weights
+//      come pre-laid-out and pre-rounded ([NG][CIN/16][9][2][COUT][8] bf16): a straight copy. ----
+template <class Cfg, int NT_ = kThreads>
+struct StagerBF {
+  static constexpr int CIN = Cfg::CIN_, COUT = Cfg::COUT_, NG = Cfg::NG_, HY = Cfg::HY, HX = Cfg::HX;
+  static constexpr int HXB = Cfg::HXB, NCH = CIN / 16;
+  static constexpr int NITEM = 2 * HY * HX, IT = (NITEM + NT_ - 1) / NT_;
+  static constexpr int NWQ = NG * 18 * COUT, WIT = (NWQ + NT_ - 1) / NT_;
+  float st_f[IT][8];
+  uint4 st_w[WIT];
 
+  __device__ __forceinline__ void load(const ConvArgs& a, int c0, int tid, int ty0, int tx0, int bq, int) {
+    const int H = a.H, W = a.W;
+    const size_t HW = (size_t)H * W;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int i = tid + it * NT_;
+      const int hx = i % HX, r = i / HX, hy = r % HY, half = r / HY;
+      const int gy = ty0 - 1 + hy, gx = tx0 - 1 + hx, cb = c0 + 8 * half;
+      const bool ok = i < NITEM && gy >= 0 && gy < H && gx >= 0 && gx < W;
+      const size_t base = ok ? ((size_t)bq * a.cin + cb) * HW + (size_t)gy * W + gx : 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bool okc = ok && cb + j < a.cin;
+        const float v = a.in[okc ? base + j * HW : 0];
+        st_f[it][j] = okc ? v : 0.f;
+      }
+    }
+    const uint4* wq = reinterpret_cast<const uint4*>(a.wts);
+    const int chunk = c0 / 16;
+#pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      const int idx = tid + it * NT_;
+      const bool ok = idx < NWQ;
+      const int g = idx / (18 * COUT), rem = idx % (18 * COUT);
+      st_w[it] = wq[ok ? ((size_t)g * NCH + chunk) * 18 * COUT + rem : 0];
+    }
+  }
 
-template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AMODE, EPI>::WPE))) void conv3x3_kernel(ConvArgs a) {
-  using Cfg = ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AMODE, EPI>;
+  __device__ __forceinline__ void store(float* halo, float* wl, int tid) const {
+    uint4* hb = reinterpret_cast<uint4*>(halo);
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int i = tid + it * NT_;
+      if (i < NITEM) {
+        const int hx = i % HX, r = i / HX;
+        uint4 q;
+        q.x = pack_bf16x2(st_f[it][0], st_f[it][1]);
+        q.y = pack_bf16x2(st_f[it][2], st_f[it][3]);
+        q.z = pack_bf16x2(st_f[it][4], st_f[it][5]);
+        q.w = pack_bf16x2(st_f[it][6], st_f[it][7]);
+        hb[r * HXB + hx] = q;   // r = half * HY + hy
+      }
+    }
+    uint4* wb = reinterpret_cast<uint4*>(wl);
+#pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      const int idx = tid + it * NT_;
+      if (idx < NWQ) wb[idx] = st_w[it];
+    }
+  }
+};
+
+// x+ / x- of 8 packed bf16 (sign bit per 16-bit half): Gamma's NG = 3 forward on a signed input
+__device__ __forceinline__ uint32_t bf2_neg_mask(uint32_t w) { return ((w >> 15) & 0x00010001u) * 0xffffu; }
+
+// ---- bf16 MFMA over one staged 16-channel chunk: one v_mfma_f32_32x32x16_bf16 per tap and
+//      (set, m-tile, n-tile); lane l reads its 8 channels (half l>>5) of pixel l&31 (B) and of
+//      output channel l&31 (A) as one ds_read_b128 each, one tap ahead. ----
+template <class Cfg>
+__device__ __forceinline__ void mfma_chunk_bf(const uint4* hb, const uint4* wb, const int (&pix_off)[Cfg::MPW],
+                                              int lane, int wn, f32x16 (&acc)[Cfg::NG_][Cfg::MPW][Cfg::NPW]) {
+  constexpr int MPW = Cfg::MPW, NPW = Cfg::NPW, NG = Cfg::NG_, COUT = Cfg::COUT_, HXB = Cfg::HXB;
+  const uint4* wlane = wb + (lane >> 5) * COUT + wn * NPW * 32 + (lane & 31);
+  uint4 xr[2][MPW], wr[2][NG][NPW];
+  auto rd = [&](int t, uint4 (&x)[MPW], uint4 (&w)[NG][NPW]) {
+    const int toff = (t / 3) * HXB + t % 3;
+#pragma unroll
+    for (int u = 0; u < MPW; ++u) x[u] = hb[pix_off[u] + toff];
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+      for (int v = 0; v < NPW; ++v) w[g][v] = wlane[(g * 9 + t) * 2 * COUT + v * 32];
+  };
+  rd(0, xr[0], wr[0]);
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < 9) rd(t + 1, xr[cur ^ 1], wr[cur ^ 1]);
+#pragma unroll
+    for (int v = 0; v < NPW; ++v)
+#pragma unroll
+      for (int g = 0; g < NG; ++g)
+#pragma unroll
+        for (int u = 0; u < MPW; ++u) {
+          uint4 b = xr[cur][u];
+          if constexpr (NG == 3) {
+            if (g > 0) {
+              const uint4 m = make_uint4(bf2_neg_mask(b.x), bf2_neg_mask(b.y), bf2_neg_mask(b.z), bf2_neg_mask(b.w));
+              b = (g == 1) ? make_uint4(b.x & ~m.x, b.y & ~m.y, b.z & ~m.z, b.w & ~m.w)
+                           : make_uint4(b.x & m.x, b.y & m.y, b.z & m.z, b.w & m.w);
+            }
+          }
+          acc[g][u][v] = mfma32_bf16(__builtin_bit_cast(u16x8, wr[cur][g][v]), __builtin_bit_cast(u16x8, b),
+                                     acc[g][u][v]);
+        }
+  }
+}
+
+template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI, int ET = 0>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AMODE, EPI, ET>::WPE))) void conv3x3_kernel(ConvArgs a) {
+  using Cfg = ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AMODE, EPI, ET>;
   constexpr int HY = Cfg::HY, HX = Cfg::HX, RS = Cfg::RS, PLANE = Cfg::PLANE;
   constexpr int MTH = Cfg::MTH, MTW = Cfg::MTW, MTX = Cfg::MTX;
   constexpr int WM = Cfg::WM, MPW = Cfg::MPW, NPW = Cfg::NPW;
   constexpr int KC = Cfg::KC, KCP = Cfg::KCP;
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* halo = smem;                          // [CIC][PLANE]
-  float* wl = smem + CIC * PLANE;              // [NG][KCP][COUT]
+  float* halo = smem;                          // [CIC][PLANE]   (bf16: [2][HY][HXB] x 16 B)
+  float* wl = smem + (Cfg::BF ? Cfg::bf_halo_floats : (size_t)CIC * PLANE);   // [NG][KCP][COUT]
 
   const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
   const int H = a.H, W = a.W;
@@ -412,7 +542,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
     const int p = lane & 31, win = p >> 2, sub = p & 3;
     pix_y[u] = (mt / MTX) * MTH + 2 * (win / MW) + (sub >> 1);
     pix_x[u] = (mt % MTX) * MTW + 2 * (win % MW) + (sub & 1);
-    pix_off[u] = pix_y[u] * RS + pix_x[u] + XO;
+    pix_off[u] = Cfg::BF ? (h * HY + pix_y[u]) * Cfg::HXB + pix_x[u] : pix_y[u] * RS + pix_x[u] + XO;
   }
 
   f32x16 acc[NG][MPW][NPW];
@@ -459,7 +589,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
   auto gch = [&](int cl, int v) { return ((cl >> 5) * NPW + v) * 32 + (cl & 31); };   // global channel
   // global channel of staged row cl in pass sub (ES = 2 implies WN = 1)
   auto gchs = [&](int cl, int v, int sub) { return ES == 1 ? gch(cl, v) : v * 32 + sub * TCH + cl; };
-  Stager<Cfg> stg;
+  typename std::conditional<Cfg::BF, StagerBF<Cfg>, Stager<Cfg>>::type stg;
   stg.load(a, 0, tid, ty0, tx0, bq, bs);
   // backward: all chunks but the last here, the last one peeled below (after the epilogue
   // addressing is set up, so that none of it is live across the loop)
@@ -469,7 +599,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
     __syncthreads();
     if (chunk + 1 < Cfg::NCHUNK) stg.load(a, (chunk + 1) * CIC, tid, ty0, tx0, bq, bs);
     if (!active || (a.dbg & 4)) continue;
-    mfma_chunk<Cfg, Cfg::PD>(halo, wl, pix_off, lane, wn, acc);
+    if constexpr (Cfg::BF)
+      mfma_chunk_bf<Cfg>(reinterpret_cast<const uint4*>(halo), reinterpret_cast<const uint4*>(wl), pix_off, lane, wn, acc);
+    else
+      mfma_chunk<Cfg, Cfg::PD>(halo, wl, pix_off, lane, wn, acc);
   }
   constexpr int Q = TH * TW / 4, CS = kThreads / Q;
   static_assert(kThreads % Q == 0, "float4 groups per tile must divide the block");
@@ -766,12 +899,18 @@ struct Entry {
   int cin_p, cout_p, th, tw, mw, cic, ng, amode, epi;
   KernFn fn;
   size_t lds;
+  int et = 0;   // operand type (ConvCfg ET)
 };
 
 #define CONV_ENTRY(CIN, COUT, TH, TW, MW, CIC, NG, AM, EP)                                                 \
   drsa_conv::Entry{CIN, COUT, TH, TW, MW, CIC, NG, AM, EP,                                                 \
                    drsa_conv::conv3x3_kernel<CIN, COUT, TH, TW, MW, CIC, NG, AM, EP>,                      \
                    drsa_conv::ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AM, EP>::lds_floats * sizeof(float)}
+
+#define CONV_ENTRY_BF(CIN, COUT, TH, TW, MW, NG, EP)                                                     \
+  drsa_conv::Entry{CIN, COUT, TH, TW, MW, 16, NG, drsa_conv::A_DENSE, EP,                                 \
+                   drsa_conv::conv3x3_kernel<CIN, COUT, TH, TW, MW, 16, NG, drsa_conv::A_DENSE, EP, 1>,   \
+                   drsa_conv::ConvCfg<CIN, COUT, TH, TW, MW, 16, NG, drsa_conv::A_DENSE, EP, 1>::lds_floats * sizeof(float), 1}
 
 // tile by output width: W >= 32 -> 16x32 (32 output channels) or 8x32 (MW 8); 8 < W < 32 -> 8x16
 // (MW 8); W <= 8 -> 8x8 (MW 4)
@@ -794,6 +933,21 @@ struct Entry {
   CONV_FAMILY(CIN, COUT, CIC, 2, drsa_conv::A_DENSE, drsa_conv::EPI_BWD),               \
   CONV_FAMILY(CIN, COUT, CIC, 1, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD),          \
   CONV_FAMILY(CIN, COUT, CIC, 2, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD)
+
+#define CONV_FAMILY_BF(CIN, COUT, NG, EP)                      \
+  CONV_ENTRY_BF(CIN, COUT, 16, 32, 8, NG, EP),                 \
+  CONV_ENTRY_BF(CIN, COUT, 8, 32, 8, NG, EP),                  \
+  CONV_ENTRY_BF(CIN, COUT, 8, 16, 8, NG, EP),                  \
+  CONV_ENTRY_BF(CIN, COUT, 8, 8, 4, NG, EP)
+
+// bf16-operand forward (ET = 1), every denominator set count and both epilogues
+#define FWD_SET_BF(CIN, COUT)                                                 \
+  CONV_FAMILY_BF(CIN, COUT, 1, drsa_conv::EPI_FWD_POOL),                      \
+  CONV_FAMILY_BF(CIN, COUT, 2, drsa_conv::EPI_FWD_POOL),                      \
+  CONV_FAMILY_BF(CIN, COUT, 3, drsa_conv::EPI_FWD_POOL),                      \
+  CONV_FAMILY_BF(CIN, COUT, 1, drsa_conv::EPI_FWD_RELU),                      \
+  CONV_FAMILY_BF(CIN, COUT, 2, drsa_conv::EPI_FWD_RELU),                      \
+  CONV_FAMILY_BF(CIN, COUT, 3, drsa_conv::EPI_FWD_RELU)
 
 struct Table {
   const Entry* entries;

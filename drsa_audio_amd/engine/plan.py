@@ -20,6 +20,13 @@ path fans one forward out into K+1 relevance clones at the projection
 Weights are prepared on the device once per plan (rule-modified, flipped/transposed for
 the backward, padded to the kernels' channel tiles).  Activation buffers are cached per
 batch size.
+
+Precision: a model whose parameters are bfloat16 (``model.bfloat16()``) compiles a bf16 plan
+(the reference has no bf16 path): every conv weight set (rule-modified, forward and
+backward) is rounded to bf16, the network input is rounded to bf16, and every conv with Cin > 1
+runs forward on ``drsa_amd_conv_fwd_bf16`` (inputs rounded to bf16 as they are staged,
+v_mfma_f32_32x32x16_bf16, fp32 accumulation).  Biases, activations, denominators, the dense head
+and the whole relevance backward stay fp32 (oracle: ``lrp_ref.lrp(mode="bf16")``).
 """
 from __future__ import annotations
 
@@ -93,6 +100,8 @@ class ConvStage:
     wts_fwd_n: torch.Tensor = None
     bias3_n: torch.Tensor = None
     wts_bwd_n: torch.Tensor = None
+    wts_fwd_bf: torch.Tensor = None      # bf16 plan: [ng][cin_p/16][9][2][cout_p][8] bfloat16
+    wts_fwd_n_bf: torch.Tensor = None
     alpha: float = 1.0
     beta: float = 0.0
     ng_bwd: int = 1
@@ -120,7 +129,8 @@ class EngineError(NotImplementedError):
 
 
 class LRPEngine:
-    def __init__(self, model: nn.Module, composite, device: Optional[torch.device] = None):
+    def __init__(self, model: nn.Module, composite, device: Optional[torch.device] = None,
+                 precision: Optional[str] = None):
         _capi.load()
         # no strong references to the model / composite: the plan owns prepared copies of what it
         # needs, and get_engine's cache is keyed by weak references (engine/__init__.py)
@@ -128,6 +138,12 @@ class LRPEngine:
         self._composite_ref = (lambda: None) if composite is None else weakref.ref(composite)
         p0 = next(model.parameters())
         self.device = device or p0.device
+        if precision is None:
+            precision = "bf16" if p0.dtype == torch.bfloat16 else "fp32"
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
+        self.precision = precision
+        self.bf16 = precision == "bf16"
         if self.device.type != "cuda":
             raise _capi.DrsaAmdError("the LRP engine runs on the GPU only; move the model to a HIP device")
         rules = composite.rules(model) if composite is not None else {}
@@ -192,6 +208,8 @@ class LRPEngine:
                     raise EngineError("BatchNorm2d in the trunk needs the SequentialMergeBatchNorm canonizer")
                 W, b = SequentialMergeBatchNorm.fold(W, b, _bn_to(feats[j][1], torch.device("cpu")))
                 j += 1
+            if self.bf16:
+                W = _bf16r(W)
             W, b = W.to(self.device), b.to(self.device)
             if j >= n or not isinstance(feats[j][1], nn.ReLU):
                 raise EngineError(f"engine: conv features.{name} must be followed by ReLU")
@@ -388,9 +406,23 @@ class LRPEngine:
         else:   # no rule: plain gradient
             sets, st.ng_fwd, st.den_kind = [W], 1, None
             st.ng_bwd, st.xmode_bwd, bsets = 1, XM_NONE, [W]
+        if self.bf16:
+            # every weight set the kernels see holds bf16 values (forward and backward alike)
+            sets, bsets = [_bf16r(s_) for s_ in sets], [_bf16r(s_) for s_ in bsets]
+            if k in ("wsquare", "flat"):
+                st.W2 = _bf16r(st.W2)
+                if st.w2_first is not None:
+                    st.w2_first = _bf16r(st.w2_first)
+            if st.wts_fwd_n is not None:
+                st.wts_fwd_n = _bf16r(st.wts_fwd_n)
+                st.wts_bwd_n = _bf16r(st.wts_bwd_n)
         st.wts_fwd = torch.stack([fwd_layout(s) for s in sets]).contiguous()
         st.bias3 = bias3.contiguous()
         st.wts_bwd = torch.stack([bwd_layout(s) for s in bsets]).contiguous()
+        if self.bf16 and st.cin > 1:
+            st.wts_fwd_bf = _bf16_layout(st.wts_fwd, cin_p, cout_p)
+            if st.wts_fwd_n is not None:
+                st.wts_fwd_n_bf = _bf16_layout(st.wts_fwd_n, cin_p, cout_p)
         if st.proj is not None and st.proj.U.size(0) != st.cout:
             raise EngineError("engine: projection width differs from the conv channels")
 
@@ -402,6 +434,16 @@ class LRPEngine:
                        st.cin, H, W, _capi.stream_ptr(self.device))
             st.den_maps[key] = den
         return st.den_maps[key]
+
+    def _conv_fwd(self, tag, st: ConvStage, neg: bool, cur, den_map, out, amax, den, B, h, w, ng, pool, s):
+        """One conv forward launch: the bf16 kernel in a bf16 plan (Cin > 1), else fp32."""
+        bias3 = st.bias3_n if neg else st.bias3
+        if self.bf16 and st.cin > 1:
+            name, wts = "drsa_amd_conv_fwd_bf16", (st.wts_fwd_n_bf if neg else st.wts_fwd_bf)
+        else:
+            name, wts = "drsa_amd_conv_fwd", (st.wts_fwd_n if neg else st.wts_fwd)
+        self._call(tag, name, cur.data_ptr(), wts.data_ptr(), bias3.data_ptr(), _capi.ptr(den_map), out.data_ptr(),
+                   _capi.ptr(amax), _capi.ptr(den), B, st.cin, st.cout, h, w, ng, pool, s)
 
     # ---------------------------------------------------------------- buffers
     def _buf(self, key, shape, dtype=torch.float32):
@@ -418,7 +460,10 @@ class LRPEngine:
         index of a conv stage whose full-resolution ReLU output is kept even though a max-pool
         follows (the reference's store_hook, preprocessing.py:92-103)."""
         _capi.require_gpu(x, "input", dtype=None)
-        x = x.detach().to(torch.float32).contiguous()
+        x = x.detach()
+        if self.bf16:
+            x = x.to(torch.bfloat16)
+        x = x.to(torch.float32).contiguous()
         if x.dim() != 4 or x.size(1) != self.stages[0].cin:
             raise ValueError(f"input must be [B, {self.stages[0].cin}, H, W]")
         B, _, H, W = x.shape
@@ -438,9 +483,7 @@ class LRPEngine:
             if st.proj is None and st.pool and (li == capture or st.pool_k != (2, 2)):
                 a = self._buf((li, "a"), (B, st.cout, h, w))
                 den_full = self._buf((li, "den_full"), (B, st.cout, h, w)) if need_den else None
-                self._call(f"conv_fwd:{st.name}", "drsa_amd_conv_fwd", cur.data_ptr(), st.wts_fwd.data_ptr(),
-                           st.bias3.data_ptr(), _capi.ptr(den_map), a.data_ptr(), None, _capi.ptr(den_full), B, st.cin,
-                           st.cout, h, w, st.ng_fwd, 0, s)
+                self._conv_fwd(f"conv_fwd:{st.name}", st, False, cur, den_map, a, None, den_full, B, h, w, st.ng_fwd, 0, s)
                 out = self._buf((li, "y"), (B, st.cout, h // ph, w // pw))
                 amax = self._buf((li, "amax"), (B, st.cout, h // ph, w // pw), torch.uint8)
                 den = self._buf((li, "den"), (B, st.cout, h // ph, w // pw)) if need_den else None
@@ -452,29 +495,21 @@ class LRPEngine:
                 out = self._buf((li, "y"), (B, st.cout, h // 2, w // 2))
                 amax = self._buf((li, "amax"), (B, st.cout, h // 2, w // 2), torch.uint8)
                 den = self._buf((li, "den"), (B, st.cout, h // 2, w // 2)) if need_den else None
-                self._call(f"conv_fwd:{st.name}", "drsa_amd_conv_fwd", cur.data_ptr(), st.wts_fwd.data_ptr(),
-                           st.bias3.data_ptr(), _capi.ptr(den_map), out.data_ptr(), amax.data_ptr(), _capi.ptr(den), B, st.cin, st.cout,
-                           h, w, st.ng_fwd, 1, s)
+                self._conv_fwd(f"conv_fwd:{st.name}", st, False, cur, den_map, out, amax, den, B, h, w, st.ng_fwd, 1, s)
                 rec.update(y=out, amax=amax, den=den, Hout=h // 2, Wout=w // 2)
                 if st.den_kind == "ab":   # second pass: den_n (y and argmax rewritten with the same values)
                     den_n = self._buf((li, "den_n"), (B, st.cout, h // 2, w // 2))
-                    self._call(f"conv_fwd_n:{st.name}", "drsa_amd_conv_fwd", cur.data_ptr(), st.wts_fwd_n.data_ptr(),
-                               st.bias3_n.data_ptr(), None, out.data_ptr(), amax.data_ptr(), den_n.data_ptr(), B, st.cin,
-                               st.cout, h, w, 2, 1, s)
+                    self._conv_fwd(f"conv_fwd_n:{st.name}", st, True, cur, None, out, amax, den_n, B, h, w, 2, 1, s)
                     rec.update(den_n=den_n)
                 cur, h, w = out, h // 2, w // 2
             else:
                 a = self._buf((li, "a"), (B, st.cout, h, w))
                 den = self._buf((li, "den"), (B, st.cout, h, w)) if need_den else None
-                self._call(f"conv_fwd:{st.name}", "drsa_amd_conv_fwd", cur.data_ptr(), st.wts_fwd.data_ptr(),
-                           st.bias3.data_ptr(), _capi.ptr(den_map), a.data_ptr(), None, _capi.ptr(den), B, st.cin, st.cout, h, w,
-                           st.ng_fwd, 0, s)
+                self._conv_fwd(f"conv_fwd:{st.name}", st, False, cur, den_map, a, None, den, B, h, w, st.ng_fwd, 0, s)
                 rec.update(a=a, den=den)
                 if st.den_kind == "ab":
                     den_n = self._buf((li, "den_n"), (B, st.cout, h, w))
-                    self._call(f"conv_fwd_n:{st.name}", "drsa_amd_conv_fwd", cur.data_ptr(), st.wts_fwd_n.data_ptr(),
-                               st.bias3_n.data_ptr(), None, a.data_ptr(), None, den_n.data_ptr(), B, st.cin, st.cout, h, w,
-                               2, 0, s)
+                    self._conv_fwd(f"conv_fwd_n:{st.name}", st, True, cur, None, a, None, den_n, B, h, w, 2, 0, s)
                     rec.update(den_n=den_n)
                 if st.proj is not None:
                     P = st.proj
@@ -706,6 +741,19 @@ class LRPEngine:
                    out["standard_relevance"].data_ptr(), out["subspace_heatmaps"].data_ptr(),
                    out["subspace_relevances"].data_ptr(), out["mask"].data_ptr(), _capi.stream_ptr(self.device))
         return out
+
+
+def _bf16r(t: torch.Tensor) -> torch.Tensor:
+    """Round to bf16 (nearest even) and back: the values a bf16 plan's kernels see."""
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+def _bf16_layout(wf: torch.Tensor, cin_p: int, cout_p: int) -> torch.Tensor:
+    """[ng][9*cin_p][cout_p] fp32 (row k = ci*9 + tap) -> [ng][cin_p/16][9][2][cout_p][8] bf16,
+    input channel ci = 16*chunk + 8*half + j (drsa_amd_conv_fwd_bf16, include/drsa_amd.h)."""
+    ng = wf.size(0)
+    t = wf.reshape(ng, cin_p // 16, 2, 8, 9, cout_p).permute(0, 1, 4, 2, 5, 3)
+    return t.to(torch.bfloat16).contiguous()
 
 
 def _bn_to(bn, device):

@@ -108,6 +108,19 @@ int drsa_amd_conv_fwd(const float* in, const float* wts, const float* bias, cons
                       uint8_t* out_amax, float* out_den, int B, int cin, int cout, int H, int W, int ng,
                       int pool, void* stream);
 
+/* bf16-operand variant of drsa_amd_conv_fwd (the bf16 CNN with fp32 accumulate; the
+ * reference has no bf16 path).  The conv input is rounded to bf16 (nearest even) as it is staged,
+ * the weights come pre-rounded in the layout [ng][cin_p/16][9 taps][2][cout_p][8] bf16
+ * (cin_p = pad32(cin), cout_p = pad32(cout); input channel = 16 chunk + 8 half + j, tap = 3 ky + kx;
+ * drsa_amd_conv_weight_bf16_elems elements, 16-byte aligned), products are summed in fp32 on
+ * v_mfma_f32_32x32x16_bf16 and everything after the accumulator (bias, ReLU, pool, argmax,
+ * denominators) and every output is fp32, exactly as drsa_amd_conv_fwd.  cin > 1 only (the
+ * Cin = 1 first layer stays on the fp32 kernel). */
+size_t drsa_amd_conv_weight_bf16_elems(int cin, int cout, int ng);
+int drsa_amd_conv_fwd_bf16(const float* in, const uint16_t* wts, const float* bias, const float* den_map, float* out,
+                           uint8_t* out_amax, float* out_den, int B, int cin, int cout, int H, int W, int ng,
+                           int pool, void* stream);
+
 /* Rule backward of one conv as a transposed conv (flipped/transposed weights), with the
  * max-pool/ReLU backward folded into the input (g_amax != NULL: g at pool resolution) and
  * the next layer's division folded into the output (post).  Bq rows = samples * clones.

@@ -29,7 +29,7 @@ Rule arithmetic (z = f(x; W, b), Jᵀ_W g = input-gradient of f with weights W):
 Layers without a rule use their plain gradient (ReLU, MaxPool [first max], Dropout
 (eval), BatchNorm (eval), flatten), exactly like zennit's Gradient attributor.
 
-Four execution modes share that arithmetic:
+Five execution modes share that arithmetic:
 * ``mode="analytic"`` — each rule evaluated with explicit conv/conv-transpose calls.
 * ``mode="zennit"``   — each rule evaluated the way zennit's BasicHook does it
   (modified forwards + ``torch.autograd.grad``), and the heatmap generator replicates
@@ -45,6 +45,8 @@ Four execution modes share that arithmetic:
   rounding (the ProjectionModel's a' = (aU)Uᵀ differs from a at rounding level and the
   ε = 1e-6 stabilisers amplify that at dead ReLU channels: correctly rounded projections
   move subspace relevances by up to ~6 %), so only a pinned order can pin it.
+* ``mode="bf16"``     — float64 with every conv's input and weights rounded to bf16 (class
+  ``Bf16Ops``): the definition of the product's bf16 plan (no reference bf16 path).
 """
 from __future__ import annotations
 
@@ -272,9 +274,30 @@ class ExactOps:
         return out.reshape(lead)
 
 
+def _bf16r(t: torch.Tensor) -> torch.Tensor:
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+class Bf16Ops(TorchOps):
+    """The bf16 plan's arithmetic (the reference has no bf16 path, so this is the
+    definition the product's bf16 mode is checked against): every conv rounds its input and its
+    (rule-modified) weights to bf16, in both directions, and accumulates in float64 here; biases,
+    dense layers, divisions and products with the activations stay at full precision."""
+    name = "bf16"
+
+    @staticmethod
+    def conv(m, x, w, b):
+        return TorchOps.conv(m, _bf16r(x), _bf16r(w), b)
+
+    @staticmethod
+    def conv_t(m, x_shape, w, g):
+        return TorchOps.conv_t(m, x_shape, _bf16r(w), g)
+
+
 # "f64": the analytic structure evaluated in float64 (model and input promoted): the accuracy
-# anchor that fp32 implementations (the reference's own path, the HIP kernels) are measured against
-OPS = {"analytic": TorchOps, "zennit": TorchOps, "exact": ExactOps, "f64": TorchOps}
+# anchor that fp32 implementations (the reference's own path, the HIP kernels) are measured against.
+# "bf16": the same in float64 with Bf16Ops (input rounded to bf16 first).
+OPS = {"analytic": TorchOps, "zennit": TorchOps, "exact": ExactOps, "f64": TorchOps, "bf16": Bf16Ops}
 
 
 def _aff(L: Layer, x, w, b, ops=TorchOps):
@@ -512,17 +535,32 @@ def output_seed(logits: torch.Tensor, class_idx=None, num_classes=None,
 @torch.no_grad()
 def lrp(model: nn.Module, rules: Dict[str, RuleSpec], x: torch.Tensor, class_idx=None,
         num_classes=None, one_hot_encoded=False, mode: str = "analytic",
-        capture: Optional[str] = None):
-    """Returns (logits, R_input[, (act, rel) at layer ``capture``])."""
-    if mode == "f64":
+        capture: Optional[str] = None, forced_inputs: Optional[Dict[str, torch.Tensor]] = None):
+    """Returns (logits, R_input[, (act, rel) at layer ``capture``]).
+
+    ``forced_inputs`` (layer name -> tensor): the input of that layer is replaced by the given
+    values (the product's own activations, which differ from this forward's by accumulation-order
+    rounding only), so that a bf16 rounding decision taken on them is the product's; the rest of
+    the forward and the whole backward are evaluated here."""
+    if mode in ("f64", "bf16"):
         import copy
         model = copy.deepcopy(model).double()
+    if mode == "bf16":
+        # the plan's weights are bf16 values (after any BN merge); rule-modified sets derived from
+        # them are rounded again by Bf16Ops
+        for mod in model.modules():
+            if isinstance(mod, nn.Conv2d):
+                mod.weight.data = _bf16r(mod.weight.data)
     layers = sequential_layers(model)
     ops = OPS[mode]
     acts: List[Tuple[torch.Tensor, torch.Tensor, object]] = []
-    h = x.detach().to(torch.float64 if mode == "f64" else torch.float32)
+    h = x.detach().to(torch.float64 if mode in ("f64", "bf16") else torch.float32)
+    if mode == "bf16":
+        h = _bf16r(h)
     for L in layers:
         aux = None
+        if forced_inputs is not None and L.name in forced_inputs:
+            h = forced_inputs[L.name].detach().to(h.device, h.dtype).reshape(h.shape)
         if L.kind == "maxpool":
             m = L.module
             out, aux = F.max_pool2d(h, m.kernel_size, m.stride, m.padding, m.dilation,

@@ -1,0 +1,200 @@
+"""bf16 plan on the GPU ("a bf16 path with fp32 accumulate"; BASELINE configs[4]).
+
+The reference has no bf16 path, so the definition checked here is oracle/lrp_ref.py mode="bf16"
+(class Bf16Ops): every conv rounds its input and its rule-modified weights to bf16 (nearest
+even); accumulation, biases, divisions, the dense head and the products with the activations
+are exact (float64).  The HIP path accumulates in fp32 (v_mfma_f32_32x32x16_bf16), so the
+tolerance is loosened and stated per check:
+
+* conv kernel: |out - ref| <= 2e-5 * conv(|bf16(x)|, |bf16(W)|) elementwise (fp32 summation
+  of <= 1152 exact bf16 products), pool argmax equal wherever the window's top two values are
+  further apart than that bound;
+* whole plan: per-sample relative L2 distance of the relevances <= 5e-3 and logits within
+  1e-4 relative.  A relevance map is a difference of large terms on these random-init models,
+  and an activation within 2^-24 of a bf16 rounding boundary can round the other way in fp32
+  (one bf16 ulp on one value): measured on the CPU with fp32-accumulating Bf16Ops, 3 samples of 4
+  land within 5e-6 and one at 3e-4.
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import lrp_ref
+from lrp_common import gtzan128, logmel, spec, vggish
+from drsa_audio_amd import _capi
+from drsa_audio_amd.engine.plan import _bf16_layout
+from drsa_audio_amd.utils.constants import LRP_NAME_MAP_GTZAN, LRP_NAME_MAP_VGGISH
+from drsa_audio_amd.zennit.canonizers import SequentialMergeBatchNorm
+from drsa_audio_amd.zennit.composites import NameMapComposite
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+KTOL = 2e-5
+
+
+def _r(t):
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+def _pad32(c):
+    return (c + 31) // 32 * 32
+
+
+def _fwd_layout(W, cin_p, cout_p):
+    cout, cin = W.shape[:2]
+    t = torch.zeros(cin_p, 3, 3, cout_p, dtype=torch.float32)
+    t[:cin, :, :, :cout] = W.permute(1, 2, 3, 0)
+    return t.reshape(9 * cin_p, cout_p)
+
+
+def _run_kernel(x, sets, bias3, ng, pool):
+    B, cin, H, W = x.shape
+    cout = sets[0].size(0)
+    cin_p, cout_p = _pad32(cin), _pad32(cout)
+    wf = torch.stack([_fwd_layout(_r(s), cin_p, cout_p) for s in sets])
+    wb = _bf16_layout(wf, cin_p, cout_p).to(DEV)
+    assert wb.numel() == _capi.lib().drsa_amd_conv_weight_bf16_elems(cin, cout, ng)
+    xd = x.to(DEV).contiguous()
+    b3 = torch.zeros(3, cout_p)
+    b3[:, :cout] = bias3
+    b3 = b3.to(DEV)
+    Ho, Wo = (H // 2, W // 2) if pool else (H, W)
+    out = torch.full((B, cout, Ho, Wo), float("nan"), device=DEV)
+    den = torch.full((B, cout, Ho, Wo), float("nan"), device=DEV)
+    amax = torch.zeros((B, cout, Ho, Wo), dtype=torch.uint8, device=DEV) if pool else None
+    _capi.call("drsa_amd_conv_fwd_bf16", xd.data_ptr(), wb.data_ptr(), b3.data_ptr(), None, out.data_ptr(),
+               _capi.ptr(amax), den.data_ptr(), B, cin, cout, H, W, ng, pool, _capi.stream_ptr())
+    torch.cuda.synchronize()
+    return out.cpu(), den.cpu(), None if amax is None else amax.cpu()
+
+
+def _ref(x, sets, bias3, ng):
+    xd = _r(x.double())
+    ins = [xd, xd, None]
+    if ng == 3:
+        ins = [xd, xd.clamp(min=0), xd.clamp(max=0)]
+    z = [F.conv2d(ins[g], _r(sets[g].double()), padding=1) for g in range(ng)]
+    scale = sum(F.conv2d(ins[g].abs(), _r(sets[g].double()).abs(), padding=1) for g in range(ng))
+    b = bias3.double()
+    y = (z[0] + b[0][None, :, None, None]).clamp(min=0)
+    if ng == 1:
+        den = z[0] + b[1][None, :, None, None]
+    else:
+        den = (z[1] + b[1][None, :, None, None]) + ((z[2] if ng == 3 else 0) + b[2][None, :, None, None])
+    return y, den, scale
+
+
+@pytest.mark.parametrize("cin,cout", [(32, 32), (32, 64), (64, 64), (64, 100), (100, 128), (128, 128)])
+@pytest.mark.parametrize("ng", [1, 2, 3])
+@pytest.mark.parametrize("W", [64, 16, 8])
+def test_conv_fwd_bf16_kernel(cin, cout, ng, W):
+    g = torch.Generator().manual_seed(cin * 7 + cout + ng * 13 + W)
+    B, H = 2, 16
+    x = torch.randn(B, cin, H, W, generator=g)
+    if ng < 3:
+        x = x.clamp(min=0)          # ng = 1 / 2: the non-negative input contract of the forward sets
+    Wt = torch.randn(cout, cin, 3, 3, generator=g) / (9 * cin) ** 0.5
+    sets = [Wt, Wt + 0.25 * Wt.clamp(min=0), Wt + 0.25 * Wt.clamp(max=0)][:ng]
+    bias3 = torch.randn(3, cout, generator=g) * 0.1
+    y, den, sc = _ref(x, sets, bias3, ng)
+    bound = KTOL * (sc + bias3.abs().sum(0).double()[None, :, None, None]) + 1e-30
+    for pool in (0, 1):
+        out, dg, am = _run_kernel(x, sets, bias3, ng, pool)
+        if not pool:
+            assert torch.all((out.double() - y).abs() <= bound), (cin, cout, ng, W)
+            assert torch.all((dg.double() - den).abs() <= bound)
+            continue
+        win = y.reshape(B, cout, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, cout, H // 2, W // 2, 4)
+        bwin = bound.reshape(B, cout, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, cout, H // 2, W // 2, 4)
+        ym, _ = win.max(-1)
+        assert torch.all((out.double() - ym).abs() <= bwin.max(-1).values)
+        top2 = win.topk(2, dim=-1).values
+        clear = (top2[..., 0] - top2[..., 1]) > 2 * bwin.max(-1).values
+        ref_am = win.argmax(-1)
+        assert torch.equal(am.long()[clear], ref_am[clear])
+        dwin = den.reshape(B, cout, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, cout, H // 2, W // 2, 4)
+        dref = torch.gather(dwin, -1, am.long()[..., None])[..., 0]
+        bsel = torch.gather(bwin, -1, am.long()[..., None])[..., 0]
+        assert torch.all((dg.double() - dref).abs() <= bsel)
+
+
+def _rel_ok(R, Rref, tol=5e-3):
+    for b in range(R.size(0)):
+        d = float((R[b].double() - Rref[b]).norm() / Rref[b].norm())
+        assert d <= tol, (b, d)
+
+
+def test_gtzan_bf16_plan_standard_lrp_vs_oracle():
+    from drsa_audio_amd.engine import get_engine
+    from drsa_audio_amd.xai.explain.attribute import compute_relevances
+    net = gtzan128().bfloat16()
+    x = logmel(4, seed=21).bfloat16()
+    comp = NameMapComposite(LRP_NAME_MAP_GTZAN)
+    logits, Rref = lrp_ref.lrp(copy.deepcopy(net).float(), spec(LRP_NAME_MAP_GTZAN), x.float(), class_idx=6, mode="bf16")
+    ng = copy.deepcopy(net).to(DEV)
+    R = compute_relevances(ng, x.to(DEV), comp, class_idx=6).cpu()
+    eng = get_engine(ng, comp)
+    assert eng.precision == "bf16"
+    assert all(st.wts_fwd_bf is not None for st in eng.stages if st.cin > 1)
+    lg = eng.forward(x.to(DEV)).cpu().double()
+    np.testing.assert_allclose(lg, logits, rtol=1e-4, atol=1e-4 * float(logits.abs().max()))
+    _rel_ok(R, Rref)
+
+
+def test_gtzan_bf16_plan_differs_from_fp32_plan_by_rounding_only():
+    """The fp32 model keeps the fp32 (bit-exact) plan; the bf16 plan differs from it only by the
+    bf16 rounding (logits close, not equal)."""
+    from drsa_audio_amd.engine import get_engine
+    net = gtzan128()
+    x = logmel(2, seed=22)
+    comp = NameMapComposite(LRP_NAME_MAP_GTZAN)
+    e32 = get_engine(copy.deepcopy(net).to(DEV), comp)
+    e16 = get_engine(copy.deepcopy(net).bfloat16().to(DEV), comp)
+    assert e32.precision == "fp32" and e16.precision == "bf16"
+    e16.trace = []
+    l16 = e16.forward(x.to(DEV)).cpu()
+    e16.trace = None
+    l32 = e32.forward(x.to(DEV)).cpu()
+    assert not torch.equal(l16, l32)
+    np.testing.assert_allclose(l16, l32, rtol=0.1, atol=0.05 * float(l32.abs().max()))
+
+
+@pytest.mark.parametrize("layer_idx", [26, 33])
+def test_vggish_bf16_capture_vs_oracle(layer_idx):
+    """C5's CNN leg: VGGish-BN (BN folded in fp32, then rounded) in bf16, DRSA data capture at
+    j = 26 / 33 (activations and relevances) against the bf16 definition.
+
+    The relevances of this random-init BN model are ill-conditioned with respect to the bf16
+    rounding of the activations (Gamma denominators near zero in blocks 4-5): on the CPU, the same
+    bf16 arithmetic accumulated in fp32 instead of float64 flips one activation's rounding and
+    moves the j = 26 relevances by 46 % (j = 29: 1.2 %, j = 33: 3e-4).  So the oracle is run
+    teacher-forced: every conv's input, and the captured ReLU output where the max-pool takes its
+    argmax, is the engine's own stored activation (lrp_ref ``forced_inputs``), which leaves
+    accumulation order as the only difference (measured: <= 6e-4 at j = 26/27/30/33)."""
+    from drsa_audio_amd.engine import get_engine
+    from drsa_audio_amd.xai.drsa.preprocessing import get_intermediate
+    net = vggish().bfloat16()
+    x = logmel(2, 128, 256, seed=layer_idx).bfloat16()
+    comp = NameMapComposite(LRP_NAME_MAP_VGGISH, canonizers=[SequentialMergeBatchNorm()])
+    mg = copy.deepcopy(net).to(DEV)
+    a, r = get_intermediate(mg, x.to(DEV), comp, layer_idx, 1)
+    a, r = a.cpu(), r.cpu()
+    eng = get_engine(mg, comp)
+    assert eng.precision == "bf16"
+    forced = {st.name: rec["in"].cpu() for st, rec in zip(eng.stages, eng.last["stages"])}
+    # and the max-pool after the captured ReLU takes its argmax on the engine's activations: a
+    # near-tie in a 2x2 window (values equal to ~1e-7) otherwise routes relevance to another pixel
+    forced[f"features.{layer_idx + 1}"] = a
+    merged = lrp_ref.merge_batch_norm(copy.deepcopy(net).float())
+    _, _, (act, rel) = lrp_ref.lrp(merged, spec(LRP_NAME_MAP_VGGISH), x.float(), class_idx=1, mode="bf16",
+                                   capture=f"features.{layer_idx}", forced_inputs=forced)
+    assert a.dtype == torch.float32 and a.shape == act.shape
+    _rel_ok(a, act, 1e-5)
+    _rel_ok(r, rel)
+    # unforced: the activations still agree to bf16 level
+    _, _, (act_u, _) = lrp_ref.lrp(merged, spec(LRP_NAME_MAP_VGGISH), x.float(), class_idx=1, mode="bf16",
+                                   capture=f"features.{layer_idx}")
+    _rel_ok(a, act_u, 1e-3)
