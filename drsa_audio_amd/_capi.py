@@ -39,6 +39,7 @@ SIGNATURES = {
     "drsa_amd_conv_weight_floats": (_sz, [_i32, _i32, _i32]),
     "drsa_amd_conv_fwd": (_i32, [_fp, _fp, _fp, _fp, _fp, _vp, _fp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
     "drsa_amd_conv_weight_bf16_elems": (_sz, [_i32, _i32, _i32]),
+    "drsa_amd_conv_fwd_has_kernel": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32]),
     "drsa_amd_conv_fwd_bf16": (_i32, [_fp, _vp, _fp, _fp, _fp, _vp, _fp, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
                                       _vp]),
     "drsa_amd_conv_bwd": (_i32, [_fp, _vp, _fp, _fp, _fp, _fp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32,

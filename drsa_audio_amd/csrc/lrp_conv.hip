@@ -10,7 +10,7 @@
 // ---------------------------------------------------------------------------
 namespace drsa_conv {
 extern const Table kTableFwdA, kTableFwdB, kTableFwdC, kTableFwdD, kTableFwdE, kTableBwdA, kTableBwdB, kTableBwdC,
-    kTableBwdcA, kTableBwdcB, kTableFwdBfA, kTableFwdBfB, kTableFwdBfC;
+    kTableBwdcA, kTableBwdcB, kTableFwdBfA, kTableFwdBfB, kTableFwdBfC, kTableFwdP4;
 }
 
 namespace {
@@ -21,7 +21,7 @@ const drsa_conv::Table* kTables[] = {&drsa_conv::kTableFwdA, &drsa_conv::kTableF
                                      &drsa_conv::kTableFwdD, &drsa_conv::kTableFwdE, &drsa_conv::kTableBwdA,
                                      &drsa_conv::kTableBwdB, &drsa_conv::kTableBwdC, &drsa_conv::kTableBwdcA,
                                      &drsa_conv::kTableBwdcB, &drsa_conv::kTableFwdBfA, &drsa_conv::kTableFwdBfB,
-                                     &drsa_conv::kTableFwdBfC};
+                                     &drsa_conv::kTableFwdBfC, &drsa_conv::kTableFwdP4};
 
 int pad32(int c) { return (c + 31) / 32 * 32; }
 
@@ -30,7 +30,7 @@ int env_int(const char* name, int dflt) {
   return v ? atoi(v) : dflt;
 }
 
-const Entry* find(int cin_p, int cout_p, int W, int ng, int amode, int epi, int et = 0) {
+const Entry* find(int cin_p, int cout_p, int W, int ng, int amode, int epi, int et = 0, int pw = 2) {
   int th = 8, tw, mw;
   static const int th16 = env_int("DRSA_AMD_CONV_TH16", 0);
   if (W >= 32) { tw = 32; mw = 8; th = (th16 && cout_p == 32 && ng <= 2 && epi != EPI_BWDC) ? 16 : 8; }
@@ -40,7 +40,7 @@ const Entry* find(int cin_p, int cout_p, int W, int ng, int amode, int epi, int 
     for (int i = 0; i < t->n; ++i) {
       const Entry& e = t->entries[i];
       if (e.cin_p == cin_p && e.cout_p == cout_p && e.th == th && e.tw == tw && e.mw == mw && e.ng == ng &&
-          e.amode == amode && e.epi == epi && e.et == et)
+          e.amode == amode && e.epi == epi && e.et == et && e.pw == pw)
         return &e;
     }
   return nullptr;
@@ -70,17 +70,19 @@ int drsa_amd_conv_fwd(const float* in, const float* wts, const float* bias, cons
   DRSA_REQUIRE(B > 0 && H > 0 && W > 0, "conv_fwd: bad shape");
   DRSA_REQUIRE(ng >= 1 && ng <= 3, "conv_fwd: ng must be 1..3");
   DRSA_REQUIRE(H % 2 == 0 && W % 2 == 0, "conv_fwd: H and W must be even (got %dx%d)", H, W);
+  DRSA_REQUIRE(pool >= 0 && pool <= 2, "conv_fwd: pool must be 0 (none), 1 (2x2) or 2 (2x4)");
   DRSA_REQUIRE(!pool || out_amax, "conv_fwd: pool needs out_amax");
   DRSA_REQUIRE(pool || W % 4 == 0, "conv_fwd: an unpooled output needs W %% 4 == 0 (float4 epilogue; got W=%d)", W);
+  DRSA_REQUIRE(pool != 2 || W % 4 == 0, "conv_fwd: a 2x4 pool needs W %% 4 == 0 (got W=%d)", W);
   const int cin_p = cin_pad(cin), cout_p = pad32(cout);
   const int first_generic = env_int("DRSA_AMD_CONV_FIRST_GENERIC", 0);   // per call: tests compare both paths
-  if (cin == 1 && pool && W % 8 == 0 && !first_generic) {
+  if (cin == 1 && pool == 1 && W % 8 == 0 && !first_generic) {
     ConvArgs a{};
     a.in = in; a.wts = wts; a.bias = bias; a.den_map = den_map; a.out = out; a.out_amax = out_amax;
     a.out_den = out_den; a.H = H; a.W = W; a.cin = cin; a.cout = cout; a.clones = 1;
     return drsa_first_conv_pool(a, cout_p, ng, B, (hipStream_t)stream);
   }
-  const Entry* e = find(cin_p, cout_p, W, ng, A_DENSE, pool ? EPI_FWD_POOL : EPI_FWD_RELU);
+  const Entry* e = find(cin_p, cout_p, W, ng, A_DENSE, pool ? EPI_FWD_POOL : EPI_FWD_RELU, 0, pool == 2 ? 4 : 2);
   if (!e) {
     drsa::set_error("conv_fwd: no kernel for cin=%d cout=%d W=%d ng=%d pool=%d", cin, cout, W, ng, pool);
     return DRSA_EUNSUPPORTED;
@@ -89,6 +91,13 @@ int drsa_amd_conv_fwd(const float* in, const float* wts, const float* bias, cons
   a.in = in; a.wts = wts; a.bias = bias; a.den_map = den_map; a.out = out; a.out_amax = out_amax;
   a.out_den = out_den; a.H = H; a.W = W; a.cin = cin; a.cout = cout; a.clones = 1;
   return launch(e, a, B, (hipStream_t)stream);
+}
+
+int drsa_amd_conv_fwd_has_kernel(int cin, int cout, int W, int ng, int pool, int bf16) {
+  if (cin == 1 && !bf16 && pool == 1) return 1;   // conv_first (W % 8 == 0) or the generic Cin = 1 kernels
+  if (pool < 0 || pool > 2 || ng < 1 || ng > 3 || (bf16 && cin == 1)) return 0;
+  return find(bf16 ? pad32(cin) : cin_pad(cin), pad32(cout), W, ng, A_DENSE, pool ? EPI_FWD_POOL : EPI_FWD_RELU, bf16 ? 1 : 0,
+              pool == 2 ? 4 : 2) != nullptr;
 }
 
 size_t drsa_amd_conv_weight_bf16_elems(int cin, int cout, int ng) {
@@ -102,10 +111,12 @@ int drsa_amd_conv_fwd_bf16(const float* in, const uint16_t* wts, const float* bi
   DRSA_REQUIRE(cin > 1, "conv_fwd_bf16: cin = 1 runs on drsa_amd_conv_fwd (fp32 VALU kernel)");
   DRSA_REQUIRE(ng >= 1 && ng <= 3, "conv_fwd_bf16: ng must be 1..3");
   DRSA_REQUIRE(H % 2 == 0 && W % 2 == 0, "conv_fwd_bf16: H and W must be even (got %dx%d)", H, W);
+  DRSA_REQUIRE(pool >= 0 && pool <= 2, "conv_fwd_bf16: pool must be 0 (none), 1 (2x2) or 2 (2x4)");
   DRSA_REQUIRE(!pool || out_amax, "conv_fwd_bf16: pool needs out_amax");
   DRSA_REQUIRE(pool || W % 4 == 0, "conv_fwd_bf16: an unpooled output needs W %% 4 == 0 (got W=%d)", W);
+  DRSA_REQUIRE(pool != 2 || W % 4 == 0, "conv_fwd_bf16: a 2x4 pool needs W %% 4 == 0 (got W=%d)", W);
   DRSA_REQUIRE(((uintptr_t)wts & 15) == 0, "conv_fwd_bf16: weights must be 16-byte aligned");
-  const Entry* e = find(pad32(cin), pad32(cout), W, ng, A_DENSE, pool ? EPI_FWD_POOL : EPI_FWD_RELU, 1);
+  const Entry* e = find(pad32(cin), pad32(cout), W, ng, A_DENSE, pool ? EPI_FWD_POOL : EPI_FWD_RELU, 1, pool == 2 ? 4 : 2);
   if (!e) {
     drsa::set_error("conv_fwd_bf16: no kernel for cin=%d cout=%d W=%d ng=%d pool=%d", cin, cout, W, ng, pool);
     return DRSA_EUNSUPPORTED;

@@ -46,6 +46,9 @@
 #ifndef DRSA_CONV_BWDC_WPE
 #define DRSA_CONV_BWDC_WPE 2
 #endif
+#ifndef DRSA_CONV_BF_WPE
+#define DRSA_CONV_BF_WPE 2
+#endif
 #ifndef DRSA_CONV_FWD_WPE
 #define DRSA_CONV_FWD_WPE 3
 #endif
@@ -90,7 +93,7 @@ constexpr int bf_stride(int hx) {
 // chain), 1 = bf16 (v_mfma_f32_32x32x16_bf16, forward only: conv inputs and weights rounded to
 // bf16 when staged, fp32 accumulation, fp32 outputs).  The bf16 chunk is 16 input channels = one
 // tap per MFMA (k = tap * 16 + ci); its halo is pixel-major, 8 channels per 16-byte pixel slot.
-template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI, int ET = 0>
+template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI, int ET = 0, int PW = 2>
 struct ConvCfg {
   static constexpr int CIN_ = CIN, COUT_ = COUT, TH_ = TH, TW_ = TW, MW_ = MW, CIC_ = CIC, NG_ = NG;
   static constexpr int AMODE_ = AMODE, EPI_ = EPI;
@@ -131,7 +134,8 @@ struct ConvCfg {
   static constexpr size_t lds_floats =
       (EPI == EPI_BWDC || staging_floats > epi_floats) ? staging_floats : epi_floats;
   // minimum waves per SIMD the register allocation must allow (1 block = 1 wave per SIMD)
-  static constexpr int WPE = EPI == EPI_BWDC ? DRSA_CONV_BWDC_WPE : (EPI == EPI_BWD && NG == 1) ? (SMALL_BWD ? 4 : DRSA_CONV_BWD_WPE)
+  static constexpr int WPE = BF ? (COUT <= 64 ? DRSA_CONV_BF_WPE : 1)
+                             : EPI == EPI_BWDC ? DRSA_CONV_BWDC_WPE : (EPI == EPI_BWD && NG == 1) ? (SMALL_BWD ? 4 : DRSA_CONV_BWD_WPE)
                              : (EPI != EPI_BWD && CIC <= 8 && COUT <= 32 && NG <= 2 ? DRSA_CONV_FWD_WPE : 1);
   // operand prefetch distance of the MFMA loop (k-steps)
   static constexpr int PD = DRSA_CONV_PD_BWD > 0 && EPI >= EPI_BWD ? DRSA_CONV_PD_BWD : 1;
@@ -140,6 +144,7 @@ struct ConvCfg {
   static_assert(CIN % CIC == 0, "CIN must be a multiple of the chunk");
   static_assert(MT % WM == 0 && NT % WN == 0 && WM * WN <= 4, "wave split");
   static_assert(!BF || (CIC == 16 && EPI < EPI_BWD && AMODE == A_DENSE), "bf16: dense forward, 16-channel chunks");
+  static_assert(PW == 2 || (PW == 4 && EPI == EPI_FWD_POOL), "2x4 pool windows: forward pool epilogue only");
 };
 
 // ---- staging of one input-channel chunk: registers <- global (load), LDS <- registers
@@ -507,9 +512,10 @@ __device__ __forceinline__ void mfma_chunk_bf(const uint4* hb, const uint4* wb, 
   }
 }
 
-template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI, int ET = 0>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AMODE, EPI, ET>::WPE))) void conv3x3_kernel(ConvArgs a) {
-  using Cfg = ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AMODE, EPI, ET>;
+// PW: pool window width of EPI_FWD_POOL (2 x PW windows; 4 = VGGish's (2,4) pool)
+template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI, int ET = 0, int PW = 2>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AMODE, EPI, ET, PW>::WPE))) void conv3x3_kernel(ConvArgs a) {
+  using Cfg = ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AMODE, EPI, ET, PW>;
   constexpr int HY = Cfg::HY, HX = Cfg::HX, RS = Cfg::RS, PLANE = Cfg::PLANE;
   constexpr int MTH = Cfg::MTH, MTW = Cfg::MTW, MTX = Cfg::MTX;
   constexpr int WM = Cfg::WM, MPW = Cfg::MPW, NPW = Cfg::NPW;
@@ -651,6 +657,22 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
     if (active && !(a.dbg & 4)) mfma_chunk<Cfg, Cfg::PD>(halo, wl, pix_off, lane, wn, acc);
   }
 
+  // the pool cells of the staged tile T (2 x PWc windows), one per thread and iteration `it`
+  // (it < CT; CT is sized for 2x2 cells, the most)
+  auto pool_cells = [&](auto pwc, auto&& fn) {
+    constexpr int PWc = decltype(pwc)::value;
+    constexpr int CW = TW / PWc, NC = TCH * (TH / 2) * CW;
+    const int H2 = H >> 1, W2 = W / PWc;
+#pragma unroll
+    for (int it = 0; it < CT; ++it) {
+      const int i = tid + it * kThreads;
+      if (i < NC) {
+        const int cl = i / ((TH / 2) * CW), rem = i % ((TH / 2) * CW);
+        const int cy = rem / CW, cx = rem % CW;
+        fn(it, cl, cy, cx, (ty0 >> 1) + cy, tx0 / PWc + cx, H2, W2);
+      }
+    }
+  };
 #pragma unroll
   for (int v = 0; v < NPW; ++v) {
     if constexpr (EPI == EPI_FWD_POOL || EPI == EPI_FWD_RELU) {
@@ -677,29 +699,58 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
       });
       int am_keep[CT];
       if constexpr (EPI == EPI_FWD_POOL) {
-        const int H2 = H >> 1, W2 = W >> 1;
-#pragma unroll
-        for (int it = 0; it < CT; ++it) {
-          const int i = tid + it * kThreads;
-          am_keep[it] = 0;
-          if (i < NCELL) {
-            const int cl = i / ((TH / 2) * (TW / 2)), rem = i % ((TH / 2) * (TW / 2));
-            const int cy = rem / (TW / 2), cx = rem % (TW / 2);
+        // 2 x PWc pool windows (PWc = PW: 2, or 4 for VGGish's (2,4) pool): first maximum
+        // in row-major window order, NaN wins (torch max_pool2d); argmax byte = row * PWc + col
+        auto pass0 = [&](auto pwc) {
+          constexpr int PWc = decltype(pwc)::value;
+          pool_cells(pwc, [&](int it, int cl, int cy, int cx, int qy, int qx, int H2, int W2) {
             const int co = gch(cl, v);
-            const int qy = (ty0 >> 1) + cy, qx = (tx0 >> 1) + cx;
-            const float* t = T + (cl * TH + 2 * cy) * TWP + 2 * cx;
-            const float yy[4] = {t[0], t[1], t[TWP], t[TWP + 1]};
-            // torch max_pool2d: first maximum in row-major window order; NaN wins
+            const float* t = T + (cl * TH + 2 * cy) * TWP + PWc * cx;
             int am = 0;
-            float m = yy[0];
+            float m = t[0];
 #pragma unroll
-            for (int s4 = 1; s4 < 4; ++s4)
-              if (yy[s4] > m || (yy[s4] != yy[s4] && m == m)) { m = yy[s4]; am = s4; }
+            for (int s4 = 1; s4 < 2 * PWc; ++s4) {
+              const float yv = t[(s4 / PWc) * TWP + s4 % PWc];
+              if (yv > m || (yv != yv && m == m)) { m = yv; am = s4; }
+            }
             am_keep[it] = am;
             if (co < a.cout && qy < H2 && qx < W2) {
               const size_t o = (((size_t)bq * a.cout + co) * H2 + qy) * W2 + qx;
               a.out[o] = m;
               a.out_amax[o] = (uint8_t)am;
+            }
+          });
+        };
+        if constexpr (PW == 4) {
+#pragma unroll
+          for (int it = 0; it < CT; ++it) am_keep[it] = 0;
+          pass0(std::integral_constant<int, 4>{});
+        } else {
+          // 2x2 (the GTZAN trunk): the original straight-line form (the generic lambda form costs
+          // the fp32 forward kernels ~2-10 %: one more spilled register)
+          const int H2 = H >> 1, W2 = W >> 1;
+#pragma unroll
+          for (int it = 0; it < CT; ++it) {
+            const int i = tid + it * kThreads;
+            am_keep[it] = 0;
+            if (i < NCELL) {
+              const int cl = i / ((TH / 2) * (TW / 2)), rem = i % ((TH / 2) * (TW / 2));
+              const int cy = rem / (TW / 2), cx = rem % (TW / 2);
+              const int co = gch(cl, v);
+              const int qy = (ty0 >> 1) + cy, qx = (tx0 >> 1) + cx;
+              const float* t = T + (cl * TH + 2 * cy) * TWP + 2 * cx;
+              const float yy[4] = {t[0], t[1], t[TWP], t[TWP + 1]};
+              int am = 0;
+              float m = yy[0];
+#pragma unroll
+              for (int s4 = 1; s4 < 4; ++s4)
+                if (yy[s4] > m || (yy[s4] != yy[s4] && m == m)) { m = yy[s4]; am = s4; }
+              am_keep[it] = am;
+              if (co < a.cout && qy < H2 && qx < W2) {
+                const size_t o = (((size_t)bq * a.cout + co) * H2 + qy) * W2 + qx;
+                a.out[o] = m;
+                a.out_amax[o] = (uint8_t)am;
+              }
             }
           }
         }
@@ -721,19 +772,33 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
       if (a.out_den && a.den_map) {
         // WSquare / Flat: input-independent map, read directly (coalesced) where it is stored
         if constexpr (EPI == EPI_FWD_POOL) {
-          const int H2 = H >> 1, W2 = W >> 1;
-#pragma unroll
-          for (int it = 0; it < CT; ++it) {
-            const int i = tid + it * kThreads;
-            if (i < NCELL) {
-              const int cl = i / ((TH / 2) * (TW / 2)), rem = i % ((TH / 2) * (TW / 2));
-              const int cy = rem / (TW / 2), cx = rem % (TW / 2);
+          auto gather_map = [&](auto pwc) {
+            constexpr int PWc = decltype(pwc)::value;
+            pool_cells(pwc, [&](int it, int cl, int, int, int qy, int qx, int H2, int W2) {
               const int co = gch(cl, v);
-              const int qy = (ty0 >> 1) + cy, qx = (tx0 >> 1) + cx;
               const int am = am_keep[it];
               if (co < a.cout && qy < H2 && qx < W2)
                 a.out_den[(((size_t)bq * a.cout + co) * H2 + qy) * W2 + qx] =
-                    a.den_map[((size_t)co * H + 2 * qy + (am >> 1)) * W + 2 * qx + (am & 1)];
+                    a.den_map[((size_t)co * H + 2 * qy + am / PWc) * W + PWc * qx + am % PWc];
+            });
+          };
+          if constexpr (PW == 4) {
+            gather_map(std::integral_constant<int, 4>{});
+          } else {
+            const int H2 = H >> 1, W2 = W >> 1;
+#pragma unroll
+            for (int it = 0; it < CT; ++it) {
+              const int i = tid + it * kThreads;
+              if (i < NCELL) {
+                const int cl = i / ((TH / 2) * (TW / 2)), rem = i % ((TH / 2) * (TW / 2));
+                const int cy = rem / (TW / 2), cx = rem % (TW / 2);
+                const int co = gch(cl, v);
+                const int qy = (ty0 >> 1) + cy, qx = (tx0 >> 1) + cx;
+                const int am = am_keep[it];
+                if (co < a.cout && qy < H2 && qx < W2)
+                  a.out_den[(((size_t)bq * a.cout + co) * H2 + qy) * W2 + qx] =
+                      a.den_map[((size_t)co * H + 2 * qy + (am >> 1)) * W + 2 * qx + (am & 1)];
+              }
             }
           }
         } else {
@@ -763,19 +828,33 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
           return acc[0][u][v][r] + b1[r];
         });
         if constexpr (EPI == EPI_FWD_POOL) {
-          const int H2 = H >> 1, W2 = W >> 1;
-#pragma unroll
-          for (int it = 0; it < CT; ++it) {
-            const int i = tid + it * kThreads;
-            if (i < NCELL) {
-              const int cl = i / ((TH / 2) * (TW / 2)), rem = i % ((TH / 2) * (TW / 2));
-              const int cy = rem / (TW / 2), cx = rem % (TW / 2);
+          auto gather_den = [&](auto pwc) {
+            constexpr int PWc = decltype(pwc)::value;
+            pool_cells(pwc, [&](int it, int cl, int cy, int cx, int qy, int qx, int H2, int W2) {
               const int co = gch(cl, v);
-              const int qy = (ty0 >> 1) + cy, qx = (tx0 >> 1) + cx;
               const int am = am_keep[it];
               if (co < a.cout && qy < H2 && qx < W2)
                 a.out_den[(((size_t)bq * a.cout + co) * H2 + qy) * W2 + qx] =
-                    T[(cl * TH + 2 * cy + (am >> 1)) * TWP + 2 * cx + (am & 1)];
+                    T[(cl * TH + 2 * cy + am / PWc) * TWP + PWc * cx + am % PWc];
+            });
+          };
+          if constexpr (PW == 4) {
+            gather_den(std::integral_constant<int, 4>{});
+          } else {
+            const int H2 = H >> 1, W2 = W >> 1;
+#pragma unroll
+            for (int it = 0; it < CT; ++it) {
+              const int i = tid + it * kThreads;
+              if (i < NCELL) {
+                const int cl = i / ((TH / 2) * (TW / 2)), rem = i % ((TH / 2) * (TW / 2));
+                const int cy = rem / (TW / 2), cx = rem % (TW / 2);
+                const int co = gch(cl, v);
+                const int qy = (ty0 >> 1) + cy, qx = (tx0 >> 1) + cx;
+                const int am = am_keep[it];
+                if (co < a.cout && qy < H2 && qx < W2)
+                  a.out_den[(((size_t)bq * a.cout + co) * H2 + qy) * W2 + qx] =
+                      T[(cl * TH + 2 * cy + (am >> 1)) * TWP + 2 * cx + (am & 1)];
+              }
             }
           }
         } else {
@@ -900,6 +979,7 @@ struct Entry {
   KernFn fn;
   size_t lds;
   int et = 0;   // operand type (ConvCfg ET)
+  int pw = 2;   // forward pool window width (ConvCfg PW)
 };
 
 #define CONV_ENTRY(CIN, COUT, TH, TW, MW, CIC, NG, AM, EP)                                                 \
@@ -911,6 +991,19 @@ struct Entry {
   drsa_conv::Entry{CIN, COUT, TH, TW, MW, 16, NG, drsa_conv::A_DENSE, EP,                                 \
                    drsa_conv::conv3x3_kernel<CIN, COUT, TH, TW, MW, 16, NG, drsa_conv::A_DENSE, EP, 1>,   \
                    drsa_conv::ConvCfg<CIN, COUT, TH, TW, MW, 16, NG, drsa_conv::A_DENSE, EP, 1>::lds_floats * sizeof(float), 1}
+
+// 2x4-pool forward (VGGish block 1, create_model.py:61): fp32 and bf16 operands
+#define CONV_ENTRY_P4(CIN, COUT, TH, TW, MW, CIC, NG, ET)                                                  \
+  drsa_conv::Entry{CIN, COUT, TH, TW, MW, CIC, NG, drsa_conv::A_DENSE, drsa_conv::EPI_FWD_POOL,           \
+                   drsa_conv::conv3x3_kernel<CIN, COUT, TH, TW, MW, CIC, NG, drsa_conv::A_DENSE, drsa_conv::EPI_FWD_POOL, ET, 4>, \
+                   drsa_conv::ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, drsa_conv::A_DENSE, drsa_conv::EPI_FWD_POOL, ET, 4>::lds_floats * sizeof(float), ET, 4}
+#define CONV_FAMILY_P4(CIN, COUT, CIC, NG, ET)                    \
+  CONV_ENTRY_P4(CIN, COUT, 16, 32, 8, CIC, NG, ET),                \
+  CONV_ENTRY_P4(CIN, COUT, 8, 32, 8, CIC, NG, ET),                 \
+  CONV_ENTRY_P4(CIN, COUT, 8, 16, 8, CIC, NG, ET),                 \
+  CONV_ENTRY_P4(CIN, COUT, 8, 8, 4, CIC, NG, ET)
+#define FWD_SET_P4(CIN, COUT, CIC, ET)                                                  \
+  CONV_FAMILY_P4(CIN, COUT, CIC, 1, ET), CONV_FAMILY_P4(CIN, COUT, CIC, 2, ET), CONV_FAMILY_P4(CIN, COUT, CIC, 3, ET)
 
 // tile by output width: W >= 32 -> 16x32 (32 output channels) or 8x32 (MW 8); 8 < W < 32 -> 8x16
 // (MW 8); W <= 8 -> 8x8 (MW 4)

@@ -480,7 +480,13 @@ class LRPEngine:
             need_den = st.den_kind is not None
             if st.den_kind == "ab" and li == capture and st.pool:
                 raise EngineError("engine: capture at the ReLU of an AlphaBeta conv is not supported")
-            if st.proj is None and st.pool and (li == capture or st.pool_k != (2, 2)):
+            # pools fused into the conv epilogue: 2x2 and 2x4 (code 1 / 2); others, and the capture
+            # layer (its full-resolution ReLU output is kept), go through maxpool_capture
+            fused_pool = {(2, 2): 1, (2, 4): 2}.get(st.pool_k) if st.pool else None
+            if fused_pool == 2 and not _capi.lib().drsa_amd_conv_fwd_has_kernel(
+                    st.cin, st.cout, w, st.ng_fwd, 2, int(self.bf16 and st.cin > 1)):
+                fused_pool = None
+            if st.proj is None and st.pool and (li == capture or fused_pool is None):
                 a = self._buf((li, "a"), (B, st.cout, h, w))
                 den_full = self._buf((li, "den_full"), (B, st.cout, h, w)) if need_den else None
                 self._conv_fwd(f"conv_fwd:{st.name}", st, False, cur, den_map, a, None, den_full, B, h, w, st.ng_fwd, 0, s)
@@ -492,16 +498,19 @@ class LRPEngine:
                 rec.update(a=a, y=out, amax=amax, den=den, Hout=h // ph, Wout=w // pw)
                 cur, h, w = out, h // ph, w // pw
             elif st.proj is None and st.pool:
-                out = self._buf((li, "y"), (B, st.cout, h // 2, w // 2))
-                amax = self._buf((li, "amax"), (B, st.cout, h // 2, w // 2), torch.uint8)
-                den = self._buf((li, "den"), (B, st.cout, h // 2, w // 2)) if need_den else None
-                self._conv_fwd(f"conv_fwd:{st.name}", st, False, cur, den_map, out, amax, den, B, h, w, st.ng_fwd, 1, s)
-                rec.update(y=out, amax=amax, den=den, Hout=h // 2, Wout=w // 2)
+                ph, pw = st.pool_k
+                out = self._buf((li, "y"), (B, st.cout, h // ph, w // pw))
+                amax = self._buf((li, "amax"), (B, st.cout, h // ph, w // pw), torch.uint8)
+                den = self._buf((li, "den"), (B, st.cout, h // ph, w // pw)) if need_den else None
+                self._conv_fwd(f"conv_fwd:{st.name}", st, False, cur, den_map, out, amax, den, B, h, w, st.ng_fwd,
+                               fused_pool, s)
+                rec.update(y=out, amax=amax, den=den, Hout=h // ph, Wout=w // pw)
                 if st.den_kind == "ab":   # second pass: den_n (y and argmax rewritten with the same values)
-                    den_n = self._buf((li, "den_n"), (B, st.cout, h // 2, w // 2))
-                    self._conv_fwd(f"conv_fwd_n:{st.name}", st, True, cur, None, out, amax, den_n, B, h, w, 2, 1, s)
+                    den_n = self._buf((li, "den_n"), (B, st.cout, h // ph, w // pw))
+                    self._conv_fwd(f"conv_fwd_n:{st.name}", st, True, cur, None, out, amax, den_n, B, h, w, 2,
+                                   fused_pool, s)
                     rec.update(den_n=den_n)
-                cur, h, w = out, h // 2, w // 2
+                cur, h, w = out, h // ph, w // pw
             else:
                 a = self._buf((li, "a"), (B, st.cout, h, w))
                 den = self._buf((li, "den"), (B, st.cout, h, w)) if need_den else None

@@ -99,9 +99,12 @@ int drsa_amd_subspace_relevances(const float* act, const float* ctx, int64_t B, 
 /* Floats of a prepared conv weight tensor [ng][9 * cin_p][cout_p]. */
 size_t drsa_amd_conv_weight_floats(int cin, int cout, int ng);
 
-/* Forward conv3x3 'same' + bias + ReLU [+ 2x2 max-pool with argmax] and the layer's LRP
+/* Forward conv3x3 'same' + bias + ReLU [+ max-pool with argmax] and the layer's LRP
  * denominator (Gamma: ng = 2 for x >= 0, where set 1 is applied to x as is, or ng = 3 with
  * the x+ / x- split; Epsilon: ng = 1; WSquare/Flat: den_map).
+ * pool: 0 = none (out and out_den at full resolution), 1 = 2x2, 2 = 2x4 (VGGish's (2,4) pool,
+ * create_model.py:61); pooled: out = window max, out_amax = row-major index of its first
+ * maximum (NaN wins, torch max_pool2d), out_den = the denominator at that pixel.
  * Replaces the model forward (create_model.py:91-97) plus the modified forwards zennit's
  * BasicHook re-runs in backward (attribute.py:98-107 via zennit.core.BasicHook). */
 int drsa_amd_conv_fwd(const float* in, const float* wts, const float* bias, const float* den_map, float* out,
@@ -117,6 +120,10 @@ int drsa_amd_conv_fwd(const float* in, const float* wts, const float* bias, cons
  * denominators) and every output is fp32, exactly as drsa_amd_conv_fwd.  cin > 1 only (the
  * Cin = 1 first layer stays on the fp32 kernel). */
 size_t drsa_amd_conv_weight_bf16_elems(int cin, int cout, int ng);
+
+/* 1 if drsa_amd_conv_fwd (bf16 = 0) / drsa_amd_conv_fwd_bf16 (bf16 = 1) has a kernel for this
+ * shape and pool mode, else 0 (callers then pool with drsa_amd_maxpool_capture). */
+int drsa_amd_conv_fwd_has_kernel(int cin, int cout, int W, int ng, int pool, int bf16);
 int drsa_amd_conv_fwd_bf16(const float* in, const uint16_t* wts, const float* bias, const float* den_map, float* out,
                            uint8_t* out_amax, float* out_den, int B, int cin, int cout, int H, int W, int ng,
                            int pool, void* stream);

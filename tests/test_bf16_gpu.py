@@ -61,7 +61,7 @@ def _run_kernel(x, sets, bias3, ng, pool):
     b3 = torch.zeros(3, cout_p)
     b3[:, :cout] = bias3
     b3 = b3.to(DEV)
-    Ho, Wo = (H // 2, W // 2) if pool else (H, W)
+    Ho, Wo = (H // 2, W // (4 if pool == 2 else 2)) if pool else (H, W)
     out = torch.full((B, cout, Ho, Wo), float("nan"), device=DEV)
     den = torch.full((B, cout, Ho, Wo), float("nan"), device=DEV)
     amax = torch.zeros((B, cout, Ho, Wo), dtype=torch.uint8, device=DEV) if pool else None
@@ -101,21 +101,27 @@ def test_conv_fwd_bf16_kernel(cin, cout, ng, W):
     bias3 = torch.randn(3, cout, generator=g) * 0.1
     y, den, sc = _ref(x, sets, bias3, ng)
     bound = KTOL * (sc + bias3.abs().sum(0).double()[None, :, None, None]) + 1e-30
-    for pool in (0, 1):
+    # pool 2 (2x4 windows, VGGish block 1) is instantiated for 64 -> 64
+    for pool in ((0, 1, 2) if (cin, cout) == (64, 64) else (0, 1)):
+        assert _capi.lib().drsa_amd_conv_fwd_has_kernel(cin, cout, W, ng, pool, 1) == 1
         out, dg, am = _run_kernel(x, sets, bias3, ng, pool)
         if not pool:
             assert torch.all((out.double() - y).abs() <= bound), (cin, cout, ng, W)
             assert torch.all((dg.double() - den).abs() <= bound)
             continue
-        win = y.reshape(B, cout, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, cout, H // 2, W // 2, 4)
-        bwin = bound.reshape(B, cout, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, cout, H // 2, W // 2, 4)
+        pw = 4 if pool == 2 else 2
+
+        def windows(t):
+            return t.reshape(B, cout, H // 2, 2, W // pw, pw).permute(0, 1, 2, 4, 3, 5).reshape(
+                B, cout, H // 2, W // pw, 2 * pw)
+        win, bwin = windows(y), windows(bound)
         ym, _ = win.max(-1)
         assert torch.all((out.double() - ym).abs() <= bwin.max(-1).values)
         top2 = win.topk(2, dim=-1).values
         clear = (top2[..., 0] - top2[..., 1]) > 2 * bwin.max(-1).values
         ref_am = win.argmax(-1)
         assert torch.equal(am.long()[clear], ref_am[clear])
-        dwin = den.reshape(B, cout, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, cout, H // 2, W // 2, 4)
+        dwin = windows(den)
         dref = torch.gather(dwin, -1, am.long()[..., None])[..., 0]
         bsel = torch.gather(bwin, -1, am.long()[..., None])[..., 0]
         assert torch.all((dg.double() - dref).abs() <= bsel)
