@@ -65,11 +65,14 @@ class HeatmapGenerator:
             # the reference returns numpy (explainer.py:111): D2H into fresh pinned buffers (torch's
             # caching host allocator), all copies queued on the stream, one wait
             info = {}
-            if input_batch.device.type == "cpu":
-                info["input"] = input_batch.detach().numpy()
+            inp = input_batch.detach()
+            if inp.dtype == torch.bfloat16:   # numpy has no bf16: the input as float32 (exact)
+                inp = inp.float()
+            if inp.device.type == "cpu":
+                info["input"] = inp.numpy()
             else:
-                info["input"] = torch.empty(input_batch.shape, dtype=input_batch.dtype, pin_memory=True)
-                info["input"].copy_(input_batch.detach(), non_blocking=True)
+                info["input"] = torch.empty(inp.shape, dtype=inp.dtype, pin_memory=True)
+                info["input"].copy_(inp, non_blocking=True)
             for k, v in out.items():
                 info[k] = torch.empty(v.shape, dtype=v.dtype, pin_memory=True)
                 info[k].copy_(v, non_blocking=True)

@@ -282,7 +282,9 @@ class Bf16Ops(TorchOps):
     """The bf16 plan's arithmetic (the reference has no bf16 path, so this is the
     definition the product's bf16 mode is checked against): every conv rounds its input and its
     (rule-modified) weights to bf16, in both directions, and accumulates in float64 here; biases,
-    dense layers, divisions and products with the activations stay at full precision."""
+    dense layers, divisions and products with the activations stay at full precision.  The
+    ProjectionModel GEMMs run as in the fp32 plan, in the kernels' pinned fp32 order (ExactOps):
+    the inverse projection's eps = 1e-6 division amplifies any other rounding at dead channels."""
     name = "bf16"
 
     @staticmethod
@@ -292,6 +294,10 @@ class Bf16Ops(TorchOps):
     @staticmethod
     def conv_t(m, x_shape, w, g):
         return TorchOps.conv_t(m, x_shape, _bf16r(w), g)
+
+    @staticmethod
+    def matmul(a, b):
+        return ExactOps.matmul(a, b).to(a.dtype)
 
 
 # "f64": the analytic structure evaluated in float64 (model and input promoted): the accuracy
@@ -608,11 +614,15 @@ def sort_subspaces(sub: np.ndarray, ops=TorchOps):
 @torch.no_grad()
 def subspace_heatmaps(proj_model: nn.Module, name_map: Dict[str, RuleSpec], K: int,
                       x: torch.Tensor, class_idx: int, one_hot_encoded=False,
-                      mode: str = "analytic") -> Dict[str, np.ndarray]:
-    """HeatmapGenerator.generate_subspace_heatmaps (explainer.py:87-123) on the CPU."""
+                      mode: str = "analytic", forced_inputs=None) -> Dict[str, np.ndarray]:
+    """HeatmapGenerator.generate_subspace_heatmaps (explainer.py:87-123) on the CPU.
+    ``forced_inputs``: per-sample layer inputs (see ``lrp``), replicated like the batch."""
     rules = class_composite_rules(name_map, K)
     xr = x.repeat_interleave(K + 1, dim=0)
-    _, R = lrp(proj_model, rules, xr, class_idx=class_idx, one_hot_encoded=one_hot_encoded, mode=mode)
+    if forced_inputs is not None:
+        forced_inputs = {k: v.repeat_interleave(K + 1, dim=0) for k, v in forced_inputs.items()}
+    _, R = lrp(proj_model, rules, xr, class_idx=class_idx, one_hot_encoded=one_hot_encoded, mode=mode,
+               forced_inputs=forced_inputs)
     H, W = R.shape[-2:]
     hm = R.reshape(-1, K + 1, H, W).numpy()
     std, sub = hm[:, 0:1], hm[:, 1:]

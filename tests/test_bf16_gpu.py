@@ -204,3 +204,39 @@ def test_vggish_bf16_capture_vs_oracle(layer_idx):
     _, _, (act_u, _) = lrp_ref.lrp(merged, spec(LRP_NAME_MAP_VGGISH), x.float(), class_idx=1, mode="bf16",
                                    capture=f"features.{layer_idx}")
     _rel_ok(a, act_u, 1e-3)
+
+
+def test_gtzan_bf16_heatmap_generator_vs_oracle():
+    """HeatmapGenerator (C3, j = 7, K = 4) on a bf16 model: the ProjectionModel plan with bf16 conv
+    forwards (the conv after the projection takes a signed input: NG = 3 on packed sign masks),
+    fp32 projection and backward.  Oracle teacher-forced on the engine's conv and projection
+    inputs, projection GEMMs in the kernels' pinned fp32 order (the inverse projection's
+    eps = 1e-6 amplifies any other rounding at dead channels, DESIGN D13); standard and
+    per-concept subspace heatmaps within 5e-3 relative L2 per sample."""
+    from drsa_audio_amd.engine import get_engine
+    from drsa_audio_amd.model.modify_model import ProjectionModel
+    from drsa_audio_amd.xai.explain.explainer import HeatmapGenerator
+    from lrp_common import u64
+    net = gtzan128().bfloat16()
+    x = logmel(3, seed=31).bfloat16()
+    hg = HeatmapGenerator(copy.deepcopy(net).to(DEV), u64(), LRP_NAME_MAP_GTZAN, "reggae", num_concepts=4,
+                          layer_idx=7, device="cuda")
+    hg.generate_subspace_heatmaps(x.to(DEV))
+    eng = get_engine(hg.projectionmodel, hg.composite)
+    assert eng.precision == "bf16"
+    assert any(st.ng_fwd == 3 and st.wts_fwd_bf is not None for st in eng.stages)
+    forced = {st.name: rec["in"].cpu() for st, rec in zip(eng.stages, eng.last["stages"])}
+    pm = ProjectionModel(copy.deepcopy(net).float(), 7, u64(), 4).eval()
+    # the projection's input: the engine's conv+ReLU output at the projection stage
+    pname = next(n for n, m in pm.features.named_children() if type(m).__name__ == "Projection")
+    li = next(i for i, st in enumerate(eng.stages) if st.proj is not None)
+    forced[f"features.{pname}"] = eng.last["stages"][li]["a"].cpu()
+    ref = lrp_ref.subspace_heatmaps(pm, spec(LRP_NAME_MAP_GTZAN), 4, x.float(), class_idx=4, mode="bf16",
+                                    forced_inputs=forced)
+    _rel_ok(torch.from_numpy(hg.info["standard_heatmaps"]), torch.from_numpy(ref["standard_heatmaps"]).double())
+
+    def unsort(o):
+        inv = np.argsort(o["mask"], axis=1)
+        return np.take_along_axis(o["subspace_heatmaps"], inv[:, :, None, None], 1)
+    for k in range(4):
+        _rel_ok(torch.from_numpy(unsort(hg.info)[:, k]), torch.from_numpy(unsort(ref)[:, k]).double())
