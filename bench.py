@@ -378,9 +378,34 @@ def drsa_sharded_bench(device, world, rank, steps=100):
     t = torch.tensor([time.perf_counter() - t0], device=device, dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t)
-    return {"config": f"row-sharded DRSA: {n} rows/rank x {world} ranks, d={d}, K={K}, all-reduce {d*d+K} fp32/step",
-            "ms_per_step": dt / steps * 1e3, "vector_steps_per_s": n * world * steps / dt, "steps": steps,
-            "objective_final": float(traj[-1])}
+    out = {"config": f"row-sharded DRSA: {n} rows/rank x {world} ranks, d={d}, K={K}, all-reduce {d*d+K} fp32/step",
+           "ms_per_step": dt / steps * 1e3, "vector_steps_per_s": n * world * steps / dt, "steps": steps,
+           "objective_final": float(traj[-1])}
+    # C5 on N GPUs: the two VGGish layers (j = 26, 33; d = 128, K = 16) row-sharded, one packed
+    # all-reduce of both partials per step (distributed.py::sharded_run_joint)
+    from drsa_audio_amd.xai.drsa.distributed import sharded_run_joint
+    d5, K5, s5 = 128, 16, 50
+    g = torch.Generator().manual_seed(5)
+    probs = []
+    for p_ in range(2):
+        A5, C5 = drsa_inputs(n, d5, 200 + 10 * rank + p_)
+        U5 = torch.linalg.qr(torch.randn(d5, d5, generator=g, dtype=torch.float64))[0].float()
+        probs.append((torch.from_numpy(A5).to(device), torch.from_numpy(C5).to(device), U5.to(device), K5))
+    sharded_run_joint(probs, 3)
+    torch.cuda.synchronize(device)
+    dist.barrier()
+    t0 = time.perf_counter()
+    res = sharded_run_joint(probs, s5)
+    torch.cuda.synchronize(device)
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt5 = float(t)
+    out["c5_joint"] = {"config": f"C5 joint, row-sharded: 2 problems x {n} rows/rank x {world} ranks, d={d5}, "
+                                 f"K={K5}, one all-reduce of 2 x {d5 * d5 + K5} fp32/step",
+                       "ms_per_joint_step": dt5 / s5 * 1e3, "steps": s5,
+                       "objective_final": [float(tr[-1]) for _, tr in res]}
+    return out
 
 
 # --------------------------------------------------------------------------- main
