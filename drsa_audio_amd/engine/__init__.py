@@ -6,7 +6,8 @@ engine itself keeps no strong reference to either), drops an entry as soon as it
 composite is garbage-collected, and keeps at most ``DRSA_AMD_ENGINE_CACHE`` (default 8) entries
 in LRU order; an evicted engine releases its device buffers.  So a workflow that builds a new
 ``HeatmapGenerator`` per pass (the reference does, cxai/xai/pixelflipping/cpf.py:161) keeps a
-bounded device footprint.
+bounded device footprint.  A composite that maps a module to a user-written ``Hook`` (its own
+``backward``) gets the autograd slow path ``HookedAutograd`` (``hooks.py``) instead of a plan.
 """
 from __future__ import annotations
 
@@ -14,6 +15,7 @@ import os
 import weakref
 from collections import OrderedDict
 
+from .hooks import HookedAutograd, has_custom_hooks
 from .plan import EngineError, LRPEngine
 
 _MAX = max(1, int(os.environ.get("DRSA_AMD_ENGINE_CACHE", "8")))
@@ -53,7 +55,9 @@ def get_engine(model, composite) -> LRPEngine:
             _CACHE.move_to_end(key)
             return e.eng
         _evict(key)          # stale: ids reused by new objects, or the weights changed
-    eng = LRPEngine(model, composite)
+    rules = composite.rules(model) if composite is not None else {}
+    # a composite with a user-written Hook (its own backward) cannot be compiled: autograd slow path
+    eng = HookedAutograd(model, composite) if has_custom_hooks(rules) else LRPEngine(model, composite)
     _CACHE[key] = _Entry(_ref(model), _ref(composite), fp, eng)
     weakref.finalize(model, _evict, key)
     if composite is not None:
@@ -72,4 +76,4 @@ def clear_cache() -> None:
         _evict(key)
 
 
-__all__ = ["LRPEngine", "EngineError", "get_engine", "cache_size", "clear_cache"]
+__all__ = ["LRPEngine", "HookedAutograd", "EngineError", "get_engine", "cache_size", "clear_cache"]

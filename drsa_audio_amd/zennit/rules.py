@@ -9,10 +9,11 @@ Semantics (reference name maps ``constants.py:27-51``):
   ZPlus(ε)     z = f(x+; W+, b+) + f(x-; W-, 0);  R_in = x+ ⊙ Jᵀ_{W+} g + x- ⊙ Jᵀ_{W-} g,
                g = R / stab_ε(z)   (conv layers; runs on the Gamma kernels with these sets)
   AlphaBeta(α, β, ε)  positive set (x+, W+, b+) + (x-, W-, 0), negative set (x+, W-, b-) + (x-, W+, 0),
-               one denominator per set; R_in = α·pos − β·neg (restated in oracle/lrp_ref.py and
-               pinned there by known-answer tests; not yet executed by the HIP engine)
-``AlphaBeta`` and ``Norm`` are accepted as descriptors but not executed by the HIP engine yet
-(compiling a composite that maps them raises ``EngineError``, a ``NotImplementedError``).
+               one denominator per set; R_in = α·pos − β·neg (HIP engine: convs with a non-negative
+               input; elsewhere compiling the composite raises ``EngineError``)
+  Norm(ε)      ≡ Epsilon(ε) on conv/dense layers
+A ``Hook`` subclass with its own ``backward`` (not a descriptor) runs on the autograd slow path
+(``engine/hooks.py``).
 """
 from __future__ import annotations
 
