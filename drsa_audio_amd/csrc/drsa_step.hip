@@ -34,6 +34,7 @@
 #define DRSA_PARTIAL_STAMP(slot)
 #endif
 
+#include <stdlib.h>
 #include <type_traits>
 
 namespace {
@@ -143,10 +144,15 @@ constexpr int partial_threads() { return PCfg<DP, DKP>::NT; }
 // VEC (d % 4 == 0): float4 row loads.  A compile-time choice: a runtime branch per prefetch slot
 // made the compiler wait for every outstanding load at each join, which serialised the slots and
 // defeated the prefetch of the next tile.
-template <int DP, int DKP, int DT, bool VEC>
-__global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_kernel(
-    const void* __restrict__ A_, const void* __restrict__ C_, int64_t N, int d, int K, int dk,
-    const float* __restrict__ U, float* __restrict__ partials, int64_t rb_total) {
+//
+// partial_core is the body; `pre()` runs after the first tile's loads are issued and before U is
+// read (the fused step computes U there, see drsa_fused_step_kernel), `uval(k, j, jp)` returns
+// U[k][j] (jp: its padded column), `mid()` runs after U is in registers and before the first LDS
+// tile store.
+template <int DP, int DKP, int DT, bool VEC, class Pre, class UVal, class Mid>
+__device__ __forceinline__ void partial_core(const void* __restrict__ A_, const void* __restrict__ C_, int64_t N,
+                                             int d, int K, int dk, float* __restrict__ partials, int64_t rb_total,
+                                             Pre pre, UVal uval, Mid mid) {
   using Cfg = PCfg<DP, DKP>;
   constexpr bool BF = DT != 0;   // 16-bit A/C (bf16 or fp16)
   constexpr int CW = Cfg::CW, CG = Cfg::CG, NCB = Cfg::NCB, NIB = Cfg::NIB, NW = Cfg::NW, NT = Cfg::NT;
@@ -240,6 +246,7 @@ __global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_ker
   DRSA_PARTIAL_STAMP(0);
   if (ntile > 0) load_tile(0);
   DRSA_PARTIAL_STAMP(1);
+  pre();
 
   // ---- embedded U for this wave's column group, in MFMA B-operand order (loads all independent,
   //      issued back to back, overlapping the tile loads above) ----
@@ -259,7 +266,7 @@ __global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_ker
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const int k = 16 * q + 4 * lg + t;
-          const float v = U[(size_t)(k < d ? k : 0) * d + j];   // clamped address, masked after
+          const float v = uval(k < d ? k : 0, j, jp);   // clamped address, masked after
           ureg[cb][q][t] = keep_or_zero(v, real && k < d);
         }
     } else {
@@ -268,7 +275,7 @@ __global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_ker
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) {
           const int k = 32 * q2 + 8 * lg + jj;
-          const float v = U[(size_t)(k < d ? k : 0) * d + j];
+          const float v = uval(k < d ? k : 0, j, jp);
           ubf[cb][q2][jj] = rne16<DT>(keep_or_zero(v, real && k < d));
         }
     }
@@ -285,6 +292,7 @@ __global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_ker
   const int nq_live = (d + 15) / 16;   // k chunks / Gt row blocks that can be nonzero
 
   DRSA_PARTIAL_STAMP(2);
+  mid();
   if (ntile > 0) store_tile();
   __syncthreads();
   DRSA_PARTIAL_STAMP(3);
@@ -435,6 +443,15 @@ __global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_ker
   DRSA_PARTIAL_STAMP(6);
 }
 
+template <int DP, int DKP, int DT, bool VEC>
+__global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_kernel(
+    const void* __restrict__ A_, const void* __restrict__ C_, int64_t N, int d, int K, int dk,
+    const float* __restrict__ U, float* __restrict__ partials, int64_t rb_total) {
+  partial_core<DP, DKP, DT, VEC>(
+      A_, C_, N, d, K, dk, partials, rb_total, [] {},
+      [&](int k, int j, int) { return U[(size_t)k * d + j]; }, [] {});
+}
+
 // ---------------------------------------------------------------------------
 // reduce: out[e] = sum_p partials[p][e] over the P workgroup slabs (row stride ES); fixed order:
 // 4 interleaved chains p = g, g + 4, ... combined in order g = 0..3 (deterministic, no atomics).
@@ -461,8 +478,51 @@ template <int DP>
 constexpr int polar_dim() { return DP < 32 ? 32 : DP; }
 template <int DP>
 constexpr size_t finish_lds() {
-  return (2 * (size_t)polar_dim<DP>() * ns_ld<polar_dim<DP>()>() + 64 + ns_scratch_floats<polar_dim<DP>()>()) *
-         sizeof(float);
+  // polar_ns16 (DP <= 64) needs no k-split scratch
+  constexpr int PD = polar_dim<DP>();
+  constexpr size_t scr = (PD <= 64 && DRSA_NS16) ? 0 : ns_scratch_floats<PD>();
+  return (2 * (size_t)PD * ns_ld<PD>() + 64 + scr) * sizeof(float);
+}
+
+// finish prologue: f = (mean_k sqrt(M_k))^2, M_k = sqrt(S_k / N) (evaluated in double from the fp32
+// sums), c_k = sqrt(f) / (K N M_k^1.5), and X = embed(U + Gt diag(c)): padded rows pair with the
+// padded columns through an identity block.  Returns f; X is built only when build_x.
+template <int DP>
+__device__ __forceinline__ double finish_prologue(const float* __restrict__ gs, double n_total, int d, int K, int DKP,
+                                                  const float* __restrict__ U, float* X, bool build_x,
+                                                  double* dterm, float* cvec, double* fsh) {
+  constexpr int PD = polar_dim<DP>(), NT = fin_threads<PD>(), LD = ns_ld<PD>();
+  const int tid = threadIdx.x;
+  const int dk = d / K;
+  if (tid < K) dterm[tid] = sqrt(sqrt((double)gs[DP * DP + tid] / n_total));
+  __syncthreads();
+  if (tid == 0) {
+    double sum = 0.0;
+    for (int k = 0; k < K; ++k) sum += dterm[k];
+    const double mean = sum / K;
+    *fsh = mean * mean;
+  }
+  __syncthreads();
+  const double f = *fsh;
+  if (tid < K) {
+    const double Mk = sqrt((double)gs[DP * DP + tid] / n_total);
+    cvec[tid] = (float)((Mk > 0.0) ? sqrt(f) / (K * n_total * Mk * sqrt(Mk)) : 0.0);
+  }
+  if (!build_x) return f;
+  __syncthreads();
+  // (loads from clamped addresses, pinned, so all of them are in flight at once: no exec branches)
+#pragma unroll
+  for (int q = 0; q < (PD * PD + NT - 1) / NT; ++q) {
+    const int e = tid + q * NT;
+    const int ip = e / PD, jp = e % PD, kc = jp / DKP, l = jp % DKP;
+    const bool real = e < PD * PD && ip < d && jp < DP && kc < K && l < dk;
+    const float u = U[real ? (size_t)ip * d + kc * dk + l : 0];
+    const float gv = gs[real ? ip * DP + jp : 0];
+    const float rv = keep_or_zero(u + gv * cvec[kc < K ? kc : 0], real);
+    const float v = ip < d ? rv : ((jp == pad_col(ip - d, K, dk, DKP)) ? 1.f : 0.f);
+    if (e < PD * PD) X[ip * LD + jp] = v;
+  }
+  return f;
 }
 
 // mode 0: full step (f, U_out = polar(U + G)); mode 1: objective only
@@ -482,38 +542,10 @@ __global__ __launch_bounds__(fin_threads<polar_dim<DP>()>()) void drsa_finish_ke
   __shared__ double fsh;
   const int tid = threadIdx.x;
   const int dk = d / K;
-  // f = (mean_k sqrt(M_k))^2, M_k = sqrt(S_k / N)  (evaluated in double from the fp32 sums)
-  if (tid < K) dterm[tid] = sqrt(sqrt((double)gs[DP * DP + tid] / n_total));
-  __syncthreads();
-  if (tid == 0) {
-    double sum = 0.0;
-    for (int k = 0; k < K; ++k) sum += dterm[k];
-    const double mean = sum / K;
-    fsh = mean * mean;
-  }
-  __syncthreads();
-  const double f = fsh;
-  if (tid < K) {
-    const double Mk = sqrt((double)gs[DP * DP + tid] / n_total);
-    cvec[tid] = (float)((Mk > 0.0) ? sqrt(f) / (K * n_total * Mk * sqrt(Mk)) : 0.0);
-  }
+  const double f = finish_prologue<DP>(gs, n_total, d, K, DKP, U, X, mode == 0, dterm, cvec, &fsh);
   const int slot = f_stride_by_counter ? *step_counter : 0;
   if (tid == 0) f_out[slot] = (float)f;
   if (mode == 1) return;
-  __syncthreads();
-  // X = embed(U + Gt diag(c)); padded rows pair with the padded columns through an identity block
-  // (loads from clamped addresses, pinned, so all of them are in flight at once: no exec branches)
-#pragma unroll
-  for (int q = 0; q < (PD * PD + NT - 1) / NT; ++q) {
-    const int e = tid + q * NT;
-    const int ip = e / PD, jp = e % PD, kc = jp / DKP, l = jp % DKP;
-    const bool real = e < PD * PD && ip < d && jp < DP && kc < K && l < dk;
-    const float u = U[real ? (size_t)ip * d + kc * dk + l : 0];
-    const float gv = gs[real ? ip * DP + jp : 0];
-    const float rv = keep_or_zero(u + gv * cvec[kc < K ? kc : 0], real);
-    const float v = ip < d ? rv : ((jp == pad_col(ip - d, K, dk, DKP)) ? 1.f : 0.f);
-    if (e < PD * PD) X[ip * LD + jp] = v;
-  }
   const int it = polar_run<PD>(X, T, red, scr, tol, max_iter);
   for (int e = tid; e < d * d; e += NT) {
     const int i = e / d, j = e % d;
@@ -523,6 +555,53 @@ __global__ __launch_bounds__(fin_threads<polar_dim<DP>()>()) void drsa_finish_ke
     if (iters_out) *iters_out = it;
     if (f_stride_by_counter) *step_counter = slot + 1;
   }
+}
+
+// One fused DRSA step for DP = 64 (C3, C4): every workgroup first finishes the PREVIOUS step
+// redundantly -- f and c from the reduced slab gs, X = embed(U + Gt diag(c)), the same polar -- so
+// U_next never leaves the CU before its partial uses it; workgroup 0 stores U_next and f(U).  The
+// first tile's A/C loads are issued before the polar and land under it; U_next goes from LDS into
+// the partial's registers.  Bit-identical to drsa_finish_kernel followed by drsa_partial_kernel
+// (same code, same inputs in every workgroup); one launch and the U round trip fewer per step.
+template <int DP, int DKP, bool VEC>
+__global__ __launch_bounds__(fin_threads<polar_dim<DP>()>()) void drsa_fused_step_kernel(
+    const float* __restrict__ A, const float* __restrict__ C, int64_t N, int d, int K, int dk,
+    const float* __restrict__ gs, double n_total, const float* __restrict__ U, float* __restrict__ U_out,
+    float* __restrict__ f_out, int* __restrict__ step_counter, float* __restrict__ partials, int64_t rb_total,
+    float tol, int max_iter) {
+  constexpr int PD = polar_dim<DP>(), NT = fin_threads<PD>(), LD = ns_ld<PD>();
+  static_assert(PCfg<DP, DKP>::NT == NT, "fused step: the partial and the polar use one thread count");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* X = smem;
+  float* T = X + PD * LD;
+  float* red = T + PD * LD;
+  float* scr = red + 64;
+  __shared__ double dterm[128];
+  __shared__ float cvec[128];
+  __shared__ double fsh;
+  auto pre = [&] {
+    const double f = finish_prologue<DP>(gs, n_total, d, K, DKP, U, X, true, dterm, cvec, &fsh);
+    polar_run<PD>(X, T, red, scr, tol, max_iter);   // ends with a barrier: X complete
+    if (blockIdx.x == 0) {
+      for (int e = threadIdx.x; e < d * d; e += NT) {
+        const int i = e / d, j = e % d;
+        U_out[e] = X[i * LD + (j / dk) * DKP + j % dk];
+      }
+      if (threadIdx.x == 0) {
+        const int slot = *step_counter;
+        f_out[slot] = (float)f;
+        *step_counter = slot + 1;
+      }
+    }
+  };
+  partial_core<DP, DKP, 0, VEC>(
+      A, C, N, d, K, dk, partials, rb_total, pre, [&](int k, int, int jp) { return X[k * LD + jp]; },
+      [] { __syncthreads(); });   // every wave has read U from X before the tile store overwrites it
+}
+
+template <int DP, int DKP>
+constexpr size_t fused_lds() {
+  return PCfg<DP, DKP>::lds_bytes > finish_lds<DP>() ? PCfg<DP, DKP>::lds_bytes : finish_lds<DP>();
 }
 
 // polar only (orthogonalize API): any d <= 128, embedded as diag(V, I) in DP = pow2ceil(max(32, d))
@@ -640,6 +719,53 @@ int dispatch_finish(const float* gs, double n_total, const Geom& g, const float*
 constexpr float kPolarTol = 4e-7f;
 constexpr int kPolarMaxIter = 40;
 
+int launch_reduce(const float* partials, const PartialPlan& pl, const Geom& g, float* gs_out, hipStream_t s) {
+  const size_t E = slab_floats(g), ES = slab_stride(g);
+  hipLaunchKernelGGL(drsa_reduce_kernel, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, s, partials, pl.grid, (int)E,
+                     (int)ES, gs_out);
+  DRSA_LAUNCH_CHECK();
+  return DRSA_OK;
+}
+
+// the fused step (drsa_fused_step_kernel) covers DP = 64 with concept blocks <= 16 wide (one
+// 1024-thread workgroup shape for the partial and the polar): C3 and C4.  DRSA_AMD_DRSA_FUSED=0
+// selects the three-launch step.
+bool fused_ok(const Geom& g) {
+  static const int on = getenv("DRSA_AMD_DRSA_FUSED") ? atoi(getenv("DRSA_AMD_DRSA_FUSED")) : 1;
+  return on && g.DP == 64 && g.DKp <= 16;
+}
+
+template <int DKP>
+int launch_fused(const float* A, const float* C, int64_t N, const Geom& g, const float* gs, const float* U,
+                 float* U_out, float* f_out, int* counter, float* partials, const PartialPlan& pl, hipStream_t s) {
+  auto kern = (g.d & 3) == 0 ? drsa_fused_step_kernel<64, DKP, true> : drsa_fused_step_kernel<64, DKP, false>;
+  const size_t lds = fused_lds<64, DKP>();
+  DRSA_SMEM(kern, lds);
+  hipLaunchKernelGGL(kern, dim3(pl.grid), dim3(fin_threads<64>()), lds, s, A, C, N, g.d, g.K, g.dk, gs, (double)N, U,
+                     U_out, f_out, counter, partials, pl.rb_total, kPolarTol, kPolarMaxIter);
+  DRSA_LAUNCH_CHECK();
+  return DRSA_OK;
+}
+
+// one fused step: gs (gradient slab at U) -> U_out = polar(U + G c), f(U) -> f_out[counter++],
+// partial slabs at U_out -> reduce -> gs
+int fused_step(const float* A, const float* C, int64_t N, const Geom& g, float* gs, const float* U, float* U_out,
+               float* f_out, int* counter, void* ws, hipStream_t s) {
+  const PartialPlan pl = plan_partial(N);
+  float* partials = (float*)ws;
+  int rc = DRSA_EUNSUPPORTED;
+  switch (g.DKp) {
+    case 1: rc = launch_fused<1>(A, C, N, g, gs, U, U_out, f_out, counter, partials, pl, s); break;
+    case 2: rc = launch_fused<2>(A, C, N, g, gs, U, U_out, f_out, counter, partials, pl, s); break;
+    case 4: rc = launch_fused<4>(A, C, N, g, gs, U, U_out, f_out, counter, partials, pl, s); break;
+    case 8: rc = launch_fused<8>(A, C, N, g, gs, U, U_out, f_out, counter, partials, pl, s); break;
+    case 16: rc = launch_fused<16>(A, C, N, g, gs, U, U_out, f_out, counter, partials, pl, s); break;
+    default: drsa::set_error("drsa fused step: unsupported d=%d K=%d", g.d, g.K); return rc;
+  }
+  if (rc) return rc;
+  return launch_reduce(partials, pl, g, gs, s);
+}
+
 // workspace layout: [partials grid*E] [gs E] [16 B pad]
 size_t ws_bytes(int64_t N, const Geom& g) {
   const PartialPlan pl = plan_partial(N);
@@ -667,11 +793,7 @@ int partial_impl(const void* A, const void* C, int64_t N, int d, int K, const fl
   float* partials = (float*)ws;
   int rc = dispatch_partial(A, C, N, g, U, partials, pl, s, dtype);
   if (rc) return rc;
-  const size_t ES = slab_stride(g);
-  hipLaunchKernelGGL(drsa_reduce_kernel, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, s, partials, pl.grid, (int)E,
-                     (int)ES, gs_out);
-  DRSA_LAUNCH_CHECK();
-  return DRSA_OK;
+  return launch_reduce(partials, pl, g, gs_out, s);
 }
 
 float* ws_gs(void* ws, int64_t N, const Geom& g) {
@@ -766,7 +888,15 @@ int drsa_amd_drsa_run(const float* A, const float* C, int64_t N, int d, int K, f
     if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) use_graph = 0;
   }
   DRSA_HIP(hipMemsetAsync(counter, 0, sizeof(int), s));
+  // fused: the gradient at U_0 first, then per step one fused launch (finish of the previous step
+  // + partial at the new U) and the slab reduce; the final objective reads the last gs
+  const bool fused = fused_ok(g);
+  if (fused) {
+    int rc = drsa_amd_drsa_partial(A, C, N, d, K, U_io, gs, ws, ws_size, stream);
+    if (rc) return rc;
+  }
   auto one = [&](const float* Uin, float* Uout) -> int {
+    if (fused) return fused_step(A, C, N, g, gs, Uin, Uout, f_traj, counter, ws, s);
     int rc = drsa_amd_drsa_partial(A, C, N, d, K, Uin, gs, ws, ws_size, stream);
     if (rc) return rc;
     return dispatch_finish(gs, (double)N, g, Uin, Uout, f_traj, counter, 1, 0, kPolarTol, kPolarMaxIter, nullptr, s);
@@ -804,8 +934,10 @@ int drsa_amd_drsa_run(const float* A, const float* C, int64_t N, int d, int K, f
     ++done;
   }
   // final objective -> f_traj[steps]
-  int rc = drsa_amd_drsa_partial(A, C, N, d, K, U_io, gs, ws, ws_size, stream);
-  if (rc) return rc;
+  if (!fused) {
+    int rc = drsa_amd_drsa_partial(A, C, N, d, K, U_io, gs, ws, ws_size, stream);
+    if (rc) return rc;
+  }
   return dispatch_finish(gs, (double)N, g, U_io, nullptr, f_traj, counter, 1, 1, kPolarTol, kPolarMaxIter, nullptr, s);
 }
 

@@ -62,7 +62,7 @@ constexpr size_t ns_scratch_floats() {
 }
 
 template <int DP>
-__device__ int polar_ns(float* X, float* T, float* red, float* scr, float tol, int max_iter) {
+__device__ __forceinline__ int polar_ns(float* X, float* T, float* red, float* scr, float tol, int max_iter) {
   constexpr int NT = fin_threads<DP>(), LD = ns_ld<DP>(), NB = DP / 32, NWV = NT / 64, KS = ns_ks<DP>();
   constexpr int NSYM = NB * (NB + 1) / 2, NFULL = NB * NB;
   constexpr int KR = DP / KS;                       // k range per task
@@ -213,7 +213,7 @@ __device__ int polar_ns(float* X, float* T, float* red, float* scr, float tol, i
 // LDS scratch round trip and no extra barrier per product).  16x16 D layout: lane l, reg r ->
 // row 4(l>>4) + r, col l&15; A/B operands: lane l holds k = k0 + (l>>4), row/col l&15.
 template <int DP>
-__device__ int polar_ns16(float* X, float* T, float* red, float tol, int max_iter) {
+__device__ __forceinline__ int polar_ns16(float* X, float* T, float* red, float tol, int max_iter) {
   constexpr int NT = fin_threads<DP>(), LD = ns_ld<DP>(), NB = DP / 16, NWV = NT / 64;
   constexpr int NSYM = NB * (NB + 1) / 2, NFULL = NB * NB;
   constexpr int TPR = NT / DP;
@@ -302,7 +302,7 @@ __device__ int polar_ns16(float* X, float* T, float* red, float tol, int max_ite
 
 // the production polar: 16x16 tiles below DP = 128, 32x32 (k-split where needed) otherwise
 template <int DP>
-__device__ int polar_run(float* X, float* T, float* red, float* scr, float tol, int max_iter) {
+__device__ __forceinline__ int polar_run(float* X, float* T, float* red, float* scr, float tol, int max_iter) {
   if constexpr (DP <= 64 && DRSA_NS16) return polar_ns16<DP>(X, T, red, tol, max_iter);
   else return polar_ns<DP>(X, T, red, scr, tol, max_iter);
 }

@@ -81,9 +81,11 @@ def rule_relevance(rule, m: nn.Module, x: torch.Tensor, R: torch.Tensor) -> torc
         if kind not in ("epsilon", "norm"):
             raise NotImplementedError(f"{type(rule).__name__} needs a Conv2d/Linear module (got {type(m).__name__})")
         eps = rule.epsilon if kind == "epsilon" else rule.stabilizer
+        # m.forward, not m(...): the module carries this path's hooks, and calling it would
+        # re-enter its own backward hook
         with torch.no_grad():
-            z = m(x)
-        return _grad([m], [x], [R / _stab(z, eps)])[0]
+            z = m.forward(x)
+        return _grad([m.forward], [x], [R / _stab(z, eps)])[0]
     w = m.weight.detach()
     b = None if m.bias is None or "bias" in zp else m.bias.detach()
     if "weight" in zp:
