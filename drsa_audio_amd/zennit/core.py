@@ -30,8 +30,9 @@ def _zero_params(zero_params) -> tuple:
 
 
 class Hook:
-    """Base of all rules (zennit.core.Hook).  Subclasses may override ``backward``; the
-    engine natively executes the hooks it knows (rules below and ``SubspaceHook``)."""
+    """Base of all rules (zennit.core.Hook).  The HIP plan executes the hooks it knows (the rule
+    descriptors and ``SubspaceHook``); a subclass that overrides ``backward`` runs on the
+    autograd slow path (``engine/hooks.py``), called as zennit calls it."""
 
     def __init__(self) -> None:
         self.stored_tensors = {}
