@@ -79,6 +79,38 @@ def test_graph_and_eager_runs_identical():
     assert torch.equal(U1, U2) and torch.equal(t1, t2)
 
 
+@pytest.mark.parametrize("N,d,K", [(20000, 64, 4), (9001, 64, 8), (3000, 48, 4), (777, 64, 16)])
+def test_fused_run_equals_partial_finish_loop_bitwise(N, d, K):
+    """drsa_run at DP = 64 takes the fused step (drsa_fused_step_kernel: the previous step's finish
+    redone in every workgroup, then the partial on the new U from LDS).  Its trajectory and U must
+    equal, bit for bit, the explicit three-launch loop of the partial and finish entry points."""
+    from drsa_audio_amd import _capi
+    from drsa_audio_amd.xai.drsa.drsa import DrsaWorkspace, drsa_run
+    steps = 6
+    A, C = drsa_inputs(N, d, 31)
+    Ag, Cg, Ug = _gpu(A, C, _u0(d, 8))
+    side = torch.cuda.Stream()   # a non-default stream: drsa_run replays its hipGraph
+    with torch.cuda.stream(side):
+        U_run, traj = drsa_run(Ag, Cg, Ug, K, steps)
+    torch.cuda.synchronize()
+    ws = DrsaWorkspace(N, d, K, DEV)
+    st = _capi.stream_ptr()
+    gs = ws.gs
+    f = torch.empty(steps + 1, device=DEV)
+    U = Ug.clone()
+    for t in range(steps + 1):
+        _capi.call("drsa_amd_drsa_partial", Ag.data_ptr(), Cg.data_ptr(), N, d, K, U.data_ptr(), gs.data_ptr(),
+                   ws.ptr, ws.nbytes, st)
+        U_new = torch.empty_like(U)
+        _capi.call("drsa_amd_drsa_finish", gs.data_ptr(), N, d, K, U.data_ptr(), U_new.data_ptr(),
+                   f[t:].data_ptr(), 1 if t == steps else 0, None, st)
+        if t < steps:
+            U = U_new
+    torch.cuda.synchronize()
+    assert torch.equal(torch.as_tensor(traj).to(f), f), (traj, f)
+    assert torch.equal(U_run, U)
+
+
 def test_deterministic_bitwise():
     from drsa_audio_amd.xai.drsa.drsa import drsa_step
     A, C = drsa_inputs(30000, 64, 5)
