@@ -203,6 +203,7 @@ class HookedAutograd:
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if x.device.type != "cuda":
             raise _capi.DrsaAmdError("input must be a GPU tensor")
+        self._remove()   # a forward without its backward must not leave its hooks attached
         self._x = x.detach().to(self.device, torch.float32).requires_grad_(True)
         self._handles = self._hooks()
         try:

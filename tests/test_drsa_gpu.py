@@ -79,9 +79,10 @@ def test_graph_and_eager_runs_identical():
     assert torch.equal(U1, U2) and torch.equal(t1, t2)
 
 
-@pytest.mark.parametrize("N,d,K", [(20000, 64, 4), (9001, 64, 8), (3000, 48, 4), (777, 64, 16)])
+@pytest.mark.parametrize("N,d,K", [(20000, 64, 4), (9001, 64, 8), (3000, 48, 4), (777, 64, 16), (20000, 128, 16),
+                                   (3000, 100, 4), (2048, 128, 8)])
 def test_fused_run_equals_partial_finish_loop_bitwise(N, d, K):
-    """drsa_run at DP = 64 takes the fused step (drsa_fused_step_kernel: the previous step's finish
+    """drsa_run at DP = 64 / 128 takes the fused step (drsa_fused_step_kernel: the previous step's finish
     redone in every workgroup, then the partial on the new U from LDS).  Its trajectory and U must
     equal, bit for bit, the explicit three-launch loop of the partial and finish entry points."""
     from drsa_audio_amd import _capi

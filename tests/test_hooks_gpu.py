@@ -114,3 +114,15 @@ def test_slow_path_refuses_host_input(net):
     comp = NameMapComposite(LRP_NAME_MAP_GTZAN + [(["features.1"], Doubling())])
     with pytest.raises(_capi.DrsaAmdError):
         compute_relevances(net, logmel(1), comp, class_idx=0)
+
+
+def test_slow_path_leaves_no_hooks_attached(net):
+    """A forward without its backward, then a full pass: no module keeps a hook afterwards."""
+    comp = NameMapComposite(LRP_NAME_MAP_GTZAN + [(["features.1"], Same())])
+    eng = get_engine(net, comp)
+    x = logmel(2, seed=3).to(DEV)
+    eng.forward(x)
+    eng.forward(x)
+    R = eng.backward(cls=torch.zeros(2, device=DEV, dtype=torch.int32))
+    assert torch.isfinite(R).all()
+    assert all(len(m._forward_hooks) == 0 and len(m._backward_hooks) == 0 for m in net.modules())
