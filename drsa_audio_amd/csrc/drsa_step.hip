@@ -587,10 +587,10 @@ __global__ __launch_bounds__(fin_threads<polar_dim<DP>()>()) void drsa_fused_ste
         const int i = e / d, j = e % d;
         U_out[e] = X[i * LD + (j / dk) * DKP + j % dk];
       }
-      if (threadIdx.x == 0) {
-        const int slot = *step_counter;
+      if (threadIdx.x == 0) {   // no counter: f_out[0]
+        const int slot = step_counter ? *step_counter : 0;
         f_out[slot] = (float)f;
-        *step_counter = slot + 1;
+        if (step_counter) *step_counter = slot + 1;
       }
     }
   };
@@ -736,34 +736,36 @@ bool fused_ok(const Geom& g) {
 }
 
 template <int DKP>
-int launch_fused(const float* A, const float* C, int64_t N, const Geom& g, const float* gs, const float* U,
-                 float* U_out, float* f_out, int* counter, float* partials, const PartialPlan& pl, hipStream_t s) {
+int launch_fused(const float* A, const float* C, int64_t N, double n_total, const Geom& g, const float* gs,
+                 const float* U, float* U_out, float* f_out, int* counter, float* partials, const PartialPlan& pl,
+                 hipStream_t s) {
   auto kern = (g.d & 3) == 0 ? drsa_fused_step_kernel<64, DKP, true> : drsa_fused_step_kernel<64, DKP, false>;
   const size_t lds = fused_lds<64, DKP>();
   DRSA_SMEM(kern, lds);
-  hipLaunchKernelGGL(kern, dim3(pl.grid), dim3(fin_threads<64>()), lds, s, A, C, N, g.d, g.K, g.dk, gs, (double)N, U,
+  hipLaunchKernelGGL(kern, dim3(pl.grid), dim3(fin_threads<64>()), lds, s, A, C, N, g.d, g.K, g.dk, gs, n_total, U,
                      U_out, f_out, counter, partials, pl.rb_total, kPolarTol, kPolarMaxIter);
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;
 }
 
-// one fused step: gs (gradient slab at U) -> U_out = polar(U + G c), f(U) -> f_out[counter++],
-// partial slabs at U_out -> reduce -> gs
-int fused_step(const float* A, const float* C, int64_t N, const Geom& g, float* gs, const float* U, float* U_out,
-               float* f_out, int* counter, void* ws, hipStream_t s) {
+// one fused step: gs (gradient slab at U over n_total rows) -> U_out = polar(U + G c), f(U) ->
+// f_out[counter++] (f_out[0] without a counter), partial slabs of the N local rows at U_out ->
+// reduce -> gs_out (gs_out may be gs: the reduce runs after every workgroup has read gs)
+int fused_step(const float* A, const float* C, int64_t N, double n_total, const Geom& g, const float* gs,
+               float* gs_out, const float* U, float* U_out, float* f_out, int* counter, void* ws, hipStream_t s) {
   const PartialPlan pl = plan_partial(N);
   float* partials = (float*)ws;
   int rc = DRSA_EUNSUPPORTED;
   switch (g.DKp) {
-    case 1: rc = launch_fused<1>(A, C, N, g, gs, U, U_out, f_out, counter, partials, pl, s); break;
-    case 2: rc = launch_fused<2>(A, C, N, g, gs, U, U_out, f_out, counter, partials, pl, s); break;
-    case 4: rc = launch_fused<4>(A, C, N, g, gs, U, U_out, f_out, counter, partials, pl, s); break;
-    case 8: rc = launch_fused<8>(A, C, N, g, gs, U, U_out, f_out, counter, partials, pl, s); break;
-    case 16: rc = launch_fused<16>(A, C, N, g, gs, U, U_out, f_out, counter, partials, pl, s); break;
+    case 1: rc = launch_fused<1>(A, C, N, n_total, g, gs, U, U_out, f_out, counter, partials, pl, s); break;
+    case 2: rc = launch_fused<2>(A, C, N, n_total, g, gs, U, U_out, f_out, counter, partials, pl, s); break;
+    case 4: rc = launch_fused<4>(A, C, N, n_total, g, gs, U, U_out, f_out, counter, partials, pl, s); break;
+    case 8: rc = launch_fused<8>(A, C, N, n_total, g, gs, U, U_out, f_out, counter, partials, pl, s); break;
+    case 16: rc = launch_fused<16>(A, C, N, n_total, g, gs, U, U_out, f_out, counter, partials, pl, s); break;
     default: drsa::set_error("drsa fused step: unsupported d=%d K=%d", g.d, g.K); return rc;
   }
   if (rc) return rc;
-  return launch_reduce(partials, pl, g, gs, s);
+  return launch_reduce(partials, pl, g, gs_out, s);
 }
 
 // workspace layout: [partials grid*E] [gs E] [16 B pad]
@@ -844,6 +846,21 @@ int drsa_amd_drsa_finish(const float* gs, int64_t N_total, int d, int K, const f
                          kPolarMaxIter, iters_out, (hipStream_t)stream);
 }
 
+int drsa_amd_drsa_fused_supported(int d, int K) { return fused_ok(geom(d, K)) ? 1 : 0; }
+
+int drsa_amd_drsa_fused_step(const float* A, const float* C, int64_t N, int d, int K, const float* gs,
+                             int64_t N_total, const float* U, float* U_out, float* f_out, float* gs_out, void* ws,
+                             size_t ws_size, void* stream) {
+  const Geom g = geom(d, K);
+  DRSA_REQUIRE(g.ok && fused_ok(g), "drsa_fused_step: unsupported d=%d K=%d (drsa_amd_drsa_fused_supported)", d, K);
+  DRSA_REQUIRE(N > 0 && N_total >= N, "drsa_fused_step: need 0 < N <= N_total");
+  DRSA_REQUIRE(A && C && gs && U && U_out && f_out && gs_out, "drsa_fused_step: null pointer");
+  DRSA_REQUIRE(U != U_out, "drsa_fused_step: U and U_out must not alias");
+  DRSA_REQUIRE(ws && ws_size >= ws_bytes(N, g), "drsa_fused_step: workspace too small");
+  DRSA_REQUIRE(((uintptr_t)A % 16) == 0 && ((uintptr_t)C % 16) == 0, "drsa_fused_step: A/C must be 16B aligned");
+  return fused_step(A, C, N, (double)N_total, g, gs, gs_out, U, U_out, f_out, nullptr, ws, (hipStream_t)stream);
+}
+
 int drsa_amd_drsa_step(const float* A, const float* C, int64_t N, int d, int K, const float* U,
                        float* U_out, float* f_out, void* ws, size_t ws_size, void* stream) {
   const Geom g = geom(d, K);
@@ -896,7 +913,7 @@ int drsa_amd_drsa_run(const float* A, const float* C, int64_t N, int d, int K, f
     if (rc) return rc;
   }
   auto one = [&](const float* Uin, float* Uout) -> int {
-    if (fused) return fused_step(A, C, N, g, gs, Uin, Uout, f_traj, counter, ws, s);
+    if (fused) return fused_step(A, C, N, (double)N, g, gs, gs, Uin, Uout, f_traj, counter, ws, s);
     int rc = drsa_amd_drsa_partial(A, C, N, d, K, Uin, gs, ws, ws_size, stream);
     if (rc) return rc;
     return dispatch_finish(gs, (double)N, g, Uin, Uout, f_traj, counter, 1, 0, kPolarTol, kPolarMaxIter, nullptr, s);

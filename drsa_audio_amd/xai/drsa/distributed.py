@@ -50,6 +50,17 @@ class HipBackend:
                    U_new.data_ptr(), self.f.data_ptr(), 0, None, _capi.stream_ptr(U.device))
         return U_new, self.f.clone()
 
+    def fused_supported(self) -> bool:
+        return bool(_capi.load().drsa_amd_drsa_fused_supported(self.d, self.K))
+
+    def fused(self, gs: torch.Tensor, N_total: int, U: torch.Tensor, U_out: torch.Tensor, f_out: torch.Tensor,
+              gs_out: torch.Tensor) -> None:
+        """finish(gs) -> U_out, f(U) -> f_out[0], then partial at U_out -> gs_out, in one launch
+        fewer (drsa_amd_drsa_fused_step); everything written into caller-owned buffers."""
+        _capi.call("drsa_amd_drsa_fused_step", self.A.data_ptr(), self.C.data_ptr(), self.A.size(0), self.d, self.K,
+                   gs.data_ptr(), int(N_total), U.data_ptr(), U_out.data_ptr(), f_out.data_ptr(), gs_out.data_ptr(),
+                   self.ws.ptr, self.ws.nbytes, _capi.stream_ptr(U.device))
+
     def objective(self, gs: torch.Tensor, N_total: int, U: torch.Tensor) -> torch.Tensor:
         _capi.call("drsa_amd_drsa_finish", gs.data_ptr(), int(N_total), self.d, self.K, U.data_ptr(), None,
                    self.f.data_ptr(), 1, None, _capi.stream_ptr(U.device))
@@ -65,6 +76,20 @@ def sharded_run(A_local: torch.Tensor, C_local: torch.Tensor, U0: torch.Tensor, 
     if dist.is_initialized():
         dist.all_reduce(n, op=dist.ReduceOp.SUM, group=group)
     N_total = int(n.item())
+    if getattr(backend, "fused_supported", lambda: False)() and A_local.size(0) > 0:
+        # fused steps: all-reduce(partials at U_t) -> [finish t + partial at U_t+1] -> ...; U ping-pongs
+        # between two buffers and f lands in its trajectory slot (no per-step allocation)
+        Ub = [U0.detach().clone().contiguous(), torch.empty_like(U0)]
+        traj_t = torch.empty(steps + 1, device=U0.device, dtype=torch.float32)
+        gs = backend.partial(Ub[0])
+        for t in range(steps):
+            if dist.is_initialized():
+                dist.all_reduce(gs, op=dist.ReduceOp.SUM, group=group)
+            backend.fused(gs, N_total, Ub[t % 2], Ub[(t + 1) % 2], traj_t[t:t + 1], gs)
+        if dist.is_initialized():
+            dist.all_reduce(gs, op=dist.ReduceOp.SUM, group=group)
+        traj_t[steps:] = backend.objective(gs, N_total, Ub[steps % 2])
+        return Ub[steps % 2], traj_t.cpu().numpy()
     U = U0.detach().clone().contiguous()
     traj: List[torch.Tensor] = []
     for _ in range(steps):

@@ -60,6 +60,18 @@ int drsa_amd_drsa_partial(const float* A, const float* C, int64_t N, int d, int 
 int drsa_amd_drsa_finish(const float* gs, int64_t N_total, int d, int K, const float* U, float* U_out,
                          float* f_out, int objective_only, int* iters_out, void* stream);
 
+/* One fused sharded step (row-sharded DRSA; drsa.py:84-106 split over ranks): from
+ * the ALL-REDUCED slab gs of the previous partials (N_total rows over all ranks) and the U they
+ * were taken at, U_out = polar(U + G diag(c)) and f(U) -> f_out[0]; then the partial of this
+ * rank's N rows at U_out -> gs_out (the next all-reduce's payload; may alias gs).  Equals
+ * drsa_amd_drsa_finish followed by drsa_amd_drsa_partial bit for bit, in one launch fewer.
+ * Available where drsa_amd_drsa_fused_supported(d, K) returns 1 (padded d = 64, block width
+ * <= 16: C3, C4); otherwise use the two-call form. */
+int drsa_amd_drsa_fused_supported(int d, int K);
+int drsa_amd_drsa_fused_step(const float* A, const float* C, int64_t N, int d, int K, const float* gs,
+                             int64_t N_total, const float* U, float* U_out, float* f_out, float* gs_out, void* ws,
+                             size_t ws_size, void* stream);
+
 /* One SubspaceOptimizer.run iteration (drsa.py:84-106): f_out[0] = f(U), U_out = new U. */
 int drsa_amd_drsa_step(const float* A, const float* C, int64_t N, int d, int K, const float* U,
                        float* U_out, float* f_out, void* workspace, size_t workspace_bytes, void* stream);

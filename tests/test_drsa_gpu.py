@@ -112,6 +112,24 @@ def test_fused_run_equals_partial_finish_loop_bitwise(N, d, K):
     assert torch.equal(U_run, U)
 
 
+def test_sharded_fused_step_equals_two_call_form_bitwise():
+    """sharded_run's fused path (drsa_amd_drsa_fused_step: finish + the next partial in one
+    launch, caller-owned buffers) equals the partial / finish two-call form bit for bit."""
+    from drsa_audio_amd.xai.drsa.distributed import HipBackend, sharded_run
+
+    class TwoCall(HipBackend):
+        def fused_supported(self):
+            return False
+
+    for N, d, K in ((9001, 64, 8), (3000, 48, 4)):
+        A, C = drsa_inputs(N, d, 41)
+        Ag, Cg, Ug = _gpu(A, C, _u0(d, 12))
+        assert HipBackend(Ag, Cg, d, K).fused_supported()
+        U1, t1 = sharded_run(Ag, Cg, Ug, K, 7)
+        U2, t2 = sharded_run(Ag, Cg, Ug, K, 7, backend=TwoCall(Ag, Cg, d, K))
+        assert np.array_equal(t1, t2) and torch.equal(U1, U2)
+
+
 def test_deterministic_bitwise():
     from drsa_audio_amd.xai.drsa.drsa import drsa_step
     A, C = drsa_inputs(30000, 64, 5)
