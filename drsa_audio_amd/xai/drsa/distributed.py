@@ -50,6 +50,12 @@ class HipBackend:
                    U_new.data_ptr(), self.f.data_ptr(), 0, None, _capi.stream_ptr(U.device))
         return U_new, self.f.clone()
 
+    def finish_into(self, gs: torch.Tensor, N_total: int, U: torch.Tensor, U_out: torch.Tensor,
+                    f_out: torch.Tensor) -> None:
+        """finish() into caller-owned buffers (f(U) -> f_out[0])."""
+        _capi.call("drsa_amd_drsa_finish", gs.data_ptr(), int(N_total), self.d, self.K, U.data_ptr(),
+                   U_out.data_ptr(), f_out.data_ptr(), 0, None, _capi.stream_ptr(U.device))
+
     def fused_supported(self) -> bool:
         return bool(_capi.load().drsa_amd_drsa_fused_supported(self.d, self.K))
 
@@ -121,6 +127,31 @@ def sharded_run_joint(problems, steps: int, group=None, backends=None):
     N_tot = [int(v) for v in n.tolist()]
     sizes = [b.slab_size() for b in backends]
     offs = np.concatenate([[0], np.cumsum(sizes)]).astype(int)
+    if all(isinstance(b, HipBackend) for b in backends):
+        # the partials land straight in their slices of ONE packed all-reduce buffer, U ping-pongs
+        # between preallocated buffers and f goes to its trajectory slot: no per-step allocation
+        packed = torch.empty(int(offs[-1]), device=dev, dtype=torch.float32)
+        for p, b in enumerate(backends):
+            b.gs = packed[offs[p]:offs[p + 1]]
+        Ub = [[U0.detach().clone().contiguous(), torch.empty_like(U0)] for _, _, U0, _ in problems]
+        tr = [torch.empty(steps + 1, device=dev, dtype=torch.float32) for _ in range(P)]
+
+        def reduce_all(Ucur):
+            for p in range(P):
+                backends[p].partial(Ucur[p])
+            if dist.is_initialized():
+                dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
+
+        for t in range(steps):
+            reduce_all([Ub[p][t % 2] for p in range(P)])
+            for p in range(P):
+                backends[p].finish_into(backends[p].gs, N_tot[p], Ub[p][t % 2], Ub[p][(t + 1) % 2], tr[p][t:t + 1])
+        reduce_all([Ub[p][steps % 2] for p in range(P)])
+        out = []
+        for p in range(P):
+            tr[p][steps:] = backends[p].objective(backends[p].gs, N_tot[p], Ub[p][steps % 2])
+            out.append((Ub[p][steps % 2], tr[p].cpu().numpy()))
+        return out
     Us = [U0.detach().clone().contiguous() for _, _, U0, _ in problems]
     trajs: List[List[torch.Tensor]] = [[] for _ in range(P)]
 

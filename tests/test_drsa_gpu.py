@@ -130,6 +130,38 @@ def test_sharded_fused_step_equals_two_call_form_bitwise():
         assert np.array_equal(t1, t2) and torch.equal(U1, U2)
 
 
+def test_sharded_joint_preallocated_equals_generic_loop_bitwise():
+    """sharded_run_joint with HIP backends (partials written into one packed all-reduce buffer,
+    preallocated U / trajectory) equals the generic backend loop bit for bit (C5 shapes)."""
+    from drsa_audio_amd.xai.drsa.distributed import HipBackend, sharded_run_joint
+
+    class Wrap:   # not a HipBackend: takes the generic loop
+        def __init__(self, b):
+            self.b = b
+
+        def slab_size(self):
+            return self.b.slab_size()
+
+        def partial(self, U):
+            return self.b.partial(U)
+
+        def finish(self, gs, N, U):
+            return self.b.finish(gs, N, U)
+
+        def objective(self, gs, N, U):
+            return self.b.objective(gs, N, U)
+
+    probs = []
+    for seed, (N, d, K) in enumerate(((3000, 128, 16), (2500, 64, 8))):
+        A, C = drsa_inputs(N, d, 60 + seed)
+        Ag, Cg, Ug = _gpu(A, C, _u0(d, 20 + seed))
+        probs.append((Ag, Cg, Ug, K))
+    fast = sharded_run_joint(probs, 5)
+    slow = sharded_run_joint(probs, 5, backends=[Wrap(HipBackend(A, C, U.size(0), K)) for A, C, U, K in probs])
+    for (U1, t1), (U2, t2) in zip(fast, slow):
+        assert np.array_equal(t1, t2) and torch.equal(U1, U2)
+
+
 def test_deterministic_bitwise():
     from drsa_audio_amd.xai.drsa.drsa import drsa_step
     A, C = drsa_inputs(30000, 64, 5)
