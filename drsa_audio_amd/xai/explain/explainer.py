@@ -59,6 +59,9 @@ class HeatmapGenerator:
             cls = torch.arange(self.num_classes, device=self.device, dtype=torch.int32).repeat_interleave(per)
         else:
             cls = torch.full((B,), self.class_idx, device=self.device, dtype=torch.int32)
+        if to_host and B >= 2 * self.host_chunk_min:
+            self._heatmaps_to_host_pipelined(eng, input_batch, x, cls, one_hot_encoded)
+            return
         out = eng.subspace_heatmaps(x, cls=cls, one_hot=one_hot_encoded)
         self.info_device = out
         if to_host:
@@ -78,6 +81,44 @@ class HeatmapGenerator:
                 info[k].copy_(v, non_blocking=True)
             torch.cuda.current_stream(self.device).synchronize()
             self.info = {k: (v.numpy() if torch.is_tensor(v) else v) for k, v in info.items()}
+
+    # to_host with a large batch: two halves, the second computed while the first one's results
+    # (and the input, which is ready at the start) cross PCIe on a side stream.  Every sample's
+    # results are independent of the batch it is computed in, so the output is bit-identical.
+    host_chunk_min = 128
+
+    def _heatmaps_to_host_pipelined(self, eng, input_batch, x, cls, one_hot):
+        B = x.size(0)
+        main = torch.cuda.current_stream(self.device)
+        if getattr(self, "_d2h_stream", None) is None:
+            self._d2h_stream = torch.cuda.Stream(self.device)
+        side = self._d2h_stream
+        inp = input_batch.detach()
+        if inp.dtype == torch.bfloat16:   # numpy has no bf16: the input as float32 (exact)
+            inp = inp.float()
+        info = {}
+        side.wait_stream(main)            # the input (and anything queued before) is ready
+        if inp.device.type == "cpu":
+            info["input"] = inp.numpy()
+        else:
+            info["input"] = torch.empty(inp.shape, dtype=inp.dtype, pin_memory=True)
+            with torch.cuda.stream(side):
+                info["input"].copy_(inp, non_blocking=True)
+        half = (B + 1) // 2
+        parts = []
+        for s0, s1 in ((0, half), (half, B)):
+            out = eng.subspace_heatmaps(x[s0:s1], cls=cls[s0:s1], one_hot=one_hot)
+            parts.append(out)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                for k, v in out.items():
+                    if k not in info:
+                        info[k] = torch.empty((B,) + tuple(v.shape[1:]), dtype=v.dtype, pin_memory=True)
+                    info[k][s0:s1].copy_(v, non_blocking=True)
+        self.info_device = {k: torch.cat([o[k] for o in parts]) for k in parts[0]}
+        side.synchronize()
+        main.synchronize()
+        self.info = {k: (v.numpy() if torch.is_tensor(v) else v) for k, v in info.items()}
 
     def obtain_heatmaps(self, input_batch: torch.Tensor, one_hot_encoded: bool = False,
                         flip_all_classes: bool = False) -> torch.Tensor:

@@ -283,6 +283,23 @@ def test_bench_size_properties(net):
         assert torch.equal(v, a[k][:3]), k
 
 
+@pytest.mark.parametrize("B", [256, 301])
+def test_to_host_pipelined_equals_device_results(net, B):
+    """to_host=True at B >= 256 computes two halves and copies the first (and the input) to the
+    host while the second computes: info (numpy) and info_device equal the one-shot device
+    results bit for bit (odd B too), and the input comes back unchanged."""
+    x = logmel(B, seed=51).to(DEV)
+    hg = HeatmapGenerator(_gpu_model(net), u64(), LRP_NAME_MAP_GTZAN, "rock", num_concepts=4, layer_idx=7)
+    hg.generate_subspace_heatmaps(x, to_host=False)
+    ref = {k: v.clone() for k, v in hg.info_device.items()}
+    hg.generate_subspace_heatmaps(x, to_host=True)
+    assert set(hg.info) == set(ref) | {"input"}
+    for k, v in ref.items():
+        assert torch.equal(hg.info_device[k], v), k
+        assert np.array_equal(hg.info[k], v.cpu().numpy()), k
+    assert np.array_equal(hg.info["input"], x.cpu().numpy())
+
+
 def test_large_batch_bit_exact_vs_oracle_sample(net):
     """B=96: two samples (first and last) of a large batch vs the exact oracle run on them alone."""
     x = logmel(96, seed=41)
