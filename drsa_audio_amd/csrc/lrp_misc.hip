@@ -7,6 +7,8 @@
 //   * denominator map of WSquare / Flat (input independent)
 //   * heatmap split / per-subspace sums / descending sort (explainer.py:99-176)
 #include "common.h"
+
+#include <stdlib.h>
 #include "lrp_conv.h"
 
 namespace {
@@ -896,6 +898,90 @@ __global__ __launch_bounds__(256) void heatmap_sort_kernel(const float* __restri
   }
 }
 
+// The same split / sums / sort with every map read ONCE: at K = 4 and H*W = 16384 (GTZAN-128, the
+// headline) each thread keeps its 16 float4 of the K subspace maps in registers (256 VGPRs, one
+// workgroup per CU; the kernel is HBM-bound) and copies the standard map while summing it, so the
+// sorted writes need no second read.  Sum order and outputs are those of heatmap_sort_kernel.
+template <int KC, int NV4>
+__global__ __launch_bounds__(256) void heatmap_sort_cached_kernel(const float* __restrict__ hm, float* __restrict__ std_out,
+                                                                  float* __restrict__ std_rel,
+                                                                  float* __restrict__ sub_out, float* __restrict__ rel,
+                                                                  int64_t* __restrict__ mask) {
+  constexpr int HW = NV4 * 1024;
+  __shared__ float red[KC + 1][4];
+  __shared__ float sums[KC + 1];
+  __shared__ int order[KC];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float4* base = reinterpret_cast<const float4*>(hm + (size_t)b * (KC + 1) * HW);
+  float4* so = reinterpret_cast<float4*>(std_out + (size_t)b * HW);
+  float4 v[KC][NV4];
+  float s[KC + 1];
+  {
+    float4 w[NV4];
+#pragma unroll
+    for (int j = 0; j < NV4; ++j) w[j] = base[tid + 256 * j];
+    float a = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV4; ++j) {
+      a += (w[j].x + w[j].y) + (w[j].z + w[j].w);
+      so[tid + 256 * j] = w[j];
+    }
+    s[0] = a;
+  }
+#pragma unroll
+  for (int q = 0; q < KC; ++q)
+#pragma unroll
+    for (int j = 0; j < NV4; ++j) v[q][j] = base[(size_t)(1 + q) * (HW / 4) + tid + 256 * j];
+#pragma unroll
+  for (int q = 0; q < KC; ++q) {
+    float a = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV4; ++j) a += (v[q][j].x + v[q][j].y) + (v[q][j].z + v[q][j].w);
+    s[1 + q] = a;
+  }
+#pragma unroll
+  for (int q = 0; q <= KC; ++q) {
+    float a = s[q];
+    for (int m = 32; m >= 1; m >>= 1) a += shfl_xor(a, m);
+    if (lane_id() == 0) red[q][wave_id()] = a;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int q = 0; q <= KC; ++q) sums[q] = (red[q][0] + red[q][1]) + (red[q][2] + red[q][3]);
+    // descending; ties: larger original index first
+    for (int k = 0; k < KC; ++k) order[k] = k;
+    for (int i = 1; i < KC; ++i) {
+      const int cur = order[i];
+      int j = i - 1;
+      while (j >= 0) {
+        const float a = sums[1 + order[j]], c = sums[1 + cur];
+        const bool before = (c > a) || (c == a && cur > order[j]);
+        if (!before) break;
+        order[j + 1] = order[j];
+        --j;
+      }
+      order[j + 1] = cur;
+    }
+    std_rel[b] = sums[0];
+    for (int k = 0; k < KC; ++k) {
+      rel[(size_t)b * KC + k] = sums[1 + order[k]];
+      mask[(size_t)b * KC + k] = order[k];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    const int src = order[k];   // uniform: the branch below is a scalar one
+    float4* dst = reinterpret_cast<float4*>(sub_out + ((size_t)b * KC + k) * HW);
+#pragma unroll
+    for (int q = 0; q < KC; ++q)
+      if (src == q) {
+#pragma unroll
+        for (int j = 0; j < NV4; ++j) dst[tid + 256 * j] = v[q][j];
+      }
+  }
+}
+
 // ===========================================================================
 // AlphaBeta (zennit 0.5.1 AlphaBeta, reference pf.py:289) on a conv with non-negative input,
 // around two plain backward convs (the x- terms vanish):
@@ -1103,8 +1189,13 @@ int drsa_amd_heatmap_sort(const float* hm, int B, int K, int HW, float* std_out,
                           float* rel, int64_t* mask, void* stream) {
   DRSA_REQUIRE(K >= 1 && K <= 64, "heatmap_sort: K must be in [1, 64]");
   DRSA_REQUIRE(HW % 4 == 0, "heatmap_sort: H*W must be a multiple of 4");
-  hipLaunchKernelGGL(heatmap_sort_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, hm, K, HW, std_out, std_rel,
-                     sub_out, rel, mask);
+  static const int no_cache = getenv("DRSA_AMD_SORT_GENERIC") ? atoi(getenv("DRSA_AMD_SORT_GENERIC")) : 0;
+  if (K == 4 && HW == 16384 && !no_cache)
+    hipLaunchKernelGGL((heatmap_sort_cached_kernel<4, 16>), dim3(B), dim3(256), 0, (hipStream_t)stream, hm, std_out,
+                       std_rel, sub_out, rel, mask);
+  else
+    hipLaunchKernelGGL(heatmap_sort_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, hm, K, HW, std_out, std_rel,
+                       sub_out, rel, mask);
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;
 }
