@@ -7,8 +7,11 @@ the whole hot path: forward, LRP backward with the K+1 relevance clones, split/s
 (HeatmapGenerator.info semantics), inputs resident in HBM, outputs left in HBM.
 
   python bench.py [--gpus N --steps K --warmup W --batch B]
-  (N>1: torchrun --nproc-per-node N; each rank explains its own batch, no collective on the
-   data path -> weak scaling; time = max over ranks.)
+  (N>1: either under torchrun --nproc-per-node N, or bench.py spawns the N ranks itself
+   (drsa_audio_amd/utils/launch.py) before any GPU call; each rank explains its own batch, no
+   collective on the data path -> weak scaling; time = max over ranks.  The N>1 run adds the
+   row-sharded DRSA leg (one RCCL all-reduce per step); every run has the task-parallel DRSA
+   grid leg (the reference's 90 independent problems spread over the ranks, strong scaling).)
 
 Also reported: per-kernel HIP-event timings of the dominant kernel (roofline), the standard
 LRP rate at bs=64 (C2), the DRSA step rate at C3 (N=20000, d=64, K=4) with its objective
@@ -408,7 +411,60 @@ def drsa_sharded_bench(device, world, rank, steps=100):
     return out
 
 
+def drsa_grid_bench(device, world, rank, steps=100, N=20000, classes=None):
+    """Task-parallel DRSA over the reference's problem grid (optsubspaces.py:17-23): 10 classes x
+    layers [19 (d=100), 26 (d=128), 33 (d=128)] x 3 runs = 90 independent problems, K=4, N rows
+    each (synthetic normalised A=|N(0,1)|, C~N(0,1)); LPT-assigned over the ranks, each rank's
+    problems advanced together in hipGraphs (drsa_run_multi).  Strong scaling: the grid is fixed.
+    The reference runs 5000 steps per problem; this leg times `steps` and projects."""
+    import torch.distributed as dist
+    from drsa_audio_amd.xai.drsa.cluster.optsubspaces import GTZAN_CLASSES, GTZAN_LAYERS, optimize_grid
+    from drsa_audio_amd.xai.drsa.preprocessing import normalize_vectors
+    classes = classes or GTZAN_CLASSES
+    dims = {19: 100, 26: 128, 33: 128}
+    g = torch.Generator(device=device).manual_seed(1234)
+    data = {}
+    for c in classes:
+        for l in GTZAN_LAYERS:
+            A = torch.randn(N, dims[l], device=device, generator=g).abs_()
+            C = torch.randn(N, dims[l], device=device, generator=g)
+            data[(c, l)] = (normalize_vectors(A, out=A), normalize_vectors(C, out=C))
+    optimize_grid(data, None, num_concepts=4, steps=2, device=device)        # graph instantiate / warm-up
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    res = optimize_grid(data, None, num_concepts=4, steps=steps, device=device)
+    torch.cuda.synchronize(device)
+    dt_rank = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    dts = [dt_rank]
+    if world > 1:
+        t = torch.zeros(world, device=device, dtype=torch.float64)
+        t[rank] = dt_rank
+        dist.all_reduce(t)
+        dts = t.tolist()
+    dt = max(dts)
+    P = len(res)
+    per_rank = {}
+    for k, v in res.items():
+        per_rank[v["rank"]] = per_rank.get(v["rank"], 0) + 1
+    return {"config": f"task-parallel DRSA grid: {len(classes)} classes x layers {list(GTZAN_LAYERS)} (d=100/128/128) "
+                      f"x 3 runs = {P} problems, K=4, N={N} each, {world} rank(s), LPT assignment, "
+                      "per-rank problems in one hipGraph (drsa_run_multi)",
+            "scaling": "strong", "steps": steps, "problems": P, "problems_per_rank": [per_rank.get(r, 0) for r in range(world)],
+            "problem_steps_per_s": P * steps / dt, "vector_steps_per_s": P * N * steps / dt,
+            "rank_seconds": dts,
+            "projected_full_grid_s": P * 5000 / (P * steps / dt),
+            "objective_final_min_max": [min(v["objective"] for v in res.values()),
+                                        max(v["objective"] for v in res.values())]}
+
+
 # --------------------------------------------------------------------------- main
+LEGS = ("c2", "drsa", "frontend", "joint", "vggish", "sharded", "grid", "to_host")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -419,24 +475,28 @@ def main():
     ap.add_argument("--no-drsa", action="store_true")
     ap.add_argument("--tag-order", default=None,
                     help="write the per-step kernel tag order (JSON) for scripts/tag_profile.py")
+    ap.add_argument("--grid-steps", type=int, default=100, help="steps of the task-parallel DRSA grid leg")
+    ap.add_argument("--grid-classes", type=int, default=10, help="classes of the DRSA grid (10 = the reference's)")
+    ap.add_argument("--legs", default="all",
+                    help="secondary legs to run: all, or a comma list of " + ",".join(LEGS))
     args = ap.parse_args()
+    legs = set(LEGS) if args.legs == "all" else set(args.legs.split(","))
+    if not legs <= set(LEGS):
+        ap.error(f"--legs: unknown {sorted(legs - set(LEGS))}")
+    if args.no_drsa:
+        legs -= {"drsa", "joint", "vggish", "sharded", "grid"}
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # rehearsal of the N > 1 path on a one-GPU box (tests only): every rank on cuda:0, gloo
-    if os.environ.get("DRSA_BENCH_ONE_DEVICE") == "1":
-        local = 0
+    # rehearsal of the N > 1 path on a one-GPU box (tests only): every rank on cuda:0, usually gloo
+    one_dev = os.environ.get("DRSA_BENCH_ONE_DEVICE") == "1"
     backend = os.environ.get("DRSA_BENCH_BACKEND", "nccl")   # nccl = RCCL on ROCm
+    from drsa_audio_amd.utils.launch import init_distributed, maybe_launch
+    # --gpus N without torchrun: fan out into N ranks here, before anything touches the GPU
+    maybe_launch(args.gpus, one_device=one_dev)
+    world, rank, device = init_distributed(backend, one_dev)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
+        if world != args.gpus:
+            log(f"[bench] note: WORLD_SIZE={world} but --gpus {args.gpus}; measuring {world} ranks")
 
     from drsa_audio_amd.utils.constants import LRP_NAME_MAP_GTZAN
     from drsa_audio_amd.xai.explain.explainer import HeatmapGenerator
@@ -462,10 +522,13 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    rank_ms = [dt / args.steps * 1e3]
     if world > 1:
-        t = torch.tensor([dt], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t)
+        t = torch.zeros(world, device=device, dtype=torch.float64)
+        t[rank] = dt
+        dist.all_reduce(t)                          # every rank's time; the job's time is the max
+        rank_ms = [v / args.steps * 1e3 for v in t.tolist()]
+        dt = max(t.tolist())
     ms = dt / args.steps * 1e3
     value = world * B * args.steps / dt
 
@@ -507,43 +570,49 @@ def main():
 
     log(f"[bench] headline {value:.0f} explained samples/s ({ms:.3f} ms/step); secondaries next")
     # ---- secondary: standard LRP (C2, bs=64) ----
-    from drsa_audio_amd.zennit.composites import NameMapComposite
-    from drsa_audio_amd.xai.explain.attribute import compute_relevances
-    comp = NameMapComposite(LRP_NAME_MAP_GTZAN)
-    x64 = synthetic_logmel(64, seed=7 + rank, device=device)
-    for _ in range(3):
-        compute_relevances(model, x64, comp, class_idx=3)
-    torch.cuda.synchronize(device)
-    t1 = time.perf_counter()
-    for _ in range(10):
-        compute_relevances(model, x64, comp, class_idx=3)
-    torch.cuda.synchronize(device)
-    c2 = 64 * 10 / (time.perf_counter() - t1)
-    # bs=64 explained samples (same path, C2 batch size)
-    x64b = x64
-    for _ in range(3):
-        hg.generate_subspace_heatmaps(x64b, to_host=False)
-    torch.cuda.synchronize(device)
-    t1 = time.perf_counter()
-    for _ in range(10):
-        hg.generate_subspace_heatmaps(x64b, to_host=False)
-    torch.cuda.synchronize(device)
-    bs64 = 64 * 10 / (time.perf_counter() - t1)
-
+    c2 = bs64 = None
+    if "c2" in legs:
+        from drsa_audio_amd.zennit.composites import NameMapComposite
+        from drsa_audio_amd.xai.explain.attribute import compute_relevances
+        comp = NameMapComposite(LRP_NAME_MAP_GTZAN)
+        x64 = synthetic_logmel(64, seed=7 + rank, device=device)
+        for _ in range(3):
+            compute_relevances(model, x64, comp, class_idx=3)
+        torch.cuda.synchronize(device)
+        t1 = time.perf_counter()
+        for _ in range(10):
+            compute_relevances(model, x64, comp, class_idx=3)
+        torch.cuda.synchronize(device)
+        c2 = 64 * 10 / (time.perf_counter() - t1)
+        # bs=64 explained samples (same path, C2 batch size)
+        x64b = x64
+        for _ in range(3):
+            hg.generate_subspace_heatmaps(x64b, to_host=False)
+        torch.cuda.synchronize(device)
+        t1 = time.perf_counter()
+        for _ in range(10):
+            hg.generate_subspace_heatmaps(x64b, to_host=False)
+        torch.cuda.synchronize(device)
+        bs64 = 64 * 10 / (time.perf_counter() - t1)
     drsa = None
-    if not args.no_drsa and rank == 0:
+    if "drsa" in legs and rank == 0:
         log("[bench] DRSA C3")
         drsa = drsa_bench(device)
     log("[bench] log-mel front end, DRSA C5 joint, VGGish")
-    frontend = frontend_bench(device) if rank == 0 else None
-    joint = drsa_joint_bench(device) if (rank == 0 and not args.no_drsa) else None
-    vgg = vggish_lrp_bench(device) if (rank == 0 and not args.no_drsa) else None
-    drsa_sharded = None
-    if not args.no_drsa and world > 1:
+    frontend = frontend_bench(device) if (rank == 0 and "frontend" in legs) else None
+    joint = drsa_joint_bench(device) if (rank == 0 and "joint" in legs) else None
+    vgg = vggish_lrp_bench(device) if (rank == 0 and "vggish" in legs) else None
+    drsa_sharded = grid = None
+    if "sharded" in legs and world > 1:
         drsa_sharded = drsa_sharded_bench(device, world, rank)
+    if "grid" in legs:
+        log("[bench] task-parallel DRSA grid")
+        from drsa_audio_amd.xai.drsa.cluster.optsubspaces import GTZAN_CLASSES
+        grid = drsa_grid_bench(device, world, rank, steps=args.grid_steps,
+                               classes=GTZAN_CLASSES[:max(1, args.grid_classes)])
     # the reference API returns numpy (explainer.py:111): the same steps with the D2H copy of info
     to_host = None
-    if rank == 0:
+    if rank == 0 and "to_host" in legs:
         log("[bench] to_host rate")
         for _ in range(2):
             hg.generate_subspace_heatmaps(x, to_host=True)
@@ -557,8 +626,14 @@ def main():
         to_host = {"explained_samples_per_s": B / th, "ms_per_step": th * 1e3,
                    "note": "generate_subspace_heatmaps(to_host=True): info dict as numpy (input + heatmaps + "
                            "relevances + mask copied D2H each step, PCIe-inclusive)"}
+    if world > 1:
+        # the other ranks leave before rank 0 times the CPU baseline, so nothing competes for the cores
+        dist.barrier()
+        dist.destroy_process_group()
+        if rank != 0:
+            return
     cpu = cpu_drsa = None
-    if not args.no_cpu_baseline and rank == 0 and world == 1:
+    if not args.no_cpu_baseline and rank == 0:
         cpu = cpu_baseline()
         cpu_drsa = cpu_drsa_baseline()
 
@@ -571,6 +646,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms,
+            "rank_ms_per_step": rank_ms,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -580,21 +656,23 @@ def main():
             "config": {"workload": "GTZAN-128 HeatmapGenerator: LRP (WSquare/Gamma/Epsilon name map) + DRSA "
                                    "subspace heatmaps, K=4 at layer j=7 (conv3 block, d=64), sorted info dict",
                        "global_batch": B * world, "per_gpu_batch": B, "input": "128x128 log-mel",
-                       "parallelism": f"data-parallel x{world} (no collective on the data path)"},
+                       "parallelism": f"data-parallel x{world} (no collective on the data path)",
+                       "launch": ("torchrun" if os.environ.get("TORCHELASTIC_RUN_ID") else
+                                  "bench.py --gpus (own launcher)" if world > 1 else "single process"),
+                       "one_device_rehearsal": one_dev, "backend": backend if world > 1 else None},
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": dom_ach, "peak": FP32_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": dom_ach / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic},
             "whole_path": {"algorithmic_gflop_per_sample": 2.0 * total_macs / B / 1e9,
                            "achieved_tflops": 2.0 * total_macs * value / B / world / 1e12},
             "kernels": kernels,
-            "secondary": {"standard_lrp_c2_bs64_samples_per_s": c2 * world,
-                          "explained_samples_per_s_bs64": bs64 * world, "drsa": drsa,
+            "secondary": {"standard_lrp_c2_bs64_samples_per_s": c2 and c2 * world,
+                          "explained_samples_per_s_bs64": bs64 and bs64 * world, "drsa": drsa,
                           "drsa_sharded": drsa_sharded, "drsa_joint_c5": joint, "vggish_lrp": vgg,
-                          "logmel_frontend": frontend, "to_host": to_host, "cpu_baseline_drsa_c3": cpu_drsa},
+                          "drsa_grid_task_parallel": grid, "logmel_frontend": frontend, "to_host": to_host,
+                          "cpu_baseline_drsa_c3": cpu_drsa},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -158,3 +158,114 @@ def test_shard_rows_partition():
             assert all(parts[i].stop == parts[i + 1].start for i in range(world - 1))
             sizes = [p.stop - p.start for p in parts]
             assert max(sizes) - min(sizes) <= 1
+
+
+# ---------------------------------------------------------------- task-parallel DRSA grid
+def _oracle_runner(problems, steps):
+    """float64 closed-form DRSA run per problem (drsa_ref), in the product runner's contract."""
+    import drsa_ref
+    out = []
+    for A, C, U0, K in problems:
+        A_, C_, U = A.double().numpy(), C.double().numpy(), U0.double().numpy()
+        traj = []
+        for _ in range(steps):
+            f, G, _, _ = drsa_ref.closed_form(A_, C_, U, K)
+            traj.append(f)
+            U = drsa_ref.polar(U + G)
+        traj.append(drsa_ref.closed_form(A_, C_, U, K)[0])
+        out.append((torch.from_numpy(U), np.asarray(traj)))
+    return out
+
+
+def _grid_data():
+    from gen_fixtures import drsa_inputs
+    data = {}
+    for ci, c in enumerate(("pop", "metal", "disco")):
+        for l, d in ((19, 12), (26, 16)):
+            A, C = drsa_inputs(60 + 7 * ci + l, d, 10 * ci + l)
+            data[(c, l)] = (torch.from_numpy(A), torch.from_numpy(C))
+    return data
+
+
+def _worker_grid(rank, world, port, root, steps, q):
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from drsa_audio_amd.xai.drsa.cluster.optsubspaces import optimize_grid
+    res = optimize_grid(_grid_data(), root, num_concepts=4, steps=steps, runs=3, runner=_oracle_runner)
+    q.put((rank, {k: (v["objective"], v["rank"]) for k, v in res.items()}))
+    dist.destroy_process_group()
+
+
+def test_assign_lpt_balanced_and_deterministic():
+    from drsa_audio_amd.xai.drsa.cluster.optsubspaces import GTZAN_CLASSES, assign, problem_grid
+    shapes = {(c, l): (20000, d) for c in GTZAN_CLASSES for l, d in ((19, 100), (26, 128), (33, 128))}
+    tasks = problem_grid(shapes, 3)
+    assert len(tasks) == 90 and len({t.key for t in tasks}) == 90
+    for world in (1, 2, 4, 8):
+        parts = assign(tasks, world)
+        assert sorted(t.key for p in parts for t in p) == sorted(t.key for t in tasks)
+        sizes = [len(p) for p in parts]
+        assert max(sizes) - min(sizes) <= 1          # d=100 pads to 128: equal costs
+        assert parts == assign(tasks, world)
+
+
+def test_task_parallel_grid_two_ranks_matches_sequential(tmp_path):
+    """optsubspaces grid over 2 gloo ranks: every (class, layer, run) problem equals the
+    sequential drsa.main schedule (same initial U per run), files as drsa.main writes them."""
+    import pickle
+    import pandas as pd
+    from drsa_audio_amd.xai.drsa.drsa import initial_projections
+    steps = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    root = str(tmp_path / "models")
+    procs = [ctx.Process(target=_worker_grid, args=(r, 2, port, root, steps, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == res[1] and len(res[0]) == 18
+    assert {r for _, r in res[0].values()} == {0, 1}
+    data = _grid_data()
+    for (c, l), (A, C) in data.items():
+        U0s = initial_projections(A.size(1), 3, 42)
+        for run in (1, 2, 3):
+            (U_ref, tr_ref), = _oracle_runner([(A, C, torch.tensor(U0s[run - 1], dtype=torch.float32), 4)], steps)
+            path = os.path.join(root, c, f"layer{l}", f"run{run}")
+            with open(os.path.join(path, "projection_matrix.pkl"), "rb") as fh:
+                U = pickle.load(fh)               # our own file (float32 numpy), written by this test
+            tr = pd.read_csv(os.path.join(path, "train_stats.csv"))["loss"].to_numpy()
+            assert U.dtype == np.float32 and np.array_equal(U, U_ref.numpy().astype(np.float32))
+            assert len(tr) == steps + 1 and np.allclose(tr, tr_ref, rtol=1e-6)
+            assert res[0][(c, l, run)][0] == float(tr_ref[-1])
+
+
+def test_launcher_spawns_ranks_and_forwards_rank0(tmp_path):
+    """utils/launch.spawn: N ranks with the torchrun environment, rank 0's stdout forwarded, a
+    failing rank's exit code returned."""
+    import subprocess
+    import sys
+    script = tmp_path / "w.py"
+    script.write_text(
+        "import os, sys\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "from drsa_audio_amd.utils.launch import maybe_launch, init_distributed\n"
+        "maybe_launch(int(sys.argv[1]), one_device=True)\n"
+        "import torch, torch.distributed as dist\n"
+        "world, rank, dev = init_distributed('gloo', one_device=True)\n"
+        "t = torch.tensor([rank + 1.0]); dist.all_reduce(t)\n"
+        "if rank == 0: print('SUM', world, float(t))\n"
+        "dist.destroy_process_group()\n"
+        "sys.exit(3 if len(sys.argv) > 2 and rank == 1 else 0)\n")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, str(script), "3"], env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip().splitlines()[-1] == "SUM 3 6.0"   # (gloo logs its connections to stdout)
+    r = subprocess.run([sys.executable, str(script), "2", "fail"], env=env, capture_output=True, text=True,
+                       timeout=180)
+    assert r.returncode == 3

@@ -1,0 +1,35 @@
+"""Task-parallel DRSA grid (xai/drsa/cluster/optsubspaces.py) on one GPU: every (class, layer,
+run) problem advanced in one joint hipGraph equals the same problem run alone with
+``drsa_run`` (the path ``drsa.main`` takes), bit for bit, and the run files are drsa.main's."""
+import os
+import pickle
+
+import numpy as np
+import pytest
+import torch
+
+from gen_fixtures import drsa_inputs
+
+
+@pytest.mark.gpu
+def test_optimize_grid_equals_sequential_drsa_run(tmp_path):
+    from drsa_audio_amd.xai.drsa.cluster.optsubspaces import optimize_grid
+    from drsa_audio_amd.xai.drsa.drsa import drsa_run, initial_projections
+    dev = torch.device("cuda:0")
+    data = {}
+    for ci, c in enumerate(("pop", "metal")):
+        for l, d in ((19, 100), (26, 128), (7, 64)):
+            A, C = drsa_inputs(3000 + 100 * ci + l, d, 7 * ci + l)
+            data[(c, l)] = (torch.from_numpy(A), torch.from_numpy(C))
+    steps = 6
+    res = optimize_grid(data, str(tmp_path), num_concepts=4, steps=steps, runs=3, device=dev, max_joint=7)
+    assert len(res) == 18
+    for (c, l), (A, C) in data.items():
+        Ag, Cg = A.to(dev), C.to(dev)
+        for run, U0 in enumerate(initial_projections(A.size(1), 3, 42), start=1):
+            U, tr = drsa_run(Ag, Cg, torch.tensor(U0, dtype=torch.float32, device=dev), 4, steps)
+            got = res[(c, l, run)]
+            assert np.array_equal(got["trajectory"], tr.cpu().numpy()), (c, l, run)
+            assert np.array_equal(got["U"], U.cpu().numpy())
+            with open(os.path.join(tmp_path, c, f"layer{l}", f"run{run}", "projection_matrix.pkl"), "rb") as fh:
+                assert np.array_equal(pickle.load(fh), U.cpu().numpy())   # our own file

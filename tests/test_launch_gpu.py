@@ -1,0 +1,32 @@
+"""bench.py --gpus N through its own launcher (utils/launch.py) on a one-GPU box: two ranks on
+cuda:0 over gloo run the explanation headline, the row-sharded DRSA leg and the task-parallel
+DRSA grid, and rank 0 reports n_gpus = 2 (VERDICT r02 'next' 1)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.gpu
+def test_bench_gpus2_own_launcher_one_device():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(DRSA_BENCH_ONE_DEVICE="1", DRSA_BENCH_BACKEND="gloo")
+    cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--batch", "16", "--steps", "2",
+           "--warmup", "1", "--no-cpu-baseline", "--legs", "sharded,grid", "--grid-steps", "4", "--grid-classes", "2"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 32
+    assert out["config"]["launch"].startswith("bench.py --gpus") and out["config"]["one_device_rehearsal"]
+    assert len(out["rank_ms_per_step"]) == 2 and out["ms_per_step"] == pytest.approx(max(out["rank_ms_per_step"]))
+    sec = out["secondary"]
+    assert sec["drsa_sharded"]["vector_steps_per_s"] > 0
+    g = sec["drsa_grid_task_parallel"]
+    assert g["problems"] == 18 and g["problems_per_rank"] == [9, 9] and g["scaling"] == "strong"
+    lo, hi = g["objective_final_min_max"]
+    assert 0 < lo <= hi
