@@ -842,45 +842,127 @@ __global__ void first_layer_den_kernel(const float* __restrict__ w2, const float
 //   std_out [B][HW], std_rel [B], sub_out [B][K][HW] sorted by descending relevance,
 //   rel [B][K] sorted, mask [B][K] int64 (numpy argsort(...)[..., ::-1] semantics:
 //   stable ascending order reversed, i.e. ties -> larger index first)
+//
+// The per-map relevance is the reference's numpy float32 sum over the last two axes
+// (explainer.py:161, :120): 0 + pairwise(map), numpy's pairwise summation -- n <= 8: a plain
+// left-to-right chain; n <= 128: eight strided accumulators r[j] = a[j] + a[8+j] + ... combined
+// as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the n % 8 tail; n > 128: split at
+// n2 = n/2 - (n/2 % 8) and add the two halves' sums.  For n = 128 * 2^m the leaves are the
+// 128-element blocks and the tree over them is balanced (a butterfly); other n take a serial
+// walk of the same recursion.  Bit-identical to numpy (pinned by tests/golden/lrp_pins_fixture).
 // ===========================================================================
+__device__ float pw_leaf(const float* a, int n) {   // numpy pairwise_sum for n <= 128
+  if (n < 8) {
+    float r = 0.f;
+    for (int i = 0; i < n; ++i) r = r + a[i];
+    return r;
+  }
+  float r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = a[j];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = r[j] + a[i + j];
+  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res = res + a[i];
+  return res;
+}
+
+__device__ float pw_serial(const float* a, int n) {   // the full recursion, one thread
+  struct Fr { int lo, n, state; float left; };
+  Fr st[32];
+  int sp = 0;
+  float ret = 0.f;
+  st[0] = {0, n, 0, 0.f};
+  while (sp >= 0) {
+    Fr& f = st[sp];
+    if (f.n <= 128) { ret = pw_leaf(a + f.lo, f.n); --sp; continue; }
+    int n2 = f.n / 2;
+    n2 -= n2 % 8;
+    if (f.state == 0) { f.state = 1; st[sp + 1] = {f.lo, n2, 0, 0.f}; ++sp; continue; }
+    if (f.state == 1) { f.state = 2; f.left = ret; st[sp + 1] = {f.lo + n2, f.n - n2, 0, 0.f}; ++sp; continue; }
+    ret = f.left + ret;
+    --sp;
+  }
+  return ret;
+}
+
+// half-leaf partial of the balanced case: thread (leaf L, half h) owns accumulators 4h..4h+3 of
+// leaf L; returns ((r_4h + r_4h+1) + (r_4h+2 + r_4h+3)) -- the leaf is the two halves' sum
+__device__ __forceinline__ float pw_half(const float4* leaf, int h) {
+  float4 r = leaf[h];
+#pragma unroll
+  for (int i = 1; i < 16; ++i) {
+    const float4 v = leaf[2 * i + h];
+    r.x = r.x + v.x; r.y = r.y + v.y; r.z = r.z + v.z; r.w = r.w + v.w;
+  }
+  return (r.x + r.y) + (r.z + r.w);
+}
+
+// numpy sum of one map by the whole workgroup (256 threads); part: >= 2 * min(n/128, 2048) floats
+// of LDS.  Result valid in every thread.  Contains barriers: call uniformly.
+__device__ float pw_sum_wg(const float* __restrict__ src, int n, float* part, float* bc) {
+  const int tid = threadIdx.x;
+  const int leaves = n / 128;
+  const bool bal = n > 128 && n % 128 == 0 && (leaves & (leaves - 1)) == 0 && leaves <= 2048;
+  if (bal) {
+    for (int t = tid; t < 2 * leaves; t += 256)
+      part[t] = pw_half(reinterpret_cast<const float4*>(src) + (size_t)(t >> 1) * 32, t & 1);
+    __syncthreads();
+    for (int w = 2 * leaves; w > 1; w >>= 1) {      // halves -> leaves -> balanced tree, adjacent pairs
+      float v[8];
+      int c = 0;
+      for (int t = tid; t < w / 2; t += 256) v[c++] = part[2 * t] + part[2 * t + 1];
+      __syncthreads();
+      c = 0;
+      for (int t = tid; t < w / 2; t += 256) part[t] = v[c++];
+      __syncthreads();
+    }
+    const float r = part[0];
+    __syncthreads();
+    return 0.f + r;
+  }
+  if (tid == 0) *bc = 0.f + pw_serial(src, n);
+  __syncthreads();
+  const float r = *bc;
+  __syncthreads();
+  return r;
+}
+
+__device__ void sort_desc(const float* sums, int K, int* order) {   // descending; ties: larger index first
+  for (int k = 0; k < K; ++k) order[k] = k;
+  for (int i = 1; i < K; ++i) {
+    const int cur = order[i];
+    int j = i - 1;
+    while (j >= 0) {
+      const float a = sums[1 + order[j]], c = sums[1 + cur];
+      const bool before = (c > a) || (c == a && cur > order[j]);
+      if (!before) break;
+      order[j + 1] = order[j];
+      --j;
+    }
+    order[j + 1] = cur;
+  }
+}
+
 __global__ __launch_bounds__(256) void heatmap_sort_kernel(const float* __restrict__ hm, int K, int HW,
                                                            float* __restrict__ std_out, float* __restrict__ std_rel,
                                                            float* __restrict__ sub_out, float* __restrict__ rel,
                                                            int64_t* __restrict__ mask) {
-  __shared__ float red[4];
+  __shared__ float part[4096];
+  __shared__ float bc;
   __shared__ float sums[65];
   __shared__ int order[64];
   const int b = blockIdx.x, tid = threadIdx.x;
   const float* base = hm + (size_t)b * (K + 1) * HW;
   for (int q = 0; q <= K; ++q) {
-    const float* src = base + (size_t)q * HW;
-    float s = 0.f;
-    for (int i = tid * 4; i < HW; i += 256 * 4) {
-      const float4 v = *reinterpret_cast<const float4*>(src + i);
-      s += (v.x + v.y) + (v.z + v.w);
-    }
-    for (int m = 32; m >= 1; m >>= 1) s += shfl_xor(s, m);
-    __syncthreads();
-    if (lane_id() == 0) red[wave_id()] = s;
-    __syncthreads();
-    if (tid == 0) sums[q] = (red[0] + red[1]) + (red[2] + red[3]);
+    const float s = pw_sum_wg(base + (size_t)q * HW, HW, part, &bc);
+    if (tid == 0) sums[q] = s;
   }
   __syncthreads();
   if (tid == 0) {
-    // descending; ties: larger original index first
-    for (int k = 0; k < K; ++k) order[k] = k;
-    for (int i = 1; i < K; ++i) {
-      const int cur = order[i];
-      int j = i - 1;
-      while (j >= 0) {
-        const float a = sums[1 + order[j]], c = sums[1 + cur];
-        const bool before = (c > a) || (c == a && cur > order[j]);
-        if (!before) break;
-        order[j + 1] = order[j];
-        --j;
-      }
-      order[j + 1] = cur;
-    }
+    sort_desc(sums, K, order);
     std_rel[b] = sums[0];
     for (int k = 0; k < K; ++k) {
       rel[(size_t)b * K + k] = sums[1 + order[k]];
@@ -899,69 +981,76 @@ __global__ __launch_bounds__(256) void heatmap_sort_kernel(const float* __restri
 }
 
 // The same split / sums / sort with every map read ONCE: at K = 4 and H*W = 16384 (GTZAN-128, the
-// headline) each thread keeps its 16 float4 of the K subspace maps in registers (256 VGPRs, one
-// workgroup per CU; the kernel is HBM-bound) and copies the standard map while summing it, so the
-// sorted writes need no second read.  Sum order and outputs are those of heatmap_sort_kernel.
+// headline) each thread keeps its 16 float4 of the K subspace maps in registers (one workgroup per
+// CU; the kernel is HBM-bound) and copies the standard map while loading it, so the sorted writes
+// need no second read.  The numpy pairwise sums need each accumulator chain (stride-8 elements of
+// one 128-element leaf) in one thread: every map goes through LDS once, stored at a leaf stride of
+// 136 floats so that both the coalesced float4 stores and the chain-ordered float4 reads of thread
+// (leaf t/2, half t%2) are bank-conflict-free.  Outputs equal heatmap_sort_kernel's.
 template <int KC, int NV4>
 __global__ __launch_bounds__(256) void heatmap_sort_cached_kernel(const float* __restrict__ hm, float* __restrict__ std_out,
                                                                   float* __restrict__ std_rel,
                                                                   float* __restrict__ sub_out, float* __restrict__ rel,
                                                                   int64_t* __restrict__ mask) {
   constexpr int HW = NV4 * 1024;
+  constexpr int LEAVES = HW / 128;        // 128 at 128x128: thread t = (leaf t/2, half t%2)
+  static_assert(LEAVES * 2 == 256, "cached sort: one (leaf, half) per thread");
+  constexpr int LS = 136;                  // padded leaf stride (floats)
+  __shared__ float4 lds4[LEAVES * LS / 4];
   __shared__ float red[KC + 1][4];
   __shared__ float sums[KC + 1];
   __shared__ int order[KC];
+  float* lds = reinterpret_cast<float*>(lds4);
   const int b = blockIdx.x, tid = threadIdx.x;
   const float4* base = reinterpret_cast<const float4*>(hm + (size_t)b * (KC + 1) * HW);
   float4* so = reinterpret_cast<float4*>(std_out + (size_t)b * HW);
   float4 v[KC][NV4];
   float s[KC + 1];
+  // float4 f = tid + 256 j  ->  leaf f / 32, offset 4 (f % 32)
+  auto stage = [&](const float4* w) {
+#pragma unroll
+    for (int j = 0; j < NV4; ++j) {
+      const int f = tid + 256 * j;
+      *reinterpret_cast<float4*>(lds + (f >> 5) * LS + 4 * (f & 31)) = w[j];
+    }
+  };
+  auto chain = [&]() -> float {
+    const float p = pw_half(reinterpret_cast<const float4*>(lds + (tid >> 1) * LS), tid & 1);
+    return p + shfl_xor(p, 1);           // the leaf (commutative: both halves get the same bits)
+  };
   {
     float4 w[NV4];
 #pragma unroll
     for (int j = 0; j < NV4; ++j) w[j] = base[tid + 256 * j];
-    float a = 0.f;
 #pragma unroll
-    for (int j = 0; j < NV4; ++j) {
-      a += (w[j].x + w[j].y) + (w[j].z + w[j].w);
-      so[tid + 256 * j] = w[j];
-    }
-    s[0] = a;
+    for (int j = 0; j < NV4; ++j) so[tid + 256 * j] = w[j];
+    stage(w);
   }
 #pragma unroll
   for (int q = 0; q < KC; ++q)
 #pragma unroll
     for (int j = 0; j < NV4; ++j) v[q][j] = base[(size_t)(1 + q) * (HW / 4) + tid + 256 * j];
+  __syncthreads();
+  s[0] = chain();
 #pragma unroll
   for (int q = 0; q < KC; ++q) {
-    float a = 0.f;
-#pragma unroll
-    for (int j = 0; j < NV4; ++j) a += (v[q][j].x + v[q][j].y) + (v[q][j].z + v[q][j].w);
-    s[1 + q] = a;
+    __syncthreads();
+    stage(v[q]);
+    __syncthreads();
+    s[1 + q] = chain();
   }
+  // balanced tree over the leaves: lanes 2L, 2L+1 hold leaf L; in-wave butterfly over L, then
+  // the four waves' (32-leaf) sums as (w0 + w1) + (w2 + w3)
 #pragma unroll
   for (int q = 0; q <= KC; ++q) {
     float a = s[q];
-    for (int m = 32; m >= 1; m >>= 1) a += shfl_xor(a, m);
+    for (int m = 2; m <= 32; m <<= 1) a = a + shfl_xor(a, m);
     if (lane_id() == 0) red[q][wave_id()] = a;
   }
   __syncthreads();
   if (tid == 0) {
-    for (int q = 0; q <= KC; ++q) sums[q] = (red[q][0] + red[q][1]) + (red[q][2] + red[q][3]);
-    // descending; ties: larger original index first
-    for (int k = 0; k < KC; ++k) order[k] = k;
-    for (int i = 1; i < KC; ++i) {
-      const int cur = order[i];
-      int j = i - 1;
-      while (j >= 0) {
-        const float a = sums[1 + order[j]], c = sums[1 + cur];
-        const bool before = (c > a) || (c == a && cur > order[j]);
-        if (!before) break;
-        order[j + 1] = order[j];
-        --j;
-      }
-      order[j + 1] = cur;
-    }
+    for (int q = 0; q <= KC; ++q) sums[q] = 0.f + ((red[q][0] + red[q][1]) + (red[q][2] + red[q][3]));
+    sort_desc(sums, KC, order);
     std_rel[b] = sums[0];
     for (int k = 0; k < KC; ++k) {
       rel[(size_t)b * KC + k] = sums[1 + order[k]];

@@ -131,7 +131,7 @@ def optimize_grid(datasets: Dict[Tuple[str, int], Tuple[torch.Tensor, torch.Tens
                 A, C = datasets[k]
                 dev_data[k] = (A.to(device, dtype).contiguous(), C.to(device, dtype).contiguous())
             A, C = dev_data[k]
-            U0 = torch.tensor(U0s[k][t.run - 1], dtype=torch.float32, device=device)   # drsa.py:285
+            U0 = torch.tensor(np.ascontiguousarray(U0s[k][t.run - 1]), dtype=torch.float32, device=device)  # drsa.py:285
             probs.append((A, C, U0, num_concepts))
         for t, (U, traj) in zip(chunk, runner(probs, steps)):
             U_np = U.detach().cpu().numpy()

@@ -74,3 +74,19 @@ def lrp_output_modifier(class_idx: int = None, num_classes: int = None, one_hot_
         mask = torch.repeat_interleave(torch.eye(num_classes, device=output.device, dtype=output.dtype), per, dim=0)
         return mask if one_hot_encoded else output * mask
     return attribute_all_classes
+
+
+def seed_class_indices(batch: int, class_idx: int = None, num_classes: int = None, device=None) -> torch.Tensor:
+    """The row -> attributed class map of ``lrp_output_modifier`` as int32 indices, the form the
+    fused seed of ``drsa_amd_linear_bwd`` takes: ``class_idx`` for every row, or (all-classes mode)
+    row b -> b // (batch / num_classes), the rows of ``repeat_interleave(eye(C), batch // C)``
+    (attribute.py:152).  A batch not divisible by num_classes raises, as the reference's mask
+    does (D8)."""
+    if class_idx is not None:
+        return torch.full((batch,), int(class_idx), device=device, dtype=torch.int32)
+    if num_classes is None:
+        raise ValueError("Provide either class_idx to attribute or num_classes")
+    per = batch // num_classes
+    if per * num_classes != batch:
+        raise ValueError(f"batch of {batch} is not divisible by num_classes={num_classes}")
+    return torch.arange(num_classes, device=device, dtype=torch.int32).repeat_interleave(per)

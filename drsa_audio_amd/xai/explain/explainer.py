@@ -25,7 +25,7 @@ from ...model.modify_model import ProjectionModel
 from ...utils.constants import CLASS_IDX_MAPPER, CLASS_IDX_MAPPER_TOY
 from ...zennit.composites import Composite, NameMapComposite
 from ...zennit.rules import Epsilon
-from .attribute import SubspaceHook, compute_relevances
+from .attribute import SubspaceHook, compute_relevances, seed_class_indices
 
 
 class HeatmapGenerator:
@@ -52,13 +52,8 @@ class HeatmapGenerator:
         x = input_batch.to(self.device, torch.float32).contiguous()
         eng = get_engine(self.projectionmodel, self.composite)
         B = x.size(0)
-        if flip_all_classes:
-            per = B // self.num_classes
-            if per * self.num_classes != B:
-                raise ValueError("flip_all_classes needs a batch divisible by the number of classes")
-            cls = torch.arange(self.num_classes, device=self.device, dtype=torch.int32).repeat_interleave(per)
-        else:
-            cls = torch.full((B,), self.class_idx, device=self.device, dtype=torch.int32)
+        cls = seed_class_indices(B, None if flip_all_classes else self.class_idx,
+                                 self.num_classes if flip_all_classes else None, self.device)
         if to_host and B >= 2 * self.host_chunk_min:
             self._heatmaps_to_host_pipelined(eng, input_batch, x, cls, one_hot_encoded)
             return

@@ -328,8 +328,129 @@ def main():
     print("fixtures written to", OUT)
 
 
+# ------------------------------------------------------------------ round 3: zennit-free LRP pins
+# sort_subspaces cases (B, K, H, W, seed); the reference squeezes the batch dim away at B = 1 (D7)
+SORT_CASES = [(3, 4, 128, 128, 1), (2, 4, 64, 64, 2), (2, 4, 128, 256, 3), (4, 8, 32, 32, 4), (3, 2, 36, 52, 5),
+              (5, 4, 16, 16, 6), (2, 16, 8, 8, 7), (3, 4, 6, 6, 8), (2, 4, 2, 2, 9), (6, 3, 20, 20, 10)]
+
+
+def sort_inputs(B: int, K: int, H: int, W: int, seed: int) -> np.ndarray:
+    """Heatmaps [B, K+1, H, W] (standard first): signed, heavy-tailed values; in the first case
+    sample 1 is all zeros (every concept ties) and sample 2's concept 3 duplicates concept 1."""
+    rng = np.random.default_rng(7000 + seed)
+    hm = (rng.standard_normal((B, K + 1, H, W)) * np.exp(rng.standard_normal((B, K + 1, 1, 1)))).astype(np.float32)
+    if seed == 1:
+        hm[1] = 0.0
+        hm[2, 3] = hm[2, 1]
+    return hm
+
+
+def _lrp_pins():
+    """Reference functions executed from their source text (zennit is only imported at module level):
+    lrp_output_modifier (attribute.py:111-160), SubspaceHook.backward (attribute.py:42-60) and
+    HeatmapGenerator.sort_subspaces (explainer.py:151-176), plus the standard relevance line
+    (explainer.py:120, a numpy sum over the last two axes)."""
+    import ast
+    from typing import Tuple
+    ns = _extract("cxai/xai/explain/attribute.py", {"lrp_output_modifier"}, {"torch": torch, "Tuple": Tuple})
+    out = {}
+    rng = np.random.default_rng(11)
+    logits = (rng.standard_normal((20, 10)) * 3).astype(np.float32)
+    out["seed_logits"] = logits
+    for tag, kw in {"cls3": dict(class_idx=3), "cls0_onehot": dict(class_idx=0, one_hot_encoded=True),
+                    "all10": dict(num_classes=10), "all10_onehot": dict(num_classes=10, one_hot_encoded=True),
+                    "cls9": dict(class_idx=9)}.items():
+        out[f"seed_{tag}"] = ns["lrp_output_modifier"](**kw)(torch.from_numpy(logits)).numpy()
+    try:                                           # D8: the all-classes mask needs B % num_classes == 0
+        ns["lrp_output_modifier"](num_classes=10)(torch.from_numpy(logits[:16]))
+        out["seed_all10_b16_raises"] = np.array(0)
+    except RuntimeError:
+        out["seed_all10_b16_raises"] = np.array(1)
+
+    # SubspaceHook.backward: the method body needs only self.num_concepts / self.device
+    tree = ast.parse(pathlib.Path(REF, "cxai/xai/explain/attribute.py").read_text())
+    cls = next(n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == "SubspaceHook")
+    fn = next(n for n in cls.body if isinstance(n, ast.FunctionDef) and n.name == "backward")
+    hns = {"torch": torch, "Tuple": Tuple}
+    exec(compile(ast.Module(body=[fn], type_ignores=[]), "attribute.py", "exec"), hns)
+    # n = 64 pixels (8 x 8, a shape the projection kernels take); small integers, exact under the
+    # U = I identities the GPU test uses, and compressible
+    for tag, (b, n, K, dk) in {"k4": (2, 64, 4, 4), "k2": (1, 64, 2, 8), "k8": (1, 64, 8, 4),
+                               "k5": (1, 64, 5, 4)}.items():
+        g = rng.integers(-64, 65, (b * (K + 1), n, K, dk)).astype(np.float32)
+        self_ = types.SimpleNamespace(num_concepts=K, device=torch.device("cpu"))
+        res, = hns["backward"](self_, None, None, (torch.from_numpy(g.copy()),))
+        out[f"hook_{tag}_in"] = g
+        out[f"hook_{tag}_out"] = res.numpy()
+
+    # sort_subspaces (a method; self is unused by the body)
+    ecls = next(n for n in ast.parse(pathlib.Path(REF, "cxai/xai/explain/explainer.py").read_text()).body
+                if isinstance(n, ast.ClassDef) and n.name == "HeatmapGenerator")
+    fn = next(n for n in ecls.body if isinstance(n, ast.FunctionDef) and n.name == "sort_subspaces")
+    sns = {"np": np, "Tuple": Tuple}
+    exec(compile(ast.Module(body=[fn], type_ignores=[]), "explainer.py", "exec"), sns)
+    for i, (B, K, H, W, seed) in enumerate(SORT_CASES):
+        hm = sort_inputs(B, K, H, W, seed)
+        std, sub = hm[:, 0:1], hm[:, 1:]                 # explainer.py:113-114 (views)
+        s_hm, s_rel, mask = sns["sort_subspaces"](None, sub)
+        assert np.array_equal(s_hm, sub[np.arange(B)[:, None], mask])
+        out[f"sort{i}_meta"] = np.array([B, K, H, W, seed])
+        out[f"sort{i}_checksum"] = np.array([hm.sum(dtype=np.float64)])
+        out[f"sort{i}_rel"] = s_rel
+        out[f"sort{i}_mask"] = mask
+        out[f"sort{i}_std_rel"] = std.sum(axis=(-2, -1)).flatten()      # explainer.py:120
+    try:
+        hm = sort_inputs(1, 4, 8, 8, 3)
+        sns["sort_subspaces"](None, hm[:, 1:])
+        out["sort_b1_raises"] = np.array(0)
+    except IndexError:
+        out["sort_b1_raises"] = np.array(1)                               # D7
+    return out
+
+
+# C5 long horizon: two VGGish-width problems (layers 26 / 33: d = 128, K = 16), N = 20 000
+DRSA_C5 = {"j26": (20000, 128, 16, 26, 126), "j33": (20000, 128, 16, 33, 133)}   # N, d, K, data seed, U seed
+C5_STEPS = 5000                                                                 # optsubspaces.py:23
+
+
+def _drsa_c5(rdrsa, steps=C5_STEPS):
+    from scipy.stats import ortho_group
+    out = {}
+    for tag, (N, d, K, seed, useed) in DRSA_C5.items():
+        A, C = drsa_inputs(N, d, seed)
+        np.random.seed(useed)
+        U0 = ortho_group.rvs(d).astype(np.float32)
+        opt = rdrsa.SubspaceOptimizer(torch.from_numpy(U0), torch.from_numpy(A), torch.from_numpy(C), "/nonexistent",
+                                      num_concepts=K, device=torch.device("cpu"))
+        losses = []
+        opt.save_train_stats = lambda arr: losses.extend(float(a) for a in arr)
+        opt.save_model = lambda: None
+        t0 = __import__("time").time()
+        opt.run(steps=steps)
+        print(f"[gen_fixtures] reference run C5 {tag}: {steps} steps in {__import__('time').time() - t0:.1f} s")
+        out[f"{tag}_meta"] = np.array([N, d, K, seed, useed, steps])
+        out[f"{tag}_U0"] = U0
+        out[f"{tag}_A_checksum"] = np.array([A.sum(dtype=np.float64), C.sum(dtype=np.float64)])
+        out[f"{tag}_traj"] = np.array(losses)
+        out[f"{tag}_Ufinal"] = opt.U.detach().numpy().copy()
+    return out
+
+
+def main_round3():
+    """Round-3 fixtures (new files; earlier fixtures stay byte-identical)."""
+    OUT.mkdir(parents=True, exist_ok=True)
+    np.savez_compressed(OUT / "lrp_pins_fixture.npz", **_lrp_pins())
+    print("lrp pins written")
+    if "--no-c5" not in sys.argv:
+        rdrsa, _, _ = _import_reference()
+        np.savez_compressed(OUT / "drsa_c5_fixture.npz", **_drsa_c5(rdrsa))
+    print("round-3 fixtures written to", OUT)
+
+
 if __name__ == "__main__":
-    if "--round2" in sys.argv:
+    if "--round3" in sys.argv:
+        main_round3()
+    elif "--round2" in sys.argv:
         main_round2()
     else:
         main()

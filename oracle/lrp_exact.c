@@ -8,8 +8,7 @@
  *                                                         * w[co][ci][2-ky'][2-kx']
  *   linear_exact            out[m][n] = (chain over k of x[m][k] * W[n][k]) + b[n]
  *   matmul_exact            out[m][n] = chain over k of A[m][k] * B[k][n]
- *   tree_sum_hw             the heatmap_sort_kernel reduction tree (float4 pairs, 256
- *                           threads, wave butterfly, 4-wave pair sum)
+ *   (heatmap sums are numpy's own float32 sum, the reference's: oracle/lrp_ref.py plane_sum)
  *
  * The algorithm these feed (the LRP rules) is restated in oracle/lrp_ref.py; only the
  * summation order inside dot products is fixed here.  Compiled by oracle/Makefile with
@@ -76,30 +75,4 @@ void matmul_exact(const float* A, const float* Bm, float* out, int M, int N, int
       for (int k = 0; k < K; ++k) acc = fmaf(A[(size_t)m * K + k], Bm[(size_t)k * N + n], acc);
       out[(size_t)m * N + n] = acc;
     }
-}
-
-/* sum of one HW-plane exactly as heatmap_sort_kernel reduces it */
-float tree_sum_hw(const float* src, int HW) {
-  float part[256];
-  for (int t = 0; t < 256; ++t) {
-    float s = 0.f;
-    for (int i = t * 4; i < HW; i += 256 * 4) {
-      const float a = src[i] + src[i + 1];
-      const float c = src[i + 2] + src[i + 3];
-      s = s + (a + c);
-    }
-    part[t] = s;
-  }
-  float red[4];
-  for (int wv = 0; wv < 4; ++wv) {
-    float s[64];
-    for (int l = 0; l < 64; ++l) s[l] = part[wv * 64 + l];
-    for (int m = 32; m >= 1; m >>= 1) {
-      float t[64];
-      for (int l = 0; l < 64; ++l) t[l] = s[l] + s[l ^ m];
-      for (int l = 0; l < 64; ++l) s[l] = t[l];
-    }
-    red[wv] = s[0];
-  }
-  return (red[0] + red[1]) + (red[2] + red[3]);
 }

@@ -214,8 +214,6 @@ class ExactOps:
             L.conv_transpose_exact.argtypes = [P, P, P, I, I, I, I, I]
             L.linear_exact.argtypes = [P, P, P, P, I, I, I]
             L.matmul_exact.argtypes = [P, P, P, I, I, I]
-            L.tree_sum_hw.argtypes = [P, I]
-            L.tree_sum_hw.restype = ctypes.c_float
             cls._lib = L
         return cls._lib
 
@@ -267,11 +265,9 @@ class ExactOps:
 
     @classmethod
     def plane_sum(cls, hm: np.ndarray) -> np.ndarray:
-        hm = np.ascontiguousarray(hm, dtype=np.float32)
-        lead = hm.shape[:-2]
-        flat = hm.reshape(-1, hm.shape[-2] * hm.shape[-1])
-        out = np.array([cls.lib().tree_sum_hw(r.ctypes.data, r.size) for r in flat], dtype=np.float32)
-        return out.reshape(lead)
+        """The reference's own numpy float32 sum over (H, W) (explainer.py:120, :161): 0 + numpy's
+        pairwise summation, which the heatmap_sort kernels reproduce bit for bit."""
+        return np.asarray(hm, dtype=np.float32).sum(axis=(-2, -1))
 
 
 def _bf16r(t: torch.Tensor) -> torch.Tensor:
@@ -601,6 +597,38 @@ def class_composite_rules(name_map: Dict[str, RuleSpec], K: int) -> Dict[str, Ru
     r["features.subspacefilter"] = ("subspace", K)
     r["features.projection"] = ("epsilon", 1e-6)
     return r
+
+
+def numpy_pairwise_sum(a: np.ndarray) -> np.float32:
+    """numpy's float32 add-reduce of a contiguous run (the order sort_subspaces' ``sum(axis=(-2,
+    -1))`` uses, explainer.py:161): n < 8 a left-to-right chain from 0; n <= 128 eight stride-8
+    accumulators combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) plus the n % 8 tail; otherwise the
+    two halves split at n/2 - (n/2 % 8).  The reduce adds the result to the identity 0.  Scalar
+    restatement of what heatmap_sort_kernel computes (small inputs only: pure Python)."""
+    f = np.float32
+    a = np.asarray(a, dtype=np.float32).reshape(-1)
+
+    def pw(lo, n):
+        if n < 8:
+            r = f(0)
+            for i in range(n):
+                r = f(r + a[lo + i])
+            return r
+        if n <= 128:
+            r = [a[lo + j] for j in range(8)]
+            i = 8
+            while i < n - n % 8:
+                for j in range(8):
+                    r[j] = f(r[j] + a[lo + i + j])
+                i += 8
+            res = f(f(f(r[0] + r[1]) + f(r[2] + r[3])) + f(f(r[4] + r[5]) + f(r[6] + r[7])))
+            for k in range(i, n):
+                res = f(res + a[lo + k])
+            return res
+        n2 = n // 2
+        n2 -= n2 % 8
+        return f(pw(lo, n2) + pw(lo + n2, n - n2))
+    return f(f(0) + pw(0, a.size))
 
 
 def sort_subspaces(sub: np.ndarray, ops=TorchOps):

@@ -27,7 +27,7 @@ def test_optimize_grid_equals_sequential_drsa_run(tmp_path):
     for (c, l), (A, C) in data.items():
         Ag, Cg = A.to(dev), C.to(dev)
         for run, U0 in enumerate(initial_projections(A.size(1), 3, 42), start=1):
-            U, tr = drsa_run(Ag, Cg, torch.tensor(U0, dtype=torch.float32, device=dev), 4, steps)
+            U, tr = drsa_run(Ag, Cg, torch.tensor(np.ascontiguousarray(U0), dtype=torch.float32, device=dev), 4, steps)
             got = res[(c, l, run)]
             assert np.array_equal(got["trajectory"], tr.cpu().numpy()), (c, l, run)
             assert np.array_equal(got["U"], U.cpu().numpy())

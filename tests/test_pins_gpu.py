@@ -1,0 +1,82 @@
+"""The HIP kernels against outputs of the REFERENCE functions executed in the build container
+(tests/golden/lrp_pins_fixture.npz, oracle/gen_fixtures.py --round3):
+
+* heatmap_sort (both kernels) == HeatmapGenerator.sort_subspaces (explainer.py:151-176) and the
+  standard relevance (explainer.py:120): numpy float32 sums, argsort(...)[..., ::-1] incl. ties;
+* the fused output seed of drsa_amd_linear_bwd == lrp_output_modifier (attribute.py:111-160);
+* the clone mask inside drsa_amd_projection_bwd == SubspaceHook.backward (attribute.py:42-60).
+The last two are isolated with identities (W = I, U = I, unit activations, zero stabilisers) under
+which every other operation of the kernel is exact."""
+import numpy as np
+import pytest
+import torch
+
+from gen_fixtures import SORT_CASES, sort_inputs
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def pins(golden_dir):
+    return np.load(f"{golden_dir}/lrp_pins_fixture.npz")
+
+
+def test_heatmap_sort_equals_reference_sort(pins):
+    from drsa_audio_amd import ops
+    for i, (B, K, H, W, seed) in enumerate(SORT_CASES):
+        hm = sort_inputs(B, K, H, W, seed)
+        std, std_rel, sub, rel, mask = (t.cpu().numpy() for t in ops.heatmap_sort(torch.from_numpy(hm).to(DEV), K))
+        m_ref = pins[f"sort{i}_mask"]
+        assert np.array_equal(mask, m_ref), (i, mask, m_ref)
+        assert np.array_equal(rel, pins[f"sort{i}_rel"]), i
+        assert np.array_equal(std_rel, pins[f"sort{i}_std_rel"]), i
+        assert np.array_equal(sub, hm[:, 1:][np.arange(B)[:, None], m_ref]), i
+        assert np.array_equal(std, hm[:, 0:1]), i
+        # B = 1 (the reference squeezes it away, D7): each sample alone gives its batch row
+        for b in range(B):
+            o1 = [t.cpu().numpy() for t in ops.heatmap_sort(torch.from_numpy(hm[b:b + 1].copy()).to(DEV), K)]
+            assert np.array_equal(o1[4][0], m_ref[b]) and np.array_equal(o1[3][0], pins[f"sort{i}_rel"][b])
+
+
+def test_fused_output_seed_equals_reference_modifier(pins):
+    from drsa_audio_amd import _capi
+    from drsa_audio_amd.xai.explain.attribute import seed_class_indices
+    logits = torch.from_numpy(pins["seed_logits"]).to(DEV)
+    M, C = logits.shape
+    eye = torch.eye(C, device=DEV)
+    ones = torch.ones_like(logits)
+    s = _capi.stream_ptr(DEV)
+    cases = {"cls3": (3, None, 0), "cls9": (9, None, 0), "all10": (None, 10, 0), "cls0_onehot": (0, None, 1),
+             "all10_onehot": (None, 10, 1)}
+    for tag, (ci, nc, oh) in cases.items():
+        cls = seed_class_indices(M, ci, nc, DEV)
+        out = torch.empty(M, C, device=DEV)
+        # g = seed / stab(z, 0) through W = I; class mode: z = x = logits, xmode 1 -> z * (z/z) = seed;
+        # one-hot mode: z = 1, xmode 0 -> seed
+        z = ones if oh else logits
+        _capi.call("drsa_amd_linear_bwd", None, cls.data_ptr(), oh, z.data_ptr(), 0, 1, 0.0, eye.data_ptr(),
+                   logits.data_ptr(), 0 if oh else 1, None, 0, 0.0, out.data_ptr(), M, C, C, s)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), pins[f"seed_{tag}"]), tag
+
+
+def test_projection_bwd_clone_mask_equals_reference_hook(pins):
+    from drsa_audio_amd import _capi
+    s = _capi.stream_ptr(DEV)
+    for tag in ("k4", "k2", "k8", "k5"):
+        g, ref = pins[f"hook_{tag}_in"], pins[f"hook_{tag}_out"]
+        Bq, n, K, dk = g.shape
+        D, H, W = K * dk, 8, 8
+        assert n == H * W
+        gp = torch.from_numpy(g).reshape(Bq, n, D).transpose(1, 2).contiguous().reshape(Bq, D, H, W).to(DEV)
+        a = torch.ones(Bq, D, H, W, device=DEV)
+        U = torch.eye(D, device=DEV)
+        G = torch.empty_like(a)
+        # replicated-batch rows (fanout 0: row b is clone b mod (K+1)), no pool, no division below;
+        # with U = I, a = 1 and zero stabilisers: R_h = gp, masked, R_a = mask(R_h) exactly
+        _capi.call("drsa_amd_projection_bwd", gp.data_ptr(), None, None, None, a.data_ptr(), None, U.data_ptr(),
+                   G.data_ptr(), Bq, D, H, W, K, 0.0, 0.0, 0, s)
+        torch.cuda.synchronize()
+        got = G.reshape(Bq, D, n).transpose(1, 2).reshape(Bq, n, K, dk).cpu().numpy()
+        assert np.array_equal(got, ref), tag
