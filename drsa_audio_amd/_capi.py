@@ -49,8 +49,9 @@ SIGNATURES = {
     "drsa_amd_linear_fwd": (_i32, [_fp, _fp, _fp, _fp, _fp, _i32, _i32, _i32, _vp]),
     "drsa_amd_linear_bwd": (_i32, [_fp, _ip, _i32, _fp, _i32, _i32, _f32, _fp, _fp, _i32, _fp, _i32, _f32, _fp,
                                    _i32, _i32, _i32, _vp]),
-    "drsa_amd_projection_fwd": (_i32, [_fp, _fp, _fp, _fp, _fp, _vp, _i32, _i32, _i32, _i32, _i32, _vp]),
-    "drsa_amd_projection_bwd": (_i32, [_fp, _vp, _fp, _fp, _fp, _fp, _fp, _fp, _i32, _i32, _i32, _i32, _i32,
+    "drsa_amd_projection_residual": (_i32, [_fp, _i32, _fp, _vp]),
+    "drsa_amd_projection_fwd": (_i32, [_fp, _fp, _fp, _fp, _fp, _fp, _vp, _i32, _i32, _i32, _i32, _i32, _vp]),
+    "drsa_amd_projection_bwd": (_i32, [_fp, _vp, _fp, _fp, _fp, _fp, _fp, _fp, _fp, _i32, _i32, _i32, _i32, _i32,
                                        _f32, _f32, _i32, _vp]),
     "drsa_amd_ab_split": (_i32, [_fp, _fp, _fp, _fp, _fp, _i32, _i32, _i64, _f32, _vp]),
     "drsa_amd_ab_combine": (_i32, [_fp, _fp, _f32, _f32, _fp, _fp, _fp, _i32, _i32, _i64, _i32, _f32, _vp]),

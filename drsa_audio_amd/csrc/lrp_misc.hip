@@ -173,6 +173,31 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(LinArgs a) {
 // every value is the d-term chain of the unpadded product, bit for bit; outputs past d are
 // computed (zeros) but not stored.
 // ===========================================================================
+// P = U U^T - I (d x d), the projection residual: each entry one float64 fma chain over k
+// ascending (the products of two floats are exact in float64), minus the identity, rounded
+// once to fp32.  P is symmetric bit for bit.  The projection kernels evaluate
+//   a' = h U^T  as  a' = a + a P
+// (equal in exact arithmetic): at a dead ReLU channel (a = 0) a' is then exact to its own
+// rounding instead of carrying the O(1e-8) rounding noise of the d-term chain h U^T, which the
+// invprojection's Epsilon(1e-6) amplifies into the subspace relevances.
+__global__ __launch_bounds__(256) void projection_residual_kernel(const float* __restrict__ U, int d,
+                                                                  float* __restrict__ P) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= d * d) return;
+  const int r = i / d, c = i % d;
+  double acc = 0.0;
+  for (int k = 0; k < d; ++k) acc = fma((double)U[r * d + k], (double)U[c * d + k], acc);
+  P[i] = (float)(acc - (r == c ? 1.0 : 0.0));
+}
+
+// MFMA A operand P[c][k] of lane (c, k), read as the symmetric P[k][c] so that the 16 lanes of a
+// row group load 16 consecutive floats; zero outside the d x d matrix (padded embedding)
+__device__ __forceinline__ float p_operand(const float* __restrict__ P, int d, int c, int k) {
+  const bool ok = c < d && k < d;
+  const float v = P[ok ? k * d + c : 0];
+  return ok ? v : 0.f;
+}
+
 constexpr int PT = 4;   // row-pair tiles per workgroup
 
 template <int DP>
@@ -188,6 +213,7 @@ __device__ __forceinline__ void stage_u_padded(float* Us, const float* __restric
 
 template <int DP, bool PAD>
 __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __restrict__ a, const float* __restrict__ U,
+                                                            const float* __restrict__ Pm,
                                                             float* __restrict__ h, float* __restrict__ ap,
                                                             float* __restrict__ pooled, uint8_t* __restrict__ amax,
                                                             int d_in, int H, int W, int pool) {
@@ -240,25 +266,27 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
         }
     }
     __syncthreads();
-    // a'[c][p] = sum_j U[c][j] h[j][p]
+    // a'[c][p] = a[c][p] + sum_k P[c][k] a[k][p]   (= sum_j U[c][j] h[j][p]; residual form, above)
     {
       f32x4 acc[NB];
 #pragma unroll
       for (int cb = 0; cb < NB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
       for (int k0 = 0; k0 < d4; k0 += 4) {
-        const int j = k0 + (lane >> 4);
-        const float bv = hs[j * PL + w * 16 + (lane & 15)];
+        const int k = k0 + (lane >> 4);
+        const float bv = as[k * PL + w * 16 + (lane & 15)];
 #pragma unroll
-        for (int cb = 0; cb < NB; ++cb) acc[cb] = mfma16(Us[(cb * 16 + (lane & 15)) * LD + j], bv, acc[cb]);
+        for (int cb = 0; cb < NB; ++cb) acc[cb] = mfma16(p_operand(Pm, d, cb * 16 + (lane & 15), k), bv, acc[cb]);
       }
+      // every wave reads and writes only its own 16 pixel columns of the tile
 #pragma unroll
       for (int cb = 0; cb < NB; ++cb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int c = cb * 16 + (lane >> 4) * 4 + r, p = w * 16 + (lane & 15);
-          as[c * PL + p] = acc[cb][r];   // a tile no longer needed: holds a' now
-          if (ap && c < d) ap[((size_t)b * d + c) * HW + (y0 + p / TW) * W + x0 + p % TW] = acc[cb][r];
+          const float v = as[c * PL + p] + acc[cb][r];
+          as[c * PL + p] = v;   // a tile no longer needed: holds a' now
+          if (ap && c < d) ap[((size_t)b * d + c) * HW + (y0 + p / TW) * W + x0 + p % TW] = v;
         }
     }
     if (pool) {
@@ -452,8 +480,8 @@ constexpr int PT_RC = DRSA_PT_RC;   // tiles per workgroup (U staged once)
 template <int DP, bool PAD>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? DRSA_PROJ_RC_WPE : 1))) void projection_bwd_rc_kernel(
     const float* __restrict__ gp, const uint8_t* __restrict__ amax, const float* __restrict__ a,
-    const float* __restrict__ den, const float* __restrict__ U, float* __restrict__ G, int d_in, int H, int W, int K,
-    float eps_proj, float eps_den, int sparse, int has_den, int fanout) {
+    const float* __restrict__ den, const float* __restrict__ U, const float* __restrict__ Pm, float* __restrict__ G,
+    int d_in, int H, int W, int K, float eps_proj, float eps_den, int sparse, int has_den, int fanout) {
   const int d = PAD ? d_in : DP;
   constexpr int P = 64, LD = DP + 1, PW = 16, NB = DP / 16;
   constexpr bool PF = DP <= 64;   // keep a / den of the output rows in registers
@@ -514,18 +542,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
         for (int r = 0; r < 4; ++r) RB[(jb * 16 + rg * 4 + r) * PW + pc] = acc[jb][r];
     }
     __builtin_amdgcn_wave_barrier();
-    // a'[c][p] = sum_j U[c][j] h[j][p];  g1 = R_a' / stab(a')  -> region A
+    // a'[c][p] = a[c][p] + sum_k P[c][k] a[k][p]   (projection_fwd_kernel order);
+    // g1 = R_a' / stab(a')  -> region A (in place of a; a stays in registers)
     {
       f32x4 acc[NB];
 #pragma unroll
       for (int cb = 0; cb < NB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
       for (int k0 = 0; k0 < d4; k0 += 4) {
-        const int j = k0 + rg;
-        const float bv = RB[j * PW + pc];
+        const int k = k0 + rg;
+        const float bv = RA[k * PW + pc];
 #pragma unroll
-        for (int cb = 0; cb < NB; ++cb) acc[cb] = mfma16(Us[(cb * 16 + pc) * LD + j], bv, acc[cb]);
+        for (int cb = 0; cb < NB; ++cb) acc[cb] = mfma16(p_operand(Pm, d, cb * 16 + pc, k), bv, acc[cb]);
       }
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int cb = 0; cb < NB; ++cb)
 #pragma unroll
@@ -541,7 +571,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
           } else {
             R = gp[((size_t)b * d + cc) * HW + pixl];
           }
-          const float v = R / stab(acc[cb][r], eps_proj);
+          const float apv = av[cb * 4 + r] + acc[cb][r];
+          const float v = R / stab(apv, eps_proj);
           RA[c * PW + pc] = ok ? v : 0.f;
         }
     }
@@ -844,12 +875,13 @@ __global__ void first_layer_den_kernel(const float* __restrict__ w2, const float
 //   stable ascending order reversed, i.e. ties -> larger index first)
 //
 // The per-map relevance is the reference's numpy float32 sum over the last two axes
-// (explainer.py:161, :120): 0 + pairwise(map), numpy's pairwise summation -- n <= 8: a plain
-// left-to-right chain; n <= 128: eight strided accumulators r[j] = a[j] + a[8+j] + ... combined
-// as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the n % 8 tail; n > 128: split at
-// n2 = n/2 - (n/2 % 8) and add the two halves' sums.  For n = 128 * 2^m the leaves are the
-// 128-element blocks and the tree over them is balanced (a butterfly); other n take a serial
-// walk of the same recursion.  Bit-identical to numpy (pinned by tests/golden/lrp_pins_fixture).
+// (explainer.py:161, :120): chunks of 8192 elements folded left to right into 0, each chunk by
+// numpy's pairwise summation -- n < 8: a plain left-to-right chain; n <= 128: eight strided
+// accumulators r[j] = a[j] + a[8+j] + ... combined as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then
+// the n % 8 tail; n > 128: split at n2 = n/2 - (n/2 % 8) and add the two halves' sums.  For
+// n = 128 * 2^m the leaves are the 128-element blocks and the tree over them is balanced (a
+// butterfly); other n take a serial walk of the same recursion.  Bit-identical to numpy (pinned
+// by tests/golden/lrp_pins_fixture.npz).
 // ===========================================================================
 __device__ float pw_leaf(const float* a, int n) {   // numpy pairwise_sum for n <= 128
   if (n < 8) {
@@ -900,34 +932,38 @@ __device__ __forceinline__ float pw_half(const float4* leaf, int h) {
   return (r.x + r.y) + (r.z + r.w);
 }
 
-// numpy sum of one map by the whole workgroup (256 threads); part: >= 2 * min(n/128, 2048) floats
-// of LDS.  Result valid in every thread.  Contains barriers: call uniformly.
-__device__ float pw_sum_wg(const float* __restrict__ src, int n, float* part, float* bc) {
+// numpy pairwise sum of one run of n <= 8192 by the whole workgroup (256 threads); part: >= 128
+// floats of LDS.  Result valid in every thread.  Contains barriers: call uniformly.
+__device__ float pw_chunk_wg(const float* __restrict__ src, int n, float* part, float* bc) {
   const int tid = threadIdx.x;
   const int leaves = n / 128;
-  const bool bal = n > 128 && n % 128 == 0 && (leaves & (leaves - 1)) == 0 && leaves <= 2048;
-  if (bal) {
-    for (int t = tid; t < 2 * leaves; t += 256)
-      part[t] = pw_half(reinterpret_cast<const float4*>(src) + (size_t)(t >> 1) * 32, t & 1);
+  if (n > 128 && n % 128 == 0 && (leaves & (leaves - 1)) == 0) {     // balanced: <= 64 leaves
+    if (tid < 2 * leaves) part[tid] = pw_half(reinterpret_cast<const float4*>(src) + (size_t)(tid >> 1) * 32, tid & 1);
     __syncthreads();
     for (int w = 2 * leaves; w > 1; w >>= 1) {      // halves -> leaves -> balanced tree, adjacent pairs
-      float v[8];
-      int c = 0;
-      for (int t = tid; t < w / 2; t += 256) v[c++] = part[2 * t] + part[2 * t + 1];
+      const float v = tid < w / 2 ? part[2 * tid] + part[2 * tid + 1] : 0.f;
       __syncthreads();
-      c = 0;
-      for (int t = tid; t < w / 2; t += 256) part[t] = v[c++];
+      if (tid < w / 2) part[tid] = v;
       __syncthreads();
     }
     const float r = part[0];
     __syncthreads();
-    return 0.f + r;
+    return r;
   }
-  if (tid == 0) *bc = 0.f + pw_serial(src, n);
+  if (tid == 0) *bc = pw_serial(src, n);
   __syncthreads();
   const float r = *bc;
   __syncthreads();
   return r;
+}
+
+// numpy's float32 sum of a contiguous run: the reduction iterator feeds the inner loop chunks of
+// 8192 elements (its buffer size), folded left to right into the identity 0, each chunk summed
+// pairwise (oracle/lrp_ref.py numpy_pairwise_sum).
+__device__ float pw_sum_wg(const float* __restrict__ src, int n, float* part, float* bc) {
+  float acc = 0.f;
+  for (int lo = 0; lo < n; lo += 8192) acc = acc + pw_chunk_wg(src + lo, n - lo < 8192 ? n - lo : 8192, part, bc);
+  return acc;
 }
 
 __device__ void sort_desc(const float* sums, int K, int* order) {   // descending; ties: larger index first
@@ -950,7 +986,7 @@ __global__ __launch_bounds__(256) void heatmap_sort_kernel(const float* __restri
                                                            float* __restrict__ std_out, float* __restrict__ std_rel,
                                                            float* __restrict__ sub_out, float* __restrict__ rel,
                                                            int64_t* __restrict__ mask) {
-  __shared__ float part[4096];
+  __shared__ float part[128];
   __shared__ float bc;
   __shared__ float sums[65];
   __shared__ int order[64];
@@ -1039,8 +1075,8 @@ __global__ __launch_bounds__(256) void heatmap_sort_cached_kernel(const float* _
     __syncthreads();
     s[1 + q] = chain();
   }
-  // balanced tree over the leaves: lanes 2L, 2L+1 hold leaf L; in-wave butterfly over L, then
-  // the four waves' (32-leaf) sums as (w0 + w1) + (w2 + w3)
+  // balanced tree over the leaves: lanes 2L, 2L+1 hold leaf L; in-wave butterfly over L; waves
+  // 0-1 hold the first 8192-element chunk, 2-3 the second: (0 + (w0 + w1)) + (w2 + w3)
 #pragma unroll
   for (int q = 0; q <= KC; ++q) {
     float a = s[q];
@@ -1049,7 +1085,7 @@ __global__ __launch_bounds__(256) void heatmap_sort_cached_kernel(const float* _
   }
   __syncthreads();
   if (tid == 0) {
-    for (int q = 0; q <= KC; ++q) sums[q] = 0.f + ((red[q][0] + red[q][1]) + (red[q][2] + red[q][3]));
+    for (int q = 0; q <= KC; ++q) sums[q] = (0.f + (red[q][0] + red[q][1])) + (red[q][2] + red[q][3]);
     sort_desc(sums, KC, order);
     std_rel[b] = sums[0];
     for (int k = 0; k < KC; ++k) {
@@ -1082,11 +1118,11 @@ __global__ __launch_bounds__(256) void heatmap_sort_cached_kernel(const float* _
 // ===========================================================================
 __global__ __launch_bounds__(256) void ab_split_kernel(const float* __restrict__ g, const float* __restrict__ dp,
                                                        const float* __restrict__ dn, float* __restrict__ gp,
-                                                       float* __restrict__ gn, long n, int clones, long total,
+                                                       float* __restrict__ gn, int64_t n, int clones, int64_t total,
                                                        float eps) {
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const long bq = i / n, j = i - bq * n;
-    const long o = (bq / clones) * n + j;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t bq = i / n, j = i - bq * n;
+    const int64_t o = (bq / clones) * n + j;
     const float r = g[i];
     gp[i] = div_nb(r, stab(dp[o], eps));
     gn[i] = div_nb(r, stab(dn[o], eps));
@@ -1096,10 +1132,10 @@ __global__ __launch_bounds__(256) void ab_split_kernel(const float* __restrict__
 __global__ __launch_bounds__(256) void ab_combine_kernel(const float* __restrict__ pos, const float* __restrict__ neg,
                                                          float alpha, float beta, const float* __restrict__ x,
                                                          const float* __restrict__ den, float* __restrict__ out,
-                                                         long n, int clones, long total, int post, float eps) {
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const long bq = i / n, j = i - bq * n;
-    const long o = (bq / clones) * n + j;
+                                                         int64_t n, int clones, int64_t total, int post, float eps) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t bq = i / n, j = i - bq * n;
+    const int64_t o = (bq / clones) * n + j;
     const float a = alpha * pos[i];
     const float b = beta * neg[i];
     float R = a - b;
@@ -1112,8 +1148,8 @@ __global__ __launch_bounds__(256) void ab_combine_kernel(const float* __restrict
   }
 }
 
-unsigned ew_grid(long total) {
-  const long g = (total + 255) / 256;
+unsigned ew_grid(int64_t total) {
+  const int64_t g = (total + 255) / 256;
   return (unsigned)(g < 65536 ? (g > 0 ? g : 1) : 65536);
 }
 
@@ -1141,7 +1177,7 @@ int drsa_amd_linear_fwd(const float* x, const float* Wt, const float* bias, floa
   DRSA_REQUIRE(M > 0 && N > 0 && K > 0, "linear_fwd: bad shape");
   LinArgs a{};
   a.A = x; a.W = Wt; a.bias = bias; a.out = z_out; a.out_relu = relu_out; a.M = M; a.N = N; a.K = K; a.bwd = 0;
-  // long K (float4-aligned rows): the prefetching kernel; same chain order, same results
+  // int64_t K (float4-aligned rows): the prefetching kernel; same chain order, same results
   if (K % 4 == 0 && K >= LFK)
     hipLaunchKernelGGL(linear_fwd_kernel, dim3((M + LT - 1) / LT, (N + LT - 1) / LT), dim3(256), 0, (hipStream_t)stream, a);
   else
@@ -1167,9 +1203,17 @@ int drsa_amd_linear_bwd(const float* R, const int* seed_cls, int one_hot, const 
   return DRSA_OK;
 }
 
-int drsa_amd_projection_fwd(const float* a, const float* U, float* h, float* ap, float* pooled, uint8_t* amax, int B,
-                            int D, int H, int W, int pool, void* stream) {
+int drsa_amd_projection_residual(const float* U, int D, float* P, void* stream) {
+  DRSA_REQUIRE(U && P && D >= 1 && D <= 128, "projection_residual: need U, P and 1 <= d <= 128");
+  hipLaunchKernelGGL(projection_residual_kernel, dim3((D * D + 255) / 256), dim3(256), 0, (hipStream_t)stream, U, D, P);
+  DRSA_LAUNCH_CHECK();
+  return DRSA_OK;
+}
+
+int drsa_amd_projection_fwd(const float* a, const float* U, const float* P, float* h, float* ap, float* pooled,
+                            uint8_t* amax, int B, int D, int H, int W, int pool, void* stream) {
   const int TW = W < 32 ? W : 32;
+  DRSA_REQUIRE(a && U && P, "projection_fwd: a, U and P (drsa_amd_projection_residual) are required");
   DRSA_REQUIRE((W == 8 || W == 16 || W % 32 == 0) && H % (64 / TW) == 0,
                "projection_fwd: W must be 8, 16 or a multiple of 32 and H a multiple of 64/min(W,32) (got %dx%d)", H, W);
   DRSA_REQUIRE(!pool || (pooled && amax), "projection_fwd: pool needs outputs");
@@ -1182,7 +1226,7 @@ int drsa_amd_projection_fwd(const float* a, const float* U, float* h, float* ap,
   case DD: {                                                                                          \
     auto kf = D == DD ? projection_fwd_kernel<DD, false> : projection_fwd_kernel<DD, true>;        \
     { int rc = with_lds(kf, proj_fwd_lds<DD>()); if (rc) return rc; }                               \
-    hipLaunchKernelGGL(kf, grid, dim3(256), proj_fwd_lds<DD>(), s, a, U, h, ap, pooled, amax,       \
+    hipLaunchKernelGGL(kf, grid, dim3(256), proj_fwd_lds<DD>(), s, a, U, P, h, ap, pooled, amax,       \
                        D, H, W, pool);                                                                \
     break;                                                                                            \
   }
@@ -1197,9 +1241,11 @@ int drsa_amd_projection_fwd(const float* a, const float* U, float* h, float* ap,
 }
 
 int drsa_amd_projection_bwd(const float* gp, const uint8_t* amax, const float* ap, const float* h, const float* a,
-                            const float* den, const float* U, float* G, int B, int D, int H, int W, int K,
-                            float eps_proj, float eps_den, int fanout, void* stream) {
+                            const float* den, const float* U, const float* P, float* G, int B, int D, int H, int W,
+                            int K, float eps_proj, float eps_den, int fanout, void* stream) {
   const int TW = W < 32 ? W : 32;
+  DRSA_REQUIRE(gp && a && U && G && ((ap && h) || P),
+               "projection_bwd: gp, a, U, G and P (when h / a' are recomputed) are required");
   DRSA_REQUIRE((W == 8 || W == 16 || W % 32 == 0) && H % (64 / TW) == 0,
                "projection_bwd: W must be 8, 16 or a multiple of 32 and H a multiple of 64/min(W,32) (got %dx%d)", H, W);
   DRSA_REQUIRE(K > 0 && D % K == 0, "projection_bwd: K must divide d");
@@ -1213,7 +1259,7 @@ int drsa_amd_projection_bwd(const float* gp, const uint8_t* amax, const float* a
   case DD: {                                                                                          \
     auto kr = D == DD ? projection_bwd_rc_kernel<DD, false> : projection_bwd_rc_kernel<DD, true>;  \
     { int rc = with_lds(kr, proj_bwd_rc_lds<DD>()); if (rc) return rc; }                            \
-    hipLaunchKernelGGL(kr, grid, dim3(256), proj_bwd_rc_lds<DD>(), s, gp, amax, a, den, U, G,        \
+    hipLaunchKernelGGL(kr, grid, dim3(256), proj_bwd_rc_lds<DD>(), s, gp, amax, a, den, U, P, G,     \
                        D, H, W, K, eps_proj, eps_den, sparse, has_den, fanout);                      \
     break;                                                                                            \
   }
@@ -1290,10 +1336,10 @@ int drsa_amd_heatmap_sort(const float* hm, int B, int K, int HW, float* std_out,
 }
 
 int drsa_amd_ab_split(const float* g, const float* den_p, const float* den_n, float* gp, float* gn, int Bq,
-                      int clones, long n, float eps, void* stream) {
+                      int clones, int64_t n, float eps, void* stream) {
   DRSA_REQUIRE(g && den_p && den_n && gp && gn, "ab_split: null pointer");
   DRSA_REQUIRE(Bq > 0 && clones > 0 && Bq % clones == 0 && n > 0, "ab_split: bad shape");
-  const long total = (long)Bq * n;
+  const int64_t total = (int64_t)Bq * n;
   hipLaunchKernelGGL(ab_split_kernel, dim3(ew_grid(total)), dim3(256), 0, (hipStream_t)stream, g, den_p, den_n, gp, gn,
                      n, clones, total, eps);
   DRSA_LAUNCH_CHECK();
@@ -1301,11 +1347,11 @@ int drsa_amd_ab_split(const float* g, const float* den_p, const float* den_n, fl
 }
 
 int drsa_amd_ab_combine(const float* pos, const float* neg, float alpha, float beta, const float* x, const float* den,
-                        float* out, int Bq, int clones, long n, int post, float eps, void* stream) {
+                        float* out, int Bq, int clones, int64_t n, int post, float eps, void* stream) {
   DRSA_REQUIRE(pos && neg && out, "ab_combine: null pointer");
   DRSA_REQUIRE(Bq > 0 && clones > 0 && Bq % clones == 0 && n > 0, "ab_combine: bad shape");
   DRSA_REQUIRE(post == POST_NONE || (x && (den || post == POST_MASK)), "ab_combine: post needs x (and den)");
-  const long total = (long)Bq * n;
+  const int64_t total = (int64_t)Bq * n;
   hipLaunchKernelGGL(ab_combine_kernel, dim3(ew_grid(total)), dim3(256), 0, (hipStream_t)stream, pos, neg, alpha,
                      beta, x, den, out, n, clones, total, post, eps);
   DRSA_LAUNCH_CHECK();

@@ -23,14 +23,18 @@ _CACHE: "OrderedDict[tuple, _Entry]" = OrderedDict()
 
 
 class _Entry:
-    __slots__ = ("model_ref", "comp_ref", "fp", "eng")
+    __slots__ = ("model_ref", "comp_ref", "fp", "eng", "finalizers")
 
     def __init__(self, model_ref, comp_ref, fp, eng):
         self.model_ref, self.comp_ref, self.fp, self.eng = model_ref, comp_ref, fp, eng
+        self.finalizers = []
 
 
 def _fingerprint(model):
-    return tuple((p.data_ptr(), p._version) for p in model.parameters())
+    """Parameters AND buffers: the plan folds BatchNorm running statistics into the weights, so a
+    train-mode forward or a buffers-only load_state_dict must recompile."""
+    return (tuple((p.data_ptr(), p._version) for p in model.parameters()) +
+            tuple((b.data_ptr(), b._version) for b in model.buffers()))
 
 
 def _ref(obj):
@@ -42,6 +46,8 @@ def _ref(obj):
 def _evict(key) -> None:
     e = _CACHE.pop(key, None)
     if e is not None:
+        for f in e.finalizers:        # one live finalizer per cached entry, never a pile-up
+            f.detach()
         e.eng.release()
 
 
@@ -58,10 +64,11 @@ def get_engine(model, composite) -> LRPEngine:
     rules = composite.rules(model) if composite is not None else {}
     # a composite with a user-written Hook (its own backward) cannot be compiled: autograd slow path
     eng = HookedAutograd(model, composite) if has_custom_hooks(rules) else LRPEngine(model, composite)
-    _CACHE[key] = _Entry(_ref(model), _ref(composite), fp, eng)
-    weakref.finalize(model, _evict, key)
+    entry = _Entry(_ref(model), _ref(composite), fp, eng)
+    _CACHE[key] = entry
+    entry.finalizers.append(weakref.finalize(model, _evict, key))
     if composite is not None:
-        weakref.finalize(composite, _evict, key)
+        entry.finalizers.append(weakref.finalize(composite, _evict, key))
     while len(_CACHE) > _MAX:
         _evict(next(iter(_CACHE)))
     return eng

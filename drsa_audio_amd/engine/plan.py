@@ -72,6 +72,7 @@ def _eps_of(rule) -> float:
 class ProjGroup:
     U: torch.Tensor
     K: int
+    P: Optional[torch.Tensor]   # U U^T - I (drsa_amd_projection_residual), set at plan build
     eps_inv: float
     eps_proj: float
     mask: bool          # SubspaceHook on the filter
@@ -230,7 +231,10 @@ class LRPEngine:
                 if r_f is not None and type(r_f).__name__ != "SubspaceHook":
                     raise EngineError("engine: only SubspaceHook is supported on the subspace filter")
                 U = pm.U.detach().to(self.device, torch.float32).contiguous()
-                proj = ProjGroup(U=U, K=int(pm.num_concepts), eps_inv=_eps_of(r_i), eps_proj=_eps_of(r_p),
+                Pm = torch.empty_like(U)
+                _capi.call("drsa_amd_projection_residual", U.data_ptr(), U.size(0), Pm.data_ptr(),
+                           _capi.stream_ptr(self.device))
+                proj = ProjGroup(U=U, K=int(pm.num_concepts), P=Pm, eps_inv=_eps_of(r_i), eps_proj=_eps_of(r_p),
                                  mask=r_f is not None, pool_after=False)
                 if r_f is not None and int(r_f.num_concepts) != proj.K:
                     raise EngineError("engine: SubspaceHook num_concepts differs from the projection")
@@ -531,7 +535,8 @@ class LRPEngine:
                         amax = self._buf((li, "amax"), (B, st.cout, h // 2, w // 2), torch.uint8)
                     else:
                         pooled = amax = None
-                    self._call("projection_fwd", "drsa_amd_projection_fwd", a.data_ptr(), P.U.data_ptr(), _capi.ptr(hb), _capi.ptr(ap),
+                    self._call("projection_fwd", "drsa_amd_projection_fwd", a.data_ptr(), P.U.data_ptr(), P.P.data_ptr(),
+                               _capi.ptr(hb), _capi.ptr(ap),
                                _capi.ptr(pooled), _capi.ptr(amax), B, st.cout, h, w, 1 if P.pool_after else 0, s)
                     rec.update(h=hb, ap=ap, amax=amax)
                     if P.pool_after:
@@ -638,7 +643,8 @@ class LRPEngine:
                     raise EngineError("engine: projection without SubspaceHook is not supported yet")
                 self._call("projection_bwd", "drsa_amd_projection_bwd", g.data_ptr(), _capi.ptr(rec["amax"] if P.pool_after else None),
                            _capi.ptr(rec["ap"] if _PROJ_STORE else None), _capi.ptr(rec["h"]), rec["a"].data_ptr(),
-                           _capi.ptr(den if post == POST_DIV else None), P.U.data_ptr(), G.data_ptr(), B, st.cout,
+                           _capi.ptr(den if post == POST_DIV else None), P.U.data_ptr(), P.P.data_ptr(), G.data_ptr(),
+                           B, st.cout,
                            h, w, K, P.eps_inv, eps, 1 if fan else 0, s)
                 g, clones, Bq = G, nq, B * nq
             elif st.pool and st.pool_k == (2, 2):

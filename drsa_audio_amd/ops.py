@@ -182,20 +182,28 @@ def _(R, cls, one_hot, z, relu_mask, rule_eps, eps, W, x, xmode, den, post, eps_
     return z.new_empty(z.shape[0], W.shape[1])
 
 
+def _residual(U: Tensor) -> Tensor:
+    """P = U U^T - I for the projection kernels (drsa_amd_projection_residual)."""
+    P = torch.empty_like(U)
+    _capi.call("drsa_amd_projection_residual", U.data_ptr(), U.size(0), P.data_ptr(), _s(U))
+    return P
+
+
 @torch.library.custom_op(f"{_NS}::projection_fwd", mutates_args=())
 def projection_fwd(a: Tensor, U: Tensor, pool: bool) -> Tuple[Tensor, Tensor]:
     _chk(a, "a"), _chk(U, "U")
     B, D, H, W = a.shape
+    P = _residual(U)
     if pool:
         y = a.new_empty(B, D, H // 2, W // 2)
         amax = torch.empty(B, D, H // 2, W // 2, dtype=torch.uint8, device=a.device)
-        _capi.call("drsa_amd_projection_fwd", a.data_ptr(), U.data_ptr(), None, None, y.data_ptr(), amax.data_ptr(),
-                   B, D, H, W, 1, _s(a))
+        _capi.call("drsa_amd_projection_fwd", a.data_ptr(), U.data_ptr(), P.data_ptr(), None, None, y.data_ptr(),
+                   amax.data_ptr(), B, D, H, W, 1, _s(a))
     else:
         y = torch.empty_like(a)
         amax = torch.empty(0, dtype=torch.uint8, device=a.device)
-        _capi.call("drsa_amd_projection_fwd", a.data_ptr(), U.data_ptr(), None, y.data_ptr(), None, None, B, D, H,
-                   W, 0, _s(a))
+        _capi.call("drsa_amd_projection_fwd", a.data_ptr(), U.data_ptr(), P.data_ptr(), None, y.data_ptr(), None,
+                   None, B, D, H, W, 0, _s(a))
     return y, amax
 
 
@@ -214,8 +222,10 @@ def projection_bwd(g: Tensor, amax: Optional[Tensor], a: Tensor, den: Optional[T
     B, D, H, W = a.shape
     nq = (K + 1) if fanout else 1
     G = a.new_empty(B * nq, D, H, W)
+    P = _residual(U)
     _capi.call("drsa_amd_projection_bwd", g.data_ptr(), _capi.ptr(amax), None, None, a.data_ptr(), _capi.ptr(den),
-               U.data_ptr(), G.data_ptr(), B, D, H, W, K, float(eps_proj), float(eps_den), 1 if fanout else 0, _s(a))
+               U.data_ptr(), P.data_ptr(), G.data_ptr(), B, D, H, W, K, float(eps_proj), float(eps_den),
+               1 if fanout else 0, _s(a))
     return G
 
 

@@ -27,7 +27,7 @@ import torch
 class Flipper:
     def __init__(self, perturbation_size: int = 16, perturbation_mode: str = "constant",
                  data_normaliaztion: str = "normalized", device: str | torch.device = torch.device("cpu"),
-                 fuse_steps: bool = False) -> None:
+                 fuse_steps: bool = False, fuse_max_rows: int = 2048) -> None:
         if perturbation_mode not in ("constant", "inpainting"):
             raise ValueError('Provided perturbation mode not available. Possible perturbation modes are '
                              '"constant" and "inpainting".')
@@ -36,6 +36,7 @@ class Flipper:
         self.data_normaliaztion = data_normaliaztion
         self.device = torch.device(device) if isinstance(device, str) else device
         self.fuse_steps = fuse_steps
+        self.fuse_max_rows = max(1, int(fuse_max_rows))   # cap of one fused forward (device memory)
 
     # ------------------------------------------------------------------ schedule
     @staticmethod
@@ -107,7 +108,9 @@ class Flipper:
         xs = [x] + [x * self._masks(first, s, C, H, W) for s in range(1, S)]
         with torch.no_grad():
             if self.fuse_steps:
-                out = forward_func(torch.cat(xs, 0))
+                per = max(1, self.fuse_max_rows // B)         # steps per fused forward
+                outs = [forward_func(torch.cat(xs[i:i + per], 0)) for i in range(0, S, per)]
+                out = torch.cat(outs, 0)
                 preds = torch.stack([self._scores(o, B) for o in out.reshape(S, B, -1)])
             else:
                 preds = torch.stack([self._scores(forward_func(xi), B) for xi in xs])

@@ -2,8 +2,12 @@
 ``cxai.xai.pixelflipping.pf.PixelFlipping`` (reference pf.py:29-292).
 
 The relevances of every configuration come from the HIP LRP engine (compute_relevances per
-class block, pf.py:165-176) and the perturbed forwards from the engine's forward (HIP kernels;
-``forward="torch"`` uses the model's own forward like the reference's ``forward_func``).
+class block, pf.py:165-176).  The perturbed forwards are the model's own ``model(x)``, one call per
+flipping step, exactly the reference's ``forward_func`` (pf.py:83) -- the default,
+``forward="torch"``.  ``forward="engine"`` runs them on the engine's HIP forward instead, with
+BatchNorm merged by the canonizer and several steps fused per call (at most ``fuse_max_rows``
+rows): the logits then differ from model(x) by fp32 accumulation order (AUPC within 1e-4 of the
+torch forward's, tests/test_pixelflipping_gpu.py).
 Composites: ``SpecialFirstLayerMapComposite`` (first conv -> the 'first_layer' rule, then
 (Activation, Pass), (Convolution, conv rule), (Linear, dense rule)) or, with a 'name_map' key,
 ``NameLayerMapComposite`` (pf.py:196-236).  Rules by key: ``rule_mapper`` (pf.py:18-27).
@@ -40,7 +44,8 @@ rule_mapper = {
 class PixelFlipping:
     def __init__(self, model: nn.Module, input_batch: torch.Tensor, perturbation_size: int = 8,
                  perturbation_mode: str = "constant", num_classes: int = 10, data_normaliaztion: str = "normalized",
-                 device: torch.device = torch.device("cuda"), forward: str = "engine") -> None:
+                 device: torch.device = torch.device("cuda"), forward: str = "torch",
+                 fuse_max_rows: int = 2048) -> None:
         self.device = torch.device(device) if isinstance(device, str) else device
         self.input_batch = input_batch.to(self.device)
         self.num_classes = int(num_classes)
@@ -51,7 +56,7 @@ class PixelFlipping:
         self.forward = forward
         self.pixel_flipper = Flipper(perturbation_size=perturbation_size, perturbation_mode=perturbation_mode,
                                      data_normaliaztion=data_normaliaztion, device=self.device,
-                                     fuse_steps=forward == "engine")
+                                     fuse_steps=forward == "engine", fuse_max_rows=fuse_max_rows)
 
     def _forward_func(self, canonizer):
         if self.forward == "torch":

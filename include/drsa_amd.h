@@ -160,32 +160,40 @@ int drsa_amd_linear_bwd(const float* R, const int* seed_cls, int one_hot, const 
                         float eps, const float* W, const float* x, int xmode, const float* den, int post,
                         float eps_post, float* out, int M, int Nout, int Kin, void* stream);
 
-/* ProjectionModel forward (modify_model.py:75-123): h = a_vec U, a' = h U^T [, 2x2 pool].
+/* Projection residual P = U U^T - I (d x d, d <= 128): each entry a float64 fma chain over k
+ * ascending minus the identity, rounded once to fp32 (symmetric bit for bit).  Computed once per
+ * U (plan preparation); the projection calls below evaluate a' = h U^T as a + a P, so that a' at
+ * dead ReLU channels is exact to its rounding. */
+int drsa_amd_projection_residual(const float* U, int d, float* P, void* stream);
+
+/* ProjectionModel forward (modify_model.py:75-123): h = a_vec U, a' = h U^T (as a + a P, P from
+ * drsa_amd_projection_residual) [, 2x2 pool].
  * h and ap may be NULL (not stored); ap is required when pool == 0 (it is the output).
  * Any D <= 128 (VGGish layer 19: D = 100): zero-padded embedding in the kernel; for D % 4 == 0
  * every value is the unpadded D-term chain. */
-int drsa_amd_projection_fwd(const float* a, const float* U, float* h, float* ap, float* pooled, uint8_t* amax, int B,
-                            int D, int H, int W, int pool, void* stream);
+int drsa_amd_projection_fwd(const float* a, const float* U, const float* P, float* h, float* ap, float* pooled,
+                            uint8_t* amax, int B, int D, int H, int W, int pool, void* stream);
 
 /* Epsilon(invprojection) -> SubspaceHook mask -> Epsilon(projection) -> ReLU backward ->
  * division of the conv rule below (explainer.py:198-203, attribute.py:42-60).
  * fanout != 0: each sample yields K+1 clones (standard + K subspaces); fanout == 0: row b is
  * clone (b mod (K+1)) of a replicated batch (explainer.py:92 semantics).
  * ap or h NULL: h and a' are recomputed from a in the kernel (same MFMA order as
- * drsa_amd_projection_fwd, so the result is bit-identical to passing the stored buffers). */
+ * drsa_amd_projection_fwd, so the result is bit-identical to passing the stored buffers); P is
+ * then required. */
 int drsa_amd_projection_bwd(const float* gp, const uint8_t* amax, const float* ap, const float* h, const float* a,
-                            const float* den, const float* U, float* G, int B, int D, int H, int W, int K,
-                            float eps_proj, float eps_den, int fanout, void* stream);
+                            const float* den, const float* U, const float* P, float* G, int B, int D, int H, int W,
+                            int K, float eps_proj, float eps_den, int fanout, void* stream);
 
 /* AlphaBeta on a conv with non-negative input (zennit AlphaBeta as configured at pf.py:285-289,
  * restated in oracle/lrp_ref.py): split R at the conv output into gp = R / stab(den_p) and
  * gn = R / stab(den_n) (den per sample, R rows = sample*clones + clone, n elements per row) ... */
 int drsa_amd_ab_split(const float* g, const float* den_p, const float* den_n, float* gp, float* gn, int Bq,
-                      int clones, long n, float eps, void* stream);
+                      int clones, int64_t n, float eps, void* stream);
 /* ... and after the two backward convs pos = x J^T_{W+} gp, neg = x J^T_{W-} gn:
  * R_in = alpha*pos - beta*neg, then the post step of the layer below (post as conv_bwd). */
 int drsa_amd_ab_combine(const float* pos, const float* neg, float alpha, float beta, const float* x, const float* den,
-                        float* out, int Bq, int clones, long n, int post, float eps, void* stream);
+                        float* out, int Bq, int clones, int64_t n, int post, float eps, void* stream);
 
 /* First-layer (one input channel) WSquare / Flat backward: R = J^T_{W2} g. */
 int drsa_amd_first_layer_bwd(const float* g, const uint8_t* amax, const float* w2, float* out, int Bq, int clones,

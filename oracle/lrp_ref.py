@@ -264,10 +264,34 @@ class ExactOps:
         return out.reshape(*shp[:-1], b.size(1))
 
     @classmethod
+    def inv_projection(cls, L, h, a_map):
+        """a' = h U^T evaluated as a + a (U U^T - I): the product's projection kernels'
+        order.  P = U U^T - I is formed in float64 (k ascending) and rounded once, so a' is
+        accurate to its own rounding where a = 0 (dead ReLU channels), where the d-term chain
+        h U^T leaves O(1e-8) noise that Epsilon(1e-6) amplifies (D13)."""
+        m = L.module
+        P = proj_residual(m.U_inv.t())
+        b, d = a_map.size(0), a_map.size(1)
+        av = cls._c(a_map).reshape(b, d, -1).transpose(1, 2)
+        delta = cls.matmul(av, P)
+        return (av + delta).transpose(1, 2).reshape(a_map.shape).contiguous()
+
+    @classmethod
     def plane_sum(cls, hm: np.ndarray) -> np.ndarray:
         """The reference's own numpy float32 sum over (H, W) (explainer.py:120, :161): 0 + numpy's
         pairwise summation, which the heatmap_sort kernels reproduce bit for bit."""
         return np.asarray(hm, dtype=np.float32).sum(axis=(-2, -1))
+
+
+def proj_residual(U: torch.Tensor) -> torch.Tensor:
+    """fl32(U U^T - I) with each entry one float64 fma chain over k ascending, then minus the
+    identity, rounded once (drsa_amd_projection_residual)."""
+    Ud = U.detach().double()
+    d = Ud.size(0)
+    P = torch.zeros(d, d, dtype=torch.float64)
+    for k in range(d):                       # k-ascending accumulation, as the kernel
+        P += Ud[:, k:k + 1] * Ud[:, k:k + 1].t()
+    return (P - torch.eye(d, dtype=torch.float64)).float()
 
 
 def _bf16r(t: torch.Tensor) -> torch.Tensor:
@@ -294,6 +318,10 @@ class Bf16Ops(TorchOps):
     @staticmethod
     def matmul(a, b):
         return ExactOps.matmul(a, b).to(a.dtype)
+
+    @staticmethod
+    def inv_projection(L, h, a_map):
+        return ExactOps.inv_projection(L, h, a_map).to(a_map.dtype)
 
 
 # "f64": the analytic structure evaluated in float64 (model and input promoted): the accuracy
@@ -567,8 +595,12 @@ def lrp(model: nn.Module, rules: Dict[str, RuleSpec], x: torch.Tensor, class_idx
             m = L.module
             out, aux = F.max_pool2d(h, m.kernel_size, m.stride, m.padding, m.dilation,
                                     m.ceil_mode, return_indices=True)
+        elif L.kind == "invproj" and hasattr(ops, "inv_projection"):
+            out = ops.inv_projection(L, h, proj_in)
         else:
             out = _layer_fwd(L, h, ops)
+        if L.kind == "proj":
+            proj_in = h
         acts.append((h, out, aux))
         h = out
     logits = h
@@ -601,10 +633,12 @@ def class_composite_rules(name_map: Dict[str, RuleSpec], K: int) -> Dict[str, Ru
 
 def numpy_pairwise_sum(a: np.ndarray) -> np.float32:
     """numpy's float32 add-reduce of a contiguous run (the order sort_subspaces' ``sum(axis=(-2,
-    -1))`` uses, explainer.py:161): n < 8 a left-to-right chain from 0; n <= 128 eight stride-8
+    -1))`` uses, explainer.py:161).  The reduction iterator hands the inner loop chunks of at most
+    8192 elements (numpy's buffer size) and folds them left to right into the identity 0; each
+    chunk is summed pairwise: n < 8 a left-to-right chain from 0; n <= 128 eight stride-8
     accumulators combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) plus the n % 8 tail; otherwise the
-    two halves split at n/2 - (n/2 % 8).  The reduce adds the result to the identity 0.  Scalar
-    restatement of what heatmap_sort_kernel computes (small inputs only: pure Python)."""
+    two halves split at n/2 - (n/2 % 8).  Scalar restatement of what heatmap_sort_kernel computes
+    (small inputs only: pure Python)."""
     f = np.float32
     a = np.asarray(a, dtype=np.float32).reshape(-1)
 
@@ -628,7 +662,10 @@ def numpy_pairwise_sum(a: np.ndarray) -> np.float32:
         n2 = n // 2
         n2 -= n2 % 8
         return f(pw(lo, n2) + pw(lo + n2, n - n2))
-    return f(f(0) + pw(0, a.size))
+    acc = f(0)
+    for lo in range(0, a.size, 8192):
+        acc = f(acc + pw(lo, min(8192, a.size - lo)))
+    return acc
 
 
 def sort_subspaces(sub: np.ndarray, ops=TorchOps):

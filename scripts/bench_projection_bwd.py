@@ -18,6 +18,8 @@ den = torch.rand(B, D, H, W, device=dev) + 0.5
 U = torch.from_numpy(np.linalg.qr(np.random.default_rng(0).standard_normal((D, D)))[0].astype(np.float32)).to(dev)
 G = torch.empty(B * (K + 1), D, H, W, device=dev)
 s = _capi.stream_ptr()
+P = torch.empty_like(U)
+_capi.call("drsa_amd_projection_residual", U.data_ptr(), D, P.data_ptr(), s)
 
 
 RC = os.environ.get("RC", "1") == "1"   # recompute h and a' (engine default) vs stored buffers
@@ -26,7 +28,7 @@ RC = os.environ.get("RC", "1") == "1"   # recompute h and a' (engine default) vs
 def run():
     _capi.call("drsa_amd_projection_bwd", g.data_ptr(), amax.data_ptr(), None if RC else ap.data_ptr(),
                None if RC else h.data_ptr(), a.data_ptr(),
-               den.data_ptr(), U.data_ptr(), G.data_ptr(), B, D, H, W, K, 1e-6, 1e-7, 1, s)
+               den.data_ptr(), U.data_ptr(), P.data_ptr(), G.data_ptr(), B, D, H, W, K, 1e-6, 1e-7, 1, s)
 
 
 for _ in range(3):

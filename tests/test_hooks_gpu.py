@@ -4,10 +4,9 @@ A composite that maps a module to a user-written Hook (its own ``backward``) can
 into the HIP plan; ``get_engine`` routes it to ``HookedAutograd`` (torch autograd on the device
 with zennit-style module hooks).  Gates:
 * routing: the custom composite gets the slow path, the same name map without it the HIP plan;
-* the slow path's built-in rules (no custom hook, forced) agree with the HIP plan, which is
-  bit-exact vs the oracle, to fp32 reordering: per-sample relative L2 error <= 1e-3 (torch's
-  conv order vs the plan's k-ordered chains; measured 2.7e-4 on these inputs, the same envelope
-  as the oracle's exact-vs-analytic modes, DESIGN.md 5);
+* the slow path's built-in rules (no custom hook, forced) against the float64 oracle at the C2
+  bounds of the HIP plan (lrp_common.f64_anchored_check: median <= 2x, p75 <= 4x the
+  reference fp32 path's per-sample relative L2 error), and against the HIP plan at 1e-3;
 * an identity custom hook on a ReLU reproduces the plan's heatmaps, a doubling one gives twice
   them (every rule is linear in the incoming relevance), for compute_relevances and for
   HeatmapGenerator (K+1 replicated batch, reference explainer.py:92-104; there against the
@@ -60,13 +59,20 @@ def test_routing(net):
 
 
 def test_builtin_rules_match_plan(net):
-    x = logmel(4, seed=5).to(DEV)
+    import lrp_ref
+    from lrp_common import f64_anchored_check, spec
+    x = logmel(32, seed=5)
     comp = NameMapComposite(LRP_NAME_MAP_GTZAN)
-    R_plan = compute_relevances(net, x, comp, class_idx=2)
+    R_plan = compute_relevances(net, x.to(DEV), comp, class_idx=2)
     slow = HookedAutograd(net, comp)
-    slow.forward(x)
-    R_slow = slow.backward(cls=torch.full((4,), 2, device=DEV, dtype=torch.int32))
+    slow.forward(x.to(DEV))
+    R_slow = slow.backward(cls=torch.full((32,), 2, device=DEV, dtype=torch.int32))
     assert _rel(R_slow, R_plan) <= TOL
+    cpu = copy.deepcopy(net).cpu()
+    nm = spec(LRP_NAME_MAP_GTZAN)
+    _, R64 = lrp_ref.lrp(cpu, nm, x, class_idx=2, mode="f64")
+    _, Ra = lrp_ref.lrp(cpu, nm, x, class_idx=2, mode="analytic")
+    f64_anchored_check(R_slow.cpu(), Ra, R64)
 
 
 @pytest.mark.parametrize("hook,scale", [(Same(), 1.0), (Doubling(), 2.0)])
@@ -81,13 +87,14 @@ def test_custom_hook_compute_relevances(net, hook, scale):
 def test_custom_hook_heatmap_generator(net):
     """HeatmapGenerator through the slow path (K+1 replicated batch, a doubling hook on
     features.1): heatmaps / 2 against the float64 oracle, next to the reference's fp32 path
-    (lrp_common.f64_anchored_check with the C3 bounds of test_lrp_gpu.py), and the sort order."""
+    (lrp_common.f64_anchored_check at the C2 bounds: the slow path replicates the reference's
+    K+1 batch in torch's order, so it sits next to the reference's own fp32 errors)."""
     import numpy as np
     import lrp_ref
     from drsa_audio_amd.model.modify_model import ProjectionModel
     from lrp_common import f64_anchored_check, spec
     U = ortho(64, 3).float()
-    x = logmel(8, seed=7)
+    x = logmel(16, seed=7)
     cpu = copy.deepcopy(net).cpu()
     pm = ProjectionModel(cpu, 7, U, 4).eval()
     nm = spec(LRP_NAME_MAP_GTZAN)
@@ -98,15 +105,14 @@ def test_custom_hook_heatmap_generator(net):
     assert isinstance(get_engine(hg2.projectionmodel, hg2.composite), HookedAutograd)
     hg2.generate_subspace_heatmaps(x.to(DEV), to_host=True)
     info = {k: (v / 2 if k != "mask" else v) for k, v in hg2.info.items()}
-    f64_anchored_check(info["standard_heatmaps"], oa["standard_heatmaps"], o64["standard_heatmaps"],
-                       ratio_med=8.0, ratio_p75=8.0)
+    f64_anchored_check(info["standard_heatmaps"], oa["standard_heatmaps"], o64["standard_heatmaps"])
 
     def unsort(o):
         inv = np.argsort(o["mask"], axis=1)
         return np.take_along_axis(o["subspace_heatmaps"], inv[:, :, None, None], 1)
     for k in range(4):
-        f64_anchored_check(unsort(info)[:, k], unsort(oa)[:, k], unsort(o64)[:, k], ratio_med=8.0, ratio_p75=8.0)
-    assert info["subspace_heatmaps"].shape == (8, 4, 128, 128)
+        f64_anchored_check(unsort(info)[:, k], unsort(oa)[:, k], unsort(o64)[:, k])
+    assert info["subspace_heatmaps"].shape == (16, 4, 128, 128)
 
 
 def test_slow_path_refuses_host_input(net):

@@ -66,6 +66,6 @@ def test_numpy_pairwise_restatement():
     """The summation order the heatmap_sort kernels implement, restated, equals numpy's float32
     sum for the balanced, serial-walk, single-leaf, tail and n < 8 cases."""
     rng = np.random.default_rng(3)
-    for n in (4, 7, 8, 36, 64, 128, 136, 256, 1872, 4096, 1000, 16384):
+    for n in (4, 7, 8, 36, 64, 128, 136, 256, 1872, 4096, 1000, 8192, 10000, 16384, 20000, 32768):
         x = (rng.standard_normal(n) * np.exp(rng.standard_normal(n) * 2)).astype(np.float32)
         assert lrp_ref.numpy_pairwise_sum(x) == x.reshape(1, -1).sum(axis=-1)[0], n

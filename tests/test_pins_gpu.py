@@ -73,10 +73,13 @@ def test_projection_bwd_clone_mask_equals_reference_hook(pins):
         a = torch.ones(Bq, D, H, W, device=DEV)
         U = torch.eye(D, device=DEV)
         G = torch.empty_like(a)
+        P = torch.empty_like(U)
+        _capi.call("drsa_amd_projection_residual", U.data_ptr(), D, P.data_ptr(), s)
+        assert torch.count_nonzero(P) == 0                   # U = I: the residual vanishes
         # replicated-batch rows (fanout 0: row b is clone b mod (K+1)), no pool, no division below;
         # with U = I, a = 1 and zero stabilisers: R_h = gp, masked, R_a = mask(R_h) exactly
         _capi.call("drsa_amd_projection_bwd", gp.data_ptr(), None, None, None, a.data_ptr(), None, U.data_ptr(),
-                   G.data_ptr(), Bq, D, H, W, K, 0.0, 0.0, 0, s)
+                   P.data_ptr(), G.data_ptr(), Bq, D, H, W, K, 0.0, 0.0, 0, s)
         torch.cuda.synchronize()
         got = G.reshape(Bq, D, n).transpose(1, 2).reshape(Bq, n, K, dk).cpu().numpy()
         assert np.array_equal(got, ref), tag

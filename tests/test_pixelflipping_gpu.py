@@ -81,10 +81,25 @@ def test_pixelflipping_config_vs_oracle(ci):
     assert aupc[name].shape == (10, 1) and np.all(np.isfinite(aupc[name]))
 
 
+def test_engine_forward_aupc_close_to_torch_forward():
+    """forward='engine' (HIP forward, steps fused in chunks of fuse_max_rows rows) against the
+    default model(x) forward: AUPC within 1e-4 relative + 1e-4 absolute (fp32 accumulation order)."""
+    net = gtzan128()
+    x = logmel(10, seed=71)
+    conf = CONFIGS[0]
+    out = {}
+    for fw in ("torch", "engine"):
+        pf = PixelFlipping(net, x, perturbation_size=16, num_classes=10, device=DEV, forward=fw, fuse_max_rows=50)
+        aupc, preds, flips, _ = pf([conf], plot=False)
+        out[fw] = (aupc[pf._get_configuration_name(conf)], preds[pf._get_configuration_name(conf)])
+    np.testing.assert_allclose(out["engine"][0], out["torch"][0], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(out["engine"][1], out["torch"][1], rtol=1e-4, atol=1e-4)
+
+
 def test_engine_forward_equals_torch_forward_scores():
     net = gtzan128()
     x = logmel(10, seed=70)
-    pf = PixelFlipping(net, x, perturbation_size=16, num_classes=10, device=DEV)
+    pf = PixelFlipping(net, x, perturbation_size=16, num_classes=10, device=DEV, forward="engine")
     fe = pf._forward_func(None)
     pf.forward = "torch"
     ft = pf._forward_func(None)
