@@ -198,6 +198,26 @@ __device__ __forceinline__ float p_operand(const float* __restrict__ P, int d, i
   return ok ? v : 0.f;
 }
 
+// P staged in LDS ([DP][DP + 16]: the four row groups of an MFMA operand read land on disjoint
+// bank quarters), zero outside d x d; read transposed like p_operand
+template <int DP>
+__device__ __forceinline__ void stage_p(float* Ps, const float* __restrict__ P, int d, int tid) {
+  constexpr int LP = DP + 16;
+  for (int i = tid; i < DP * DP; i += 256) {
+    const int k = i / DP, c = i % DP;
+    const bool ok = k < d && c < d;
+    const float v = P[ok ? k * d + c : 0];
+    Ps[k * LP + c] = ok ? v : 0.f;
+  }
+}
+template <int DP, bool PL>
+__device__ __forceinline__ float p_op(const float* Ps, const float* __restrict__ P, int d, int c, int k) {
+  if constexpr (PL) return Ps[k * (DP + 16) + c];
+  else return p_operand(P, d, c, k);
+}
+template <int DP, bool PL>
+constexpr size_t p_lds_floats() { return PL ? (size_t)DP * (DP + 16) : 0; }
+
 constexpr int PT = 4;   // row-pair tiles per workgroup
 
 template <int DP>
@@ -211,7 +231,7 @@ __device__ __forceinline__ void stage_u_padded(float* Us, const float* __restric
   }
 }
 
-template <int DP, bool PAD>
+template <int DP, bool PAD, bool PLDS>
 __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __restrict__ a, const float* __restrict__ U,
                                                             const float* __restrict__ Pm,
                                                             float* __restrict__ h, float* __restrict__ ap,
@@ -222,13 +242,14 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* Us = sm;               // [DP][LD]   U[c][j]
   float* as = Us + DP * LD;     // [DP][PL]   a tile, then a' tile
-  float* hs = as + DP * PL;     // [DP][PL]   h tile
+  float* Ps = as + DP * PL;     // [DP][DP + 16] P (when PLDS)
   const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
   const int b = blockIdx.y;
   const int TW = W < 32 ? W : 32, RPT = P / TW;      // tile = RPT rows x TW cols
   const int HW = H * W, xt = W / TW;
   const int d4 = (d + 3) & ~3;
   stage_u_padded<DP>(Us, U, d, tid);
+  if constexpr (PLDS) stage_p<DP>(Ps, Pm, d, tid);
   constexpr int NB = DP / 16;
   static_assert(P / 16 == 4, "one 16-pixel block per wave");
   for (int t = 0; t < PT; ++t) {
@@ -243,50 +264,34 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
       as[c * PL + p] = ok ? v : 0.f;
     }
     __syncthreads();
-    // h[j][p] = sum_c U[c][j] a[c][p]: wave w owns pixel block w and runs the NB output blocks
-    // as independent MFMA chains sharing the B operand (same per-element k order as one chain)
+    // h[j][p] = sum_c U[c][j] a[c][p] and delta[c][p] = sum_k P[c][k] a[k][p]: wave w owns pixel
+    // block w and runs the 2 NB output blocks as independent MFMA chains sharing the B operand read
+    // (per element the single-chain k order); then a' = a + delta (= h U^T, residual form above)
     {
-      f32x4 acc[NB];
+      f32x4 acc[NB], dl[NB];
 #pragma unroll
-      for (int jb = 0; jb < NB; ++jb) acc[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int jb = 0; jb < NB; ++jb) acc[jb] = dl[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
       for (int k0 = 0; k0 < d4; k0 += 4) {
         const int c = k0 + (lane >> 4);
         const float bv = as[c * PL + w * 16 + (lane & 15)];
 #pragma unroll
-        for (int jb = 0; jb < NB; ++jb) acc[jb] = mfma16(Us[c * LD + jb * 16 + (lane & 15)], bv, acc[jb]);
+        for (int jb = 0; jb < NB; ++jb) {
+          acc[jb] = mfma16(Us[c * LD + jb * 16 + (lane & 15)], bv, acc[jb]);
+          dl[jb] = mfma16(p_op<DP, PLDS>(Ps, Pm, d, jb * 16 + (lane & 15), c), bv, dl[jb]);
+        }
       }
+      // every wave reads and writes only its own 16 pixel columns of the tile
 #pragma unroll
       for (int jb = 0; jb < NB; ++jb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int j = jb * 16 + (lane >> 4) * 4 + r, p = w * 16 + (lane & 15);
-          hs[j * PL + p] = acc[jb][r];
-          if (h && j < d) h[((size_t)b * d + j) * HW + (y0 + p / TW) * W + x0 + p % TW] = acc[jb][r];
-        }
-    }
-    __syncthreads();
-    // a'[c][p] = a[c][p] + sum_k P[c][k] a[k][p]   (= sum_j U[c][j] h[j][p]; residual form, above)
-    {
-      f32x4 acc[NB];
-#pragma unroll
-      for (int cb = 0; cb < NB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-      for (int k0 = 0; k0 < d4; k0 += 4) {
-        const int k = k0 + (lane >> 4);
-        const float bv = as[k * PL + w * 16 + (lane & 15)];
-#pragma unroll
-        for (int cb = 0; cb < NB; ++cb) acc[cb] = mfma16(p_operand(Pm, d, cb * 16 + (lane & 15), k), bv, acc[cb]);
-      }
-      // every wave reads and writes only its own 16 pixel columns of the tile
-#pragma unroll
-      for (int cb = 0; cb < NB; ++cb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = cb * 16 + (lane >> 4) * 4 + r, p = w * 16 + (lane & 15);
-          const float v = as[c * PL + p] + acc[cb][r];
-          as[c * PL + p] = v;   // a tile no longer needed: holds a' now
-          if (ap && c < d) ap[((size_t)b * d + c) * HW + (y0 + p / TW) * W + x0 + p % TW] = v;
+          const size_t og = ((size_t)b * d + j) * HW + (y0 + p / TW) * W + x0 + p % TW;
+          if (h && j < d) h[og] = acc[jb][r];
+          const float v = as[j * PL + p] + dl[jb][r];
+          as[j * PL + p] = v;   // a tile no longer needed: holds a' now
+          if (ap && j < d) ap[og] = v;
         }
     }
     if (pool) {
@@ -477,7 +482,7 @@ constexpr int PT_RC = DRSA_PT_RC;   // tiles per workgroup (U staged once)
 #define DRSA_PROJ_RC_WPE 3
 #endif
 
-template <int DP, bool PAD>
+template <int DP, bool PAD, bool PLDS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? DRSA_PROJ_RC_WPE : 1))) void projection_bwd_rc_kernel(
     const float* __restrict__ gp, const uint8_t* __restrict__ amax, const float* __restrict__ a,
     const float* __restrict__ den, const float* __restrict__ U, const float* __restrict__ Pm, float* __restrict__ G,
@@ -490,6 +495,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
   float* Us = sm;                                   // [DP][LD]
   float* RA = Us + DP * LD + w * 2 * DP * PW;       // [DP][PW]
   float* RB = RA + DP * PW;                         // [DP][PW]
+  float* Ps = Us + DP * LD + 4 * 2 * DP * PW;       // [DP][DP + 16] P (when PLDS)
   const int b = blockIdx.y;
   const int TW = W < 32 ? W : 32, RPT = P / TW;
   const int HW = H * W, xt = W / TW, H2 = H / 2, W2 = W / 2;
@@ -497,6 +503,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
   const int nq = fanout ? (K + 1) : 1;
   const int pc = lane & 15, rg = lane >> 4;         // pixel column / row group of the MFMA layouts
   stage_u_padded<DP>(Us, U, d, tid);
+  if constexpr (PLDS) stage_p<DP>(Ps, Pm, d, tid);
   __syncthreads();
   for (int t = 0; t < PT_RC; ++t) {
     const int tile = blockIdx.x * PT_RC + t;
@@ -542,7 +549,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
         for (int r = 0; r < 4; ++r) RB[(jb * 16 + rg * 4 + r) * PW + pc] = acc[jb][r];
     }
     __builtin_amdgcn_wave_barrier();
-    // a'[c][p] = a[c][p] + sum_k P[c][k] a[k][p]   (projection_fwd_kernel order);
+    // a'[c][p] = a[c][p] + sum_k P[c][k] a[k][p]   (projection_fwd_kernel order; a separate pass:
+    // folded into the h GEMM above, the second accumulator set spills at 3 waves/SIMD);
     // g1 = R_a' / stab(a')  -> region A (in place of a; a stays in registers)
     {
       f32x4 acc[NB];
@@ -553,7 +561,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
         const int k = k0 + rg;
         const float bv = RA[k * PW + pc];
 #pragma unroll
-        for (int cb = 0; cb < NB; ++cb) acc[cb] = mfma16(p_operand(Pm, d, cb * 16 + pc, k), bv, acc[cb]);
+        for (int cb = 0; cb < NB; ++cb) acc[cb] = mfma16(p_op<DP, PLDS>(Ps, Pm, d, cb * 16 + pc, k), bv, acc[cb]);
       }
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -1020,61 +1028,48 @@ __global__ __launch_bounds__(256) void heatmap_sort_kernel(const float* __restri
 // headline) each thread keeps its 16 float4 of the K subspace maps in registers (one workgroup per
 // CU; the kernel is HBM-bound) and copies the standard map while loading it, so the sorted writes
 // need no second read.  The numpy pairwise sums need each accumulator chain (stride-8 elements of
-// one 128-element leaf) in one thread: every map goes through LDS once, stored at a leaf stride of
-// 136 floats so that both the coalesced float4 stores and the chain-ordered float4 reads of thread
-// (leaf t/2, half t%2) are bank-conflict-free.  Outputs equal heatmap_sort_kernel's.
+// one 128-element leaf) in one thread, so thread t = (leaf t/2, half t%2) loads the float4s
+// 32 leaf + 2 i + half, i = 0..15: its four chains in order (a wave's load covers 32 B of each of
+// 32 leaves; the four loads i..i+3 complete each 128-B line).  Outputs equal heatmap_sort_kernel's.
 template <int KC, int NV4>
 __global__ __launch_bounds__(256) void heatmap_sort_cached_kernel(const float* __restrict__ hm, float* __restrict__ std_out,
                                                                   float* __restrict__ std_rel,
                                                                   float* __restrict__ sub_out, float* __restrict__ rel,
                                                                   int64_t* __restrict__ mask) {
   constexpr int HW = NV4 * 1024;
-  constexpr int LEAVES = HW / 128;        // 128 at 128x128: thread t = (leaf t/2, half t%2)
-  static_assert(LEAVES * 2 == 256, "cached sort: one (leaf, half) per thread");
-  constexpr int LS = 136;                  // padded leaf stride (floats)
-  __shared__ float4 lds4[LEAVES * LS / 4];
+  static_assert(HW / 128 * 2 == 256 && NV4 == 16, "cached sort: one (leaf, half) per thread, 16 float4 each");
   __shared__ float red[KC + 1][4];
   __shared__ float sums[KC + 1];
   __shared__ int order[KC];
-  float* lds = reinterpret_cast<float*>(lds4);
   const int b = blockIdx.x, tid = threadIdx.x;
-  const float4* base = reinterpret_cast<const float4*>(hm + (size_t)b * (KC + 1) * HW);
-  float4* so = reinterpret_cast<float4*>(std_out + (size_t)b * HW);
+  const int L = tid >> 1, hh = tid & 1;
+  const float4* base = reinterpret_cast<const float4*>(hm + (size_t)b * (KC + 1) * HW) + 32 * L + hh;
+  float4* so = reinterpret_cast<float4*>(std_out + (size_t)b * HW) + 32 * L + hh;
   float4 v[KC][NV4];
   float s[KC + 1];
-  // float4 f = tid + 256 j  ->  leaf f / 32, offset 4 (f % 32)
-  auto stage = [&](const float4* w) {
+  auto chain = [&](const float4* x) -> float {   // pw_half on registers, then the leaf
+    float4 r = x[0];
 #pragma unroll
-    for (int j = 0; j < NV4; ++j) {
-      const int f = tid + 256 * j;
-      *reinterpret_cast<float4*>(lds + (f >> 5) * LS + 4 * (f & 31)) = w[j];
+    for (int i = 1; i < NV4; ++i) {
+      r.x = r.x + x[i].x; r.y = r.y + x[i].y; r.z = r.z + x[i].z; r.w = r.w + x[i].w;
     }
-  };
-  auto chain = [&]() -> float {
-    const float p = pw_half(reinterpret_cast<const float4*>(lds + (tid >> 1) * LS), tid & 1);
-    return p + shfl_xor(p, 1);           // the leaf (commutative: both halves get the same bits)
+    const float p = (r.x + r.y) + (r.z + r.w);
+    return p + shfl_xor(p, 1);
   };
   {
     float4 w[NV4];
 #pragma unroll
-    for (int j = 0; j < NV4; ++j) w[j] = base[tid + 256 * j];
+    for (int i = 0; i < NV4; ++i) w[i] = base[2 * i];
 #pragma unroll
-    for (int j = 0; j < NV4; ++j) so[tid + 256 * j] = w[j];
-    stage(w);
+    for (int q = 0; q < KC; ++q)
+#pragma unroll
+      for (int i = 0; i < NV4; ++i) v[q][i] = base[(size_t)(1 + q) * (HW / 4) + 2 * i];
+#pragma unroll
+    for (int i = 0; i < NV4; ++i) so[2 * i] = w[i];
+    s[0] = chain(w);
   }
 #pragma unroll
-  for (int q = 0; q < KC; ++q)
-#pragma unroll
-    for (int j = 0; j < NV4; ++j) v[q][j] = base[(size_t)(1 + q) * (HW / 4) + tid + 256 * j];
-  __syncthreads();
-  s[0] = chain();
-#pragma unroll
-  for (int q = 0; q < KC; ++q) {
-    __syncthreads();
-    stage(v[q]);
-    __syncthreads();
-    s[1 + q] = chain();
-  }
+  for (int q = 0; q < KC; ++q) s[1 + q] = chain(v[q]);
   // balanced tree over the leaves: lanes 2L, 2L+1 hold leaf L; in-wave butterfly over L; waves
   // 0-1 hold the first 8192-element chunk, 2-3 the second: (0 + (w0 + w1)) + (w2 + w3)
 #pragma unroll
@@ -1097,12 +1092,12 @@ __global__ __launch_bounds__(256) void heatmap_sort_cached_kernel(const float* _
 #pragma unroll
   for (int k = 0; k < KC; ++k) {
     const int src = order[k];   // uniform: the branch below is a scalar one
-    float4* dst = reinterpret_cast<float4*>(sub_out + ((size_t)b * KC + k) * HW);
+    float4* dst = reinterpret_cast<float4*>(sub_out + ((size_t)b * KC + k) * HW) + 32 * L + hh;
 #pragma unroll
     for (int q = 0; q < KC; ++q)
       if (src == q) {
 #pragma unroll
-        for (int j = 0; j < NV4; ++j) dst[tid + 256 * j] = v[q][j];
+        for (int i = 0; i < NV4; ++i) dst[2 * i] = v[q][i];
       }
   }
 }
@@ -1161,12 +1156,23 @@ int with_lds(F* fn, size_t lds) {
 // padded projection width: the smallest instantiated DP >= d (0 = unsupported)
 int proj_dp(int d) { return d < 1 ? 0 : d <= 16 ? 16 : d <= 32 ? 32 : d <= 64 ? 64 : d <= 128 ? 128 : 0; }
 
-template <int D>
-size_t proj_fwd_lds() { return ((size_t)D * (D + 1) + 2 * (size_t)D * 68) * sizeof(float); }
+template <int D, bool PL>
+size_t proj_fwd_lds() { return ((size_t)D * (D + 1) + (size_t)D * 68 + p_lds_floats<D, PL>()) * sizeof(float); }
 template <int D>
 size_t proj_bwd_lds() { return ((size_t)D * (D + 1) + 2 * (size_t)D * 68) * sizeof(float); }
-template <int D>
-size_t proj_bwd_rc_lds() { return ((size_t)D * (D + 1) + 4 * 2 * (size_t)D * 16) * sizeof(float); }
+template <int D, bool PL>
+size_t proj_bwd_rc_lds() { return ((size_t)D * (D + 1) + 4 * 2 * (size_t)D * 16 + p_lds_floats<D, PL>()) * sizeof(float); }
+
+// P of the projection kernels in LDS (DP <= 64) or read through L1 (DP = 128 always: U and P
+// together would exceed the LDS).  Forward: LDS (its h tile is gone, so P fits at the same
+// occupancy); backward: L1 (0.524 vs 0.537 ms at B = 512, d = 64: the LDS copy costs a workgroup
+// per CU).  DRSA_AMD_PROJ_PLDS=0 / 1 forces either for both.
+int proj_p_lds_env() {
+  static const int v = getenv("DRSA_AMD_PROJ_PLDS") ? atoi(getenv("DRSA_AMD_PROJ_PLDS")) : -1;
+  return v;
+}
+bool proj_p_lds_fwd() { return proj_p_lds_env() != 0; }
+bool proj_p_lds_bwd() { return proj_p_lds_env() == 1; }
 
 }  // namespace
 
@@ -1224,9 +1230,13 @@ int drsa_amd_projection_fwd(const float* a, const float* U, const float* P, floa
   switch (proj_dp(D)) {
 #define PF(DD)                                                                                        \
   case DD: {                                                                                          \
-    auto kf = D == DD ? projection_fwd_kernel<DD, false> : projection_fwd_kernel<DD, true>;        \
-    { int rc = with_lds(kf, proj_fwd_lds<DD>()); if (rc) return rc; }                               \
-    hipLaunchKernelGGL(kf, grid, dim3(256), proj_fwd_lds<DD>(), s, a, U, P, h, ap, pooled, amax,       \
+    constexpr bool PLC = DD <= 64;                                                                  \
+    const bool pl = PLC && proj_p_lds_fwd();                                                        \
+    auto kf = D == DD ? (pl ? projection_fwd_kernel<DD, false, PLC> : projection_fwd_kernel<DD, false, false>)  \
+                      : (pl ? projection_fwd_kernel<DD, true, PLC> : projection_fwd_kernel<DD, true, false>);   \
+    const size_t lds = pl ? proj_fwd_lds<DD, PLC>() : proj_fwd_lds<DD, false>();                    \
+    { int rc = with_lds(kf, lds); if (rc) return rc; }                                              \
+    hipLaunchKernelGGL(kf, grid, dim3(256), lds, s, a, U, P, h, ap, pooled, amax,                    \
                        D, H, W, pool);                                                                \
     break;                                                                                            \
   }
@@ -1257,9 +1267,13 @@ int drsa_amd_projection_bwd(const float* gp, const uint8_t* amax, const float* a
     switch (proj_dp(D)) {
 #define PR(DD)                                                                                        \
   case DD: {                                                                                          \
-    auto kr = D == DD ? projection_bwd_rc_kernel<DD, false> : projection_bwd_rc_kernel<DD, true>;  \
-    { int rc = with_lds(kr, proj_bwd_rc_lds<DD>()); if (rc) return rc; }                            \
-    hipLaunchKernelGGL(kr, grid, dim3(256), proj_bwd_rc_lds<DD>(), s, gp, amax, a, den, U, P, G,     \
+    constexpr bool PLC = DD <= 64;                                                                  \
+    const bool pl = PLC && proj_p_lds_bwd();                                                        \
+    auto kr = D == DD ? (pl ? projection_bwd_rc_kernel<DD, false, PLC> : projection_bwd_rc_kernel<DD, false, false>) \
+                      : (pl ? projection_bwd_rc_kernel<DD, true, PLC> : projection_bwd_rc_kernel<DD, true, false>);  \
+    const size_t lds = pl ? proj_bwd_rc_lds<DD, PLC>() : proj_bwd_rc_lds<DD, false>();              \
+    { int rc = with_lds(kr, lds); if (rc) return rc; }                                              \
+    hipLaunchKernelGGL(kr, grid, dim3(256), lds, s, gp, amax, a, den, U, P, G,                       \
                        D, H, W, K, eps_proj, eps_den, sparse, has_den, fanout);                      \
     break;                                                                                            \
   }
