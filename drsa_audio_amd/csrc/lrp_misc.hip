@@ -251,6 +251,16 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
   stage_u_padded<DP>(Us, U, d, tid);
   if constexpr (PLDS) stage_p<DP>(Ps, Pm, d, tid);
   constexpr int NB = DP / 16;
+  // unpadded DP <= 64: the residual's MFMA A operands (P[c][k], read as the symmetric P[k][c]) live
+  // in registers for the whole launch: NB * DP / 4 floats per lane
+  constexpr bool PREG = !PAD && !PLDS && DP <= 64;
+  float preg[PREG ? NB * (DP / 4) : 1];
+  if constexpr (PREG) {
+#pragma unroll
+    for (int jb = 0; jb < NB; ++jb)
+#pragma unroll
+      for (int ks = 0; ks < DP / 4; ++ks) preg[jb * (DP / 4) + ks] = Pm[(ks * 4 + (lane >> 4)) * DP + jb * 16 + (lane & 15)];
+  }
   static_assert(P / 16 == 4, "one 16-pixel block per wave");
   for (int t = 0; t < PT; ++t) {
     const int tile = blockIdx.x * PT + t;
@@ -271,14 +281,27 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
       f32x4 acc[NB], dl[NB];
 #pragma unroll
       for (int jb = 0; jb < NB; ++jb) acc[jb] = dl[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-      for (int k0 = 0; k0 < d4; k0 += 4) {
-        const int c = k0 + (lane >> 4);
-        const float bv = as[c * PL + w * 16 + (lane & 15)];
+      if constexpr (PREG) {
 #pragma unroll
-        for (int jb = 0; jb < NB; ++jb) {
-          acc[jb] = mfma16(Us[c * LD + jb * 16 + (lane & 15)], bv, acc[jb]);
-          dl[jb] = mfma16(p_op<DP, PLDS>(Ps, Pm, d, jb * 16 + (lane & 15), c), bv, dl[jb]);
+        for (int k0 = 0; k0 < DP; k0 += 4) {
+          const int c = k0 + (lane >> 4);
+          const float bv = as[c * PL + w * 16 + (lane & 15)];
+#pragma unroll
+          for (int jb = 0; jb < NB; ++jb) {
+            acc[jb] = mfma16(Us[c * LD + jb * 16 + (lane & 15)], bv, acc[jb]);
+            dl[jb] = mfma16(preg[jb * (DP / 4) + k0 / 4], bv, dl[jb]);
+          }
+        }
+      } else {
+#pragma unroll 2
+        for (int k0 = 0; k0 < d4; k0 += 4) {
+          const int c = k0 + (lane >> 4);
+          const float bv = as[c * PL + w * 16 + (lane & 15)];
+#pragma unroll
+          for (int jb = 0; jb < NB; ++jb) {
+            acc[jb] = mfma16(Us[c * LD + jb * 16 + (lane & 15)], bv, acc[jb]);
+            dl[jb] = mfma16(p_op<DP, PLDS>(Ps, Pm, d, jb * 16 + (lane & 15), c), bv, dl[jb]);
+          }
         }
       }
       // every wave reads and writes only its own 16 pixel columns of the tile
@@ -1163,15 +1186,15 @@ size_t proj_bwd_lds() { return ((size_t)D * (D + 1) + 2 * (size_t)D * 68) * size
 template <int D, bool PL>
 size_t proj_bwd_rc_lds() { return ((size_t)D * (D + 1) + 4 * 2 * (size_t)D * 16 + p_lds_floats<D, PL>()) * sizeof(float); }
 
-// P of the projection kernels in LDS (DP <= 64) or read through L1 (DP = 128 always: U and P
-// together would exceed the LDS).  Forward: LDS (its h tile is gone, so P fits at the same
-// occupancy); backward: L1 (0.524 vs 0.537 ms at B = 512, d = 64: the LDS copy costs a workgroup
-// per CU).  DRSA_AMD_PROJ_PLDS=0 / 1 forces either for both.
+// Where the projection kernels keep the residual P: in LDS (DRSA_AMD_PROJ_PLDS=1, DP <= 64), else
+// the forward holds its MFMA operands in registers (unpadded DP <= 64; 0.139 ms at B = 512, d = 64,
+// vs 0.161 from LDS, which costs a workgroup per CU) and the backward reads them through L1
+// (0.524 vs 0.537 ms from LDS; registers would cost it a wave per SIMD).
 int proj_p_lds_env() {
   static const int v = getenv("DRSA_AMD_PROJ_PLDS") ? atoi(getenv("DRSA_AMD_PROJ_PLDS")) : -1;
   return v;
 }
-bool proj_p_lds_fwd() { return proj_p_lds_env() != 0; }
+bool proj_p_lds_fwd() { return proj_p_lds_env() == 1; }
 bool proj_p_lds_bwd() { return proj_p_lds_env() == 1; }
 
 }  // namespace
