@@ -60,9 +60,10 @@ def load_u():
 
 
 # --------------------------------------------------------------------------- FLOP model
-def kernel_macs(eng, B, K):
+def kernel_macs(eng, B, K, standard="sum"):
     """Algorithmic multiply-accumulates per launch of each kernel tag for one batch of B
-    explained samples ('Algorithmic work')."""
+    explained samples ('Algorithmic work').  standard="sum": K relevance clones below
+    the projection (the standard heatmap is their sum); "clone": K+1."""
     macs = {}
     rec = eng.last["stages"]
     clones_below = False
@@ -72,9 +73,10 @@ def kernel_macs(eng, B, K):
         if st.proj is not None:
             d = st.cout
             macs["projection_fwd"] = B * h * w * d * d * 2
-            macs["projection_bwd"] = B * h * w * (d * d + d * d + d * d)   # g1 U, clone 0, K blocks
+            # g1 U, [clone 0,] the K concept blocks (d_k x d each)
+            macs["projection_bwd"] = B * h * w * (d * d + (d * d if standard == "clone" else 0) + d * d)
             clones_below = True
-        nq = (K + 1) if clones_below else 1
+        nq = (K + (1 if standard == "clone" else 0)) if clones_below else 1
         macs[f"conv_fwd:{st.name}"] = B * h * w * st.cout * st.cin * 9 * st.ng_fwd
         tag = f"first_layer_bwd:{st.name}" if (li == 0 and st.w2_first is not None) else f"conv_bwd:{st.name}"
         macs[tag] = B * nq * h * w * st.cout * st.cin * 9 * st.ng_bwd
@@ -547,7 +549,7 @@ def main():
         L = len(tags) // 3
         with open(args.tag_order, "w") as fh:
             json.dump({"tags": tags[:L], "main_steps": args.warmup + args.steps + 3, "batch": B}, fh)
-    macs = kernel_macs(eng, B, K)
+    macs = kernel_macs(eng, B, K, hg.standard)
     kernels = {}
     for tag, ts in per.items():
         avg = float(np.mean(ts))

@@ -57,7 +57,7 @@ SIGNATURES = {
     "drsa_amd_ab_combine": (_i32, [_fp, _fp, _f32, _f32, _fp, _fp, _fp, _i32, _i32, _i64, _i32, _f32, _vp]),
     "drsa_amd_first_layer_bwd": (_i32, [_fp, _vp, _fp, _fp, _i32, _i32, _i32, _i32, _i32, _vp]),
     "drsa_amd_first_layer_den": (_i32, [_fp, _fp, _fp, _i32, _i32, _i32, _i32, _vp]),
-    "drsa_amd_heatmap_sort": (_i32, [_fp, _i32, _i32, _i32, _fp, _fp, _fp, _fp, _vp, _vp]),
+    "drsa_amd_heatmap_sort": (_i32, [_fp, _i32, _i32, _i32, _i32, _fp, _fp, _fp, _fp, _vp, _vp]),
     "drsa_amd_maxpool_capture": (_i32, [_fp, _fp, _fp, _vp, _fp, _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
     "drsa_amd_relevance_unpool": (_i32, [_fp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _fp, _vp]),
     "drsa_amd_drsa_vectors": (_i32, [_fp, _fp, _vp, _ip, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _fp, _fp,

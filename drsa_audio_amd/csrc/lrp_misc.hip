@@ -381,7 +381,8 @@ __global__ __launch_bounds__(256) void projection_bwd_kernel(
   const int TW = W < 32 ? W : 32, RPT = P / TW;
   const int HW = H * W, xt = W / TW;
   const int dk = d / K, d4 = (d + 3) & ~3;
-  const int nq = fanout ? (K + 1) : 1;
+  // fanout 1: K+1 clones (standard + K subspaces); 2: the K subspace clones only; 0: replicated rows
+  const int nq = fanout == 1 ? (K + 1) : fanout == 2 ? K : 1;
   for (int t = 0; t < PT_BWD; ++t) {
     const int tile = blockIdx.x * PT_BWD + t;
     if (tile >= (H / RPT) * xt) break;
@@ -451,9 +452,9 @@ __global__ __launch_bounds__(256) void projection_bwd_kernel(
     }
     __syncthreads();
     for (int qi = 0; qi < nq; ++qi) {
-      const int q = fanout ? qi : b % (K + 1);
+      const int q = fanout == 1 ? qi : fanout == 2 ? qi + 1 : b % (K + 1);
       const int j0 = q == 0 ? 0 : (q - 1) * dk, j1 = q == 0 ? d : q * dk;
-      const size_t orow = fanout ? (size_t)b * (K + 1) + q : (size_t)b;
+      const size_t orow = fanout ? (size_t)b * nq + qi : (size_t)b;
 #pragma unroll
       for (int i = 0; i < QW; ++i) {
         const int cb = i, pb = w;
@@ -523,7 +524,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
   const int TW = W < 32 ? W : 32, RPT = P / TW;
   const int HW = H * W, xt = W / TW, H2 = H / 2, W2 = W / 2;
   const int dk = d / K, d4 = (d + 3) & ~3;
-  const int nq = fanout ? (K + 1) : 1;
+  // fanout 1: K+1 clones (standard + K subspaces); 2: the K subspace clones only; 0: replicated rows
+  const int nq = fanout == 1 ? (K + 1) : fanout == 2 ? K : 1;
   const int pc = lane & 15, rg = lane >> 4;         // pixel column / row group of the MFMA layouts
   stage_u_padded<DP>(Us, U, d, tid);
   if constexpr (PLDS) stage_p<DP>(Ps, Pm, d, tid);
@@ -631,9 +633,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
     }
     __builtin_amdgcn_wave_barrier();
     for (int qi = 0; qi < nq; ++qi) {
-      const int q = fanout ? qi : b % (K + 1);
+      const int q = fanout == 1 ? qi : fanout == 2 ? qi + 1 : b % (K + 1);
       const int j0 = q == 0 ? 0 : (q - 1) * dk, j1 = q == 0 ? d : q * dk;
-      const size_t orow = fanout ? (size_t)b * (K + 1) + q : (size_t)b;
+      const size_t orow = fanout ? (size_t)b * nq + qi : (size_t)b;
       f32x4 acc[NB];
 #pragma unroll
       for (int cb = 0; cb < NB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1013,7 +1015,7 @@ __device__ void sort_desc(const float* sums, int K, int* order) {   // descendin
   }
 }
 
-__global__ __launch_bounds__(256) void heatmap_sort_kernel(const float* __restrict__ hm, int K, int HW,
+__global__ __launch_bounds__(256) void heatmap_sort_kernel(const float* __restrict__ hm, int K, int HW, int std_sum,
                                                            float* __restrict__ std_out, float* __restrict__ std_rel,
                                                            float* __restrict__ sub_out, float* __restrict__ rel,
                                                            int64_t* __restrict__ mask) {
@@ -1022,10 +1024,27 @@ __global__ __launch_bounds__(256) void heatmap_sort_kernel(const float* __restri
   __shared__ float sums[65];
   __shared__ int order[64];
   const int b = blockIdx.x, tid = threadIdx.x;
-  const float* base = hm + (size_t)b * (K + 1) * HW;
-  for (int q = 0; q <= K; ++q) {
-    const float s = pw_sum_wg(base + (size_t)q * HW, HW, part, &bc);
-    if (tid == 0) sums[q] = s;
+  const int NM = std_sum ? K : K + 1;              // maps per sample in hm
+  const float* base = hm + (size_t)b * NM * HW;
+  const float* sub0 = base + (std_sum ? 0 : (size_t)HW);
+  float* so = std_out + (size_t)b * HW;
+  // the standard map: clone 0, or (std_sum) the sum of the K concept maps, k ascending
+  for (int i = tid * 4; i < HW; i += 256 * 4) {
+    float4 v = *reinterpret_cast<const float4*>(std_sum ? sub0 + i : base + i);
+    for (int k = 1; std_sum && k < K; ++k) {
+      const float4 u = *reinterpret_cast<const float4*>(sub0 + (size_t)k * HW + i);
+      v.x = v.x + u.x; v.y = v.y + u.y; v.z = v.z + u.z; v.w = v.w + u.w;
+    }
+    *reinterpret_cast<float4*>(so + i) = v;
+  }
+  __syncthreads();                                  // std_out complete and visible to the block
+  {
+    const float s0 = pw_sum_wg(so, HW, part, &bc);
+    if (tid == 0) sums[0] = s0;
+  }
+  for (int q = 0; q < K; ++q) {
+    const float sq = pw_sum_wg(sub0 + (size_t)q * HW, HW, part, &bc);
+    if (tid == 0) sums[1 + q] = sq;
   }
   __syncthreads();
   if (tid == 0) {
@@ -1037,10 +1056,8 @@ __global__ __launch_bounds__(256) void heatmap_sort_kernel(const float* __restri
     }
   }
   __syncthreads();
-  for (int i = tid * 4; i < HW; i += 256 * 4)
-    *reinterpret_cast<float4*>(std_out + (size_t)b * HW + i) = *reinterpret_cast<const float4*>(base + i);
   for (int k = 0; k < K; ++k) {
-    const float* src = base + (size_t)(1 + order[k]) * HW;
+    const float* src = sub0 + (size_t)order[k] * HW;
     float* dst = sub_out + ((size_t)b * K + k) * HW;
     for (int i = tid * 4; i < HW; i += 256 * 4)
       *reinterpret_cast<float4*>(dst + i) = *reinterpret_cast<const float4*>(src + i);
@@ -1054,7 +1071,7 @@ __global__ __launch_bounds__(256) void heatmap_sort_kernel(const float* __restri
 // one 128-element leaf) in one thread, so thread t = (leaf t/2, half t%2) loads the float4s
 // 32 leaf + 2 i + half, i = 0..15: its four chains in order (a wave's load covers 32 B of each of
 // 32 leaves; the four loads i..i+3 complete each 128-B line).  Outputs equal heatmap_sort_kernel's.
-template <int KC, int NV4>
+template <int KC, int NV4, bool SSUM>
 __global__ __launch_bounds__(256) void heatmap_sort_cached_kernel(const float* __restrict__ hm, float* __restrict__ std_out,
                                                                   float* __restrict__ std_rel,
                                                                   float* __restrict__ sub_out, float* __restrict__ rel,
@@ -1066,7 +1083,9 @@ __global__ __launch_bounds__(256) void heatmap_sort_cached_kernel(const float* _
   __shared__ int order[KC];
   const int b = blockIdx.x, tid = threadIdx.x;
   const int L = tid >> 1, hh = tid & 1;
-  const float4* base = reinterpret_cast<const float4*>(hm + (size_t)b * (KC + 1) * HW) + 32 * L + hh;
+  constexpr int NM = SSUM ? KC : KC + 1;            // maps per sample in hm
+  const float4* base = reinterpret_cast<const float4*>(hm + (size_t)b * NM * HW) + 32 * L + hh;
+  const float4* sub0 = base + (SSUM ? 0 : HW / 4);
   float4* so = reinterpret_cast<float4*>(std_out + (size_t)b * HW) + 32 * L + hh;
   float4 v[KC][NV4];
   float s[KC + 1];
@@ -1081,12 +1100,25 @@ __global__ __launch_bounds__(256) void heatmap_sort_cached_kernel(const float* _
   };
   {
     float4 w[NV4];
+    if constexpr (!SSUM) {
 #pragma unroll
-    for (int i = 0; i < NV4; ++i) w[i] = base[2 * i];
+      for (int i = 0; i < NV4; ++i) w[i] = base[2 * i];
+    }
 #pragma unroll
     for (int q = 0; q < KC; ++q)
 #pragma unroll
-      for (int i = 0; i < NV4; ++i) v[q][i] = base[(size_t)(1 + q) * (HW / 4) + 2 * i];
+      for (int i = 0; i < NV4; ++i) v[q][i] = sub0[(size_t)q * (HW / 4) + 2 * i];
+    if constexpr (SSUM) {   // the standard map = the concept maps summed, k ascending
+#pragma unroll
+      for (int i = 0; i < NV4; ++i) {
+        float4 t = v[0][i];
+#pragma unroll
+        for (int q = 1; q < KC; ++q) {
+          t.x = t.x + v[q][i].x; t.y = t.y + v[q][i].y; t.z = t.z + v[q][i].z; t.w = t.w + v[q][i].w;
+        }
+        w[i] = t;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < NV4; ++i) so[2 * i] = w[i];
     s[0] = chain(w);
@@ -1277,6 +1309,7 @@ int drsa_amd_projection_bwd(const float* gp, const uint8_t* amax, const float* a
                             const float* den, const float* U, const float* P, float* G, int B, int D, int H, int W,
                             int K, float eps_proj, float eps_den, int fanout, void* stream) {
   const int TW = W < 32 ? W : 32;
+  DRSA_REQUIRE(fanout >= 0 && fanout <= 2, "projection_bwd: fanout must be 0, 1 or 2");
   DRSA_REQUIRE(gp && a && U && G && ((ap && h) || P),
                "projection_bwd: gp, a, U, G and P (when h / a' are recomputed) are required");
   DRSA_REQUIRE((W == 8 || W == 16 || W % 32 == 0) && H % (64 / TW) == 0,
@@ -1357,17 +1390,18 @@ int drsa_amd_first_layer_den(const float* w2, const float* b2, float* den, int C
   return DRSA_OK;
 }
 
-int drsa_amd_heatmap_sort(const float* hm, int B, int K, int HW, float* std_out, float* std_rel, float* sub_out,
-                          float* rel, int64_t* mask, void* stream) {
+int drsa_amd_heatmap_sort(const float* hm, int B, int K, int HW, int std_from_sum, float* std_out, float* std_rel,
+                          float* sub_out, float* rel, int64_t* mask, void* stream) {
   DRSA_REQUIRE(K >= 1 && K <= 64, "heatmap_sort: K must be in [1, 64]");
   DRSA_REQUIRE(HW % 4 == 0, "heatmap_sort: H*W must be a multiple of 4");
   static const int no_cache = getenv("DRSA_AMD_SORT_GENERIC") ? atoi(getenv("DRSA_AMD_SORT_GENERIC")) : 0;
-  if (K == 4 && HW == 16384 && !no_cache)
-    hipLaunchKernelGGL((heatmap_sort_cached_kernel<4, 16>), dim3(B), dim3(256), 0, (hipStream_t)stream, hm, std_out,
-                       std_rel, sub_out, rel, mask);
-  else
-    hipLaunchKernelGGL(heatmap_sort_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, hm, K, HW, std_out, std_rel,
-                       sub_out, rel, mask);
+  if (K == 4 && HW == 16384 && !no_cache) {
+    auto kern = std_from_sum ? heatmap_sort_cached_kernel<4, 16, true> : heatmap_sort_cached_kernel<4, 16, false>;
+    hipLaunchKernelGGL(kern, dim3(B), dim3(256), 0, (hipStream_t)stream, hm, std_out, std_rel, sub_out, rel, mask);
+  } else {
+    hipLaunchKernelGGL(heatmap_sort_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, hm, K, HW, std_from_sum ? 1 : 0,
+                       std_out, std_rel, sub_out, rel, mask);
+  }
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;
 }

@@ -237,9 +237,11 @@ class HookedAutograd:
 
     @torch.no_grad()
     def subspace_heatmaps(self, x: torch.Tensor, class_idx=None, cls: Optional[torch.Tensor] = None,
-                          one_hot: bool = False) -> dict:
+                          one_hot: bool = False, standard: str = "clone") -> dict:
         """The reference's clone semantics literally (explainer.py:92-104): K+1 copies of every
-        sample through the hooked model, then split / sum / sort on the HIP kernel."""
+        sample through the hooked model, then split / sum / sort on the HIP kernel.  The standard
+        heatmap is always clone 0 here (``standard`` is accepted for the engine's signature: a
+        user hook need not be linear in the relevance, so the sum form is not used)."""
         K = next((r.num_concepts for r in self.rules.values() if _is_subspace_hook(r) or
                   hasattr(r, "num_concepts")), None)
         if K is None:
@@ -258,7 +260,7 @@ class HookedAutograd:
             "subspace_relevances": torch.empty(B, K, device=self.device),
             "mask": torch.empty(B, K, dtype=torch.int64, device=self.device),
         }
-        _capi.call("drsa_amd_heatmap_sort", hm.data_ptr(), B, K, H * W, out["standard_heatmaps"].data_ptr(),
+        _capi.call("drsa_amd_heatmap_sort", hm.data_ptr(), B, K, H * W, 0, out["standard_heatmaps"].data_ptr(),
                    out["standard_relevance"].data_ptr(), out["subspace_heatmaps"].data_ptr(),
                    out["subspace_relevances"].data_ptr(), out["mask"].data_ptr(), _capi.stream_ptr(self.device))
         return out

@@ -580,7 +580,7 @@ class LRPEngine:
 
     @torch.no_grad()
     def backward(self, seed: Optional[torch.Tensor] = None, cls: Optional[torch.Tensor] = None,
-                 one_hot: bool = False, fanout: bool = False, stop_after: Optional[int] = None) -> torch.Tensor:
+                 one_hot: bool = False, fanout: int = 0, stop_after: Optional[int] = None) -> torch.Tensor:
         """Relevance at the input.  ``seed`` [B, n_out] (output relevance) or ``cls`` [B] int32
         (lrp_output_modifier semantics).  ``fanout``: the projection stage emits K+1 clones per
         sample (HeatmapGenerator path); otherwise rows are treated as the reference's
@@ -634,8 +634,8 @@ class LRPEngine:
             if st.proj is not None:
                 P = st.proj
                 K = P.K if P.mask else P.K
-                fan = fanout and P.mask
-                nq = (K + 1) if fan else 1
+                fan = int(fanout) if P.mask else 0
+                nq = (K + 1) if fan == 1 else K if fan == 2 else 1
                 G = self._buf((li, "G"), (B * nq, st.cout, h, w))
                 post, den, eps = ((POST_DIV, rec["den"], st.eps) if st.den_kind not in (None, "ab")
                                   else (POST_MASK, None, 0.0))
@@ -645,7 +645,7 @@ class LRPEngine:
                            _capi.ptr(rec["ap"] if _PROJ_STORE else None), _capi.ptr(rec["h"]), rec["a"].data_ptr(),
                            _capi.ptr(den if post == POST_DIV else None), P.U.data_ptr(), P.P.data_ptr(), G.data_ptr(),
                            B, st.cout,
-                           h, w, K, P.eps_inv, eps, 1 if fan else 0, s)
+                           h, w, K, P.eps_inv, eps, fan, s)
                 g, clones, Bq = G, nq, B * nq
             elif st.pool and st.pool_k == (2, 2):
                 amax_in = rec["amax"]
@@ -731,9 +731,15 @@ class LRPEngine:
     # -------------------------------------------------------------- heatmaps
     @torch.no_grad()
     def subspace_heatmaps(self, x: torch.Tensor, class_idx=None, cls: Optional[torch.Tensor] = None,
-                          one_hot: bool = False) -> dict:
+                          one_hot: bool = False, standard: str = "sum") -> dict:
         """HeatmapGenerator.generate_subspace_heatmaps on device: one shared forward, the top
-        backward once, K+1 relevance clones below the projection, then split/sum/sort."""
+        backward once, relevance clones below the projection, then split/sum/sort.
+        ``standard="sum"``: K clones, the standard heatmap is the sum of the K concept heatmaps (every
+        rule is linear in the relevance, so this is clone 0 up to fp32 rounding; the bottom of the
+        network runs K instead of K+1 times).  ``"clone"``: K+1 clones, the standard heatmap is clone
+        0 as in the reference's replicated batch (explainer.py:92)."""
+        if standard not in ("sum", "clone"):
+            raise ValueError("standard must be 'sum' or 'clone'")
         proj = [st.proj for st in self.stages if st.proj is not None]
         if len(proj) != 1 or not proj[0].mask:
             raise EngineError("subspace heatmaps need exactly one projection group with a SubspaceHook")
@@ -742,7 +748,8 @@ class LRPEngine:
         B = x.size(0)
         if cls is None:
             cls = torch.full((B,), int(class_idx), dtype=torch.int32, device=self.device)
-        hm = self.backward(cls=cls, one_hot=one_hot, fanout=True)     # [B*(K+1), 1, H, W]
+        ssum = standard == "sum"
+        hm = self.backward(cls=cls, one_hot=one_hot, fanout=2 if ssum else 1)   # [B*(K or K+1), 1, H, W]
         H, W = hm.shape[-2:]
         HW = H * W
         out = {
@@ -752,9 +759,10 @@ class LRPEngine:
             "subspace_relevances": torch.empty(B, K, device=self.device),
             "mask": torch.empty(B, K, dtype=torch.int64, device=self.device),
         }
-        self._call("heatmap_sort", "drsa_amd_heatmap_sort", hm.data_ptr(), B, K, HW, out["standard_heatmaps"].data_ptr(),
-                   out["standard_relevance"].data_ptr(), out["subspace_heatmaps"].data_ptr(),
-                   out["subspace_relevances"].data_ptr(), out["mask"].data_ptr(), _capi.stream_ptr(self.device))
+        self._call("heatmap_sort", "drsa_amd_heatmap_sort", hm.data_ptr(), B, K, HW, 1 if ssum else 0,
+                   out["standard_heatmaps"].data_ptr(), out["standard_relevance"].data_ptr(),
+                   out["subspace_heatmaps"].data_ptr(), out["subspace_relevances"].data_ptr(), out["mask"].data_ptr(),
+                   _capi.stream_ptr(self.device))
         return out
 
 

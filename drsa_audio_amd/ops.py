@@ -20,7 +20,7 @@ kernel (a CPU tensor raises).
                            eps_post) -> out
   drsa_amd::projection_fwd(a, U, pool) -> (ap_or_pooled, amax)
   drsa_amd::projection_bwd(g, amax?, a, den?, U, K, eps_proj, eps_den, fanout) -> G
-  drsa_amd::heatmap_sort(hm, K) -> (std, std_rel, sub, rel, mask)   explainer.py:99-123, 151-176
+  drsa_amd::heatmap_sort(hm, K, std_from_sum) -> (std, std_rel, sub, rel, mask)   explainer.py:99-123, 151-176
   drsa_amd::logmel(wav, n_fft, hop, n_mels, width, peak_norm) -> mel  dataloading.py:138-176
 The LRP stage ops take the engine's prepared weight layouts (engine/plan.py); the DRSA and
 front-end ops take the reference's tensors directly.
@@ -236,24 +236,25 @@ def _(g, amax, a, den, U, K, eps_proj, eps_den, fanout):
 
 
 @torch.library.custom_op(f"{_NS}::heatmap_sort", mutates_args=())
-def heatmap_sort(hm: Tensor, K: int) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+def heatmap_sort(hm: Tensor, K: int, std_from_sum: bool = False) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
     _chk(hm, "hm")
     H, W = hm.shape[-2:]
-    B = hm.numel() // ((K + 1) * H * W)
+    B = hm.numel() // ((K if std_from_sum else K + 1) * H * W)
     std = hm.new_empty(B, 1, H, W)
     std_rel = hm.new_empty(B)
     sub = hm.new_empty(B, K, H, W)
     rel = hm.new_empty(B, K)
     mask = torch.empty(B, K, dtype=torch.int64, device=hm.device)
-    _capi.call("drsa_amd_heatmap_sort", hm.data_ptr(), B, K, H * W, std.data_ptr(), std_rel.data_ptr(), sub.data_ptr(),
+    _capi.call("drsa_amd_heatmap_sort", hm.data_ptr(), B, K, H * W, 1 if std_from_sum else 0, std.data_ptr(),
+               std_rel.data_ptr(), sub.data_ptr(),
                rel.data_ptr(), mask.data_ptr(), _s(hm))
     return std, std_rel, sub, rel, mask
 
 
 @heatmap_sort.register_fake
-def _(hm, K):
+def _(hm, K, std_from_sum=False):
     H, W = hm.shape[-2:]
-    B = hm.numel() // ((K + 1) * H * W)
+    B = hm.numel() // ((K if std_from_sum else K + 1) * H * W)
     return (hm.new_empty(B, 1, H, W), hm.new_empty(B), hm.new_empty(B, K, H, W), hm.new_empty(B, K),
             hm.new_empty(B, K, dtype=torch.int64))
 

@@ -31,10 +31,19 @@ from .attribute import SubspaceHook, compute_relevances, seed_class_indices
 class HeatmapGenerator:
     def __init__(self, model: nn.Module, U: torch.Tensor, name_map: List[Tuple[List[str], object]],
                  sample_class: str, num_concepts: int = 4, layer_idx: int = 10,
-                 device: str | torch.device = torch.device("cuda"), canonizers=None) -> None:
+                 device: str | torch.device = torch.device("cuda"), canonizers=None,
+                 standard: str = "sum") -> None:
         """``canonizers`` (extension, default None = the reference's composite) is passed to the
         class composite, e.g. ``[SequentialMergeBatchNorm()]`` for the VGGish-BN models of the
-        reference's DRSA scripts (getdrsadata.py:113), whose layer 19 has d = 100."""
+        reference's DRSA scripts (getdrsadata.py:113), whose layer 19 has d = 100.
+        ``standard`` (extension): "sum" (default) computes the standard heatmap as the sum of the K
+        concept heatmaps -- every LRP rule is linear in the relevance, so this is the reference's
+        clone 0 up to fp32 rounding (as close to float64 as clone 0, tests/test_lrp_gpu.py), and the
+        network below the projection runs K instead of K+1 times; "clone" propagates clone 0 as
+        the reference's replicated batch does (explainer.py:92)."""
+        if standard not in ("sum", "clone"):
+            raise ValueError("standard must be 'sum' or 'clone'")
+        self.standard = standard
         self.device = torch.device(device) if isinstance(device, str) else device
         self.num_concepts = int(num_concepts)
         case = "toy" if sample_class.endswith("1") or sample_class.endswith("2") else "gtzan"
@@ -57,7 +66,7 @@ class HeatmapGenerator:
         if to_host and B >= 2 * self.host_chunk_min:
             self._heatmaps_to_host_pipelined(eng, input_batch, x, cls, one_hot_encoded)
             return
-        out = eng.subspace_heatmaps(x, cls=cls, one_hot=one_hot_encoded)
+        out = eng.subspace_heatmaps(x, cls=cls, one_hot=one_hot_encoded, standard=self.standard)
         self.info_device = out
         if to_host:
             # the reference returns numpy (explainer.py:111): D2H into fresh pinned buffers (torch's
@@ -102,7 +111,7 @@ class HeatmapGenerator:
         half = (B + 1) // 2
         parts = []
         for s0, s1 in ((0, half), (half, B)):
-            out = eng.subspace_heatmaps(x[s0:s1], cls=cls[s0:s1], one_hot=one_hot)
+            out = eng.subspace_heatmaps(x[s0:s1], cls=cls[s0:s1], one_hot=one_hot, standard=self.standard)
             parts.append(out)
             side.wait_stream(main)
             with torch.cuda.stream(side):

@@ -176,8 +176,9 @@ int drsa_amd_projection_fwd(const float* a, const float* U, const float* P, floa
 
 /* Epsilon(invprojection) -> SubspaceHook mask -> Epsilon(projection) -> ReLU backward ->
  * division of the conv rule below (explainer.py:198-203, attribute.py:42-60).
- * fanout != 0: each sample yields K+1 clones (standard + K subspaces); fanout == 0: row b is
- * clone (b mod (K+1)) of a replicated batch (explainer.py:92 semantics).
+ * fanout == 1: each sample yields K+1 clones (standard + K subspaces); fanout == 2: the K subspace
+ * clones only (the standard heatmap is then their sum, drsa_amd_heatmap_sort std_from_sum);
+ * fanout == 0: row b is clone (b mod (K+1)) of a replicated batch (explainer.py:92 semantics).
  * ap or h NULL: h and a' are recomputed from a in the kernel (same MFMA order as
  * drsa_amd_projection_fwd, so the result is bit-identical to passing the stored buffers); P is
  * then required. */
@@ -204,9 +205,12 @@ int drsa_amd_first_layer_den(const float* w2, const float* b2, float* den, int C
 
 /* HeatmapGenerator post-processing (explainer.py:99-123, sort_subspaces 151-176): standard
  * heatmap + relevance, subspace heatmaps sorted by descending relevance, relevances, mask
- * (int64, numpy argsort(...)[..., ::-1] order). */
-int drsa_amd_heatmap_sort(const float* hm, int B, int K, int HW, float* std_out, float* std_rel, float* sub_out,
-                          float* rel, int64_t* mask, void* stream);
+ * (int64, numpy argsort(...)[..., ::-1] order; relevances are numpy's float32 sums).
+ * std_from_sum = 0: hm is [B][K+1][HW] with the standard heatmap first (clone 0);
+ * std_from_sum = 1: hm is [B][K][HW] (concept maps only) and the standard heatmap is their sum,
+ * k ascending (equal to clone 0 in exact arithmetic: every LRP rule is linear in the relevance). */
+int drsa_amd_heatmap_sort(const float* hm, int B, int K, int HW, int std_from_sum, float* std_out, float* std_rel,
+                          float* sub_out, float* rel, int64_t* mask, void* stream);
 
 /* One DRSA problem for drsa_amd_drsa_run_multi (all pointers device memory; the fields mean what
  * the same-named arguments of drsa_amd_drsa_run mean). */

@@ -679,9 +679,15 @@ def sort_subspaces(sub: np.ndarray, ops=TorchOps):
 @torch.no_grad()
 def subspace_heatmaps(proj_model: nn.Module, name_map: Dict[str, RuleSpec], K: int,
                       x: torch.Tensor, class_idx: int, one_hot_encoded=False,
-                      mode: str = "analytic", forced_inputs=None) -> Dict[str, np.ndarray]:
+                      mode: str = "analytic", forced_inputs=None, standard: Optional[str] = None) -> Dict[str, np.ndarray]:
     """HeatmapGenerator.generate_subspace_heatmaps (explainer.py:87-123) on the CPU.
-    ``forced_inputs``: per-sample layer inputs (see ``lrp``), replicated like the batch."""
+    ``forced_inputs``: per-sample layer inputs (see ``lrp``), replicated like the batch.
+    ``standard``: "clone" = clone 0 of the replicated batch (the reference); "sum" = the K concept
+    heatmaps summed, k ascending, in the heatmaps' precision (the product's HeatmapGenerator
+    default; equal in exact arithmetic since every rule is linear in the relevance).  Default:
+    "sum" for the product-order modes ("exact", "bf16"), "clone" otherwise."""
+    if standard is None:
+        standard = "sum" if mode in ("exact", "bf16") else "clone"
     rules = class_composite_rules(name_map, K)
     xr = x.repeat_interleave(K + 1, dim=0)
     if forced_inputs is not None:
@@ -691,6 +697,13 @@ def subspace_heatmaps(proj_model: nn.Module, name_map: Dict[str, RuleSpec], K: i
     H, W = R.shape[-2:]
     hm = R.reshape(-1, K + 1, H, W).numpy()
     std, sub = hm[:, 0:1], hm[:, 1:]
+    if standard == "sum":
+        acc = sub[:, 0:1].copy()
+        for k in range(1, K):
+            acc = acc + sub[:, k:k + 1]
+        std = acc
+    elif standard != "clone":
+        raise ValueError(standard)
     ops = OPS[mode]
     sub_s, rel_s, mask = sort_subspaces(sub, ops)
     return {

@@ -108,15 +108,17 @@ def test_heatmap_generator_f64_anchored(net):
         assert np.median(e) <= 1e-3 * np.median(eref) + 1e-4       # the dead-channel noise is gone
 
 
-@pytest.mark.parametrize("layer_idx", [7, 10])
-def test_heatmap_generator_bit_exact(net, layer_idx):
+@pytest.mark.parametrize("layer_idx,standard", [(7, "sum"), (10, "sum"), (7, "clone")])
+def test_heatmap_generator_bit_exact(net, layer_idx, standard):
+    """Both standard-heatmap modes: "sum" (K clones, standard = sum of the concept heatmaps, the
+    default) and "clone" (K+1 clones, clone 0 as the reference's replicated batch)."""
     d = 64
     U = u64() if layer_idx == 7 else ortho(d, 3)
     x = logmel(2, seed=5 + layer_idx)
     pm = ProjectionModel(net, layer_idx, U, 4).eval()
-    ref = lrp_ref.subspace_heatmaps(pm, spec(LRP_NAME_MAP_GTZAN), 4, x, class_idx=4, mode="exact")
+    ref = lrp_ref.subspace_heatmaps(pm, spec(LRP_NAME_MAP_GTZAN), 4, x, class_idx=4, mode="exact", standard=standard)
     hg = HeatmapGenerator(_gpu_model(net), U, LRP_NAME_MAP_GTZAN, "reggae", num_concepts=4,
-                          layer_idx=layer_idx, device="cuda")
+                          layer_idx=layer_idx, device="cuda", standard=standard)
     hg.generate_subspace_heatmaps(x)
     for k in ("standard_heatmaps", "standard_relevance", "subspace_heatmaps", "subspace_relevances", "mask"):
         assert np.array_equal(hg.info[k], ref[k]), k
@@ -153,7 +155,7 @@ def test_replicated_batch_matches_fanout(net):
     fan-out path bit for bit."""
     x = logmel(2, seed=13)
     m = _gpu_model(net)
-    hg = HeatmapGenerator(m, u64(), LRP_NAME_MAP_GTZAN, "metal", num_concepts=4, layer_idx=7)
+    hg = HeatmapGenerator(m, u64(), LRP_NAME_MAP_GTZAN, "metal", num_concepts=4, layer_idx=7, standard="clone")
     hg.generate_subspace_heatmaps(x)
     rep = hg.obtain_heatmaps(x.to(DEV).repeat_interleave(5, 0)).reshape(2, 5, 128, 128).cpu().numpy()
     assert np.array_equal(rep[:, 0:1], hg.info["standard_heatmaps"])

@@ -68,8 +68,8 @@ def test_lrp_stage_ops_equal_engine_buffers(ops):
     st2, rec2 = eng.stages[2], eng.last["stages"][2]
     yp, ap = ops.projection_fwd(rec2["a"], st2.proj.U, True)
     assert torch.equal(yp, rec2["y"]) and torch.equal(ap, rec2["amax"])
-    hm = eng.backward(cls=torch.full((3,), hg.class_idx, dtype=torch.int32, device=DEV), fanout=True)
-    std, std_rel, sub, rel, mask = ops.heatmap_sort(hm, 4)
+    hm = eng.backward(cls=torch.full((3,), hg.class_idx, dtype=torch.int32, device=DEV), fanout=2)
+    std, std_rel, sub, rel, mask = ops.heatmap_sort(hm, 4, True)
     for k, v in (("standard_heatmaps", std), ("standard_relevance", std_rel), ("subspace_heatmaps", sub),
                  ("subspace_relevances", rel), ("mask", mask)):
         assert torch.equal(v, hg.info_device[k]), k
