@@ -33,6 +33,7 @@ SIGNATURES = {
     "drsa_amd_drsa_objective": (_i32, [_fp, _fp, _i64, _i32, _i32, _fp, _fp, _vp, _sz, _vp]),
     "drsa_amd_drsa_run": (_i32, [_fp, _fp, _i64, _i32, _i32, _fp, _fp, _i32, _fp, _ip, _vp, _sz, _i32, _vp]),
     "drsa_amd_drsa_run_multi": (_i32, [_i32, _vp, _i32, _i32, _vp]),
+    "drsa_amd_drsa_run_batched": (_i32, [_i32, _vp, _i32, _i32, _i32, _vp]),
     "drsa_amd_drsa_partial_bf16": (_i32, [_vp, _vp, _i64, _i32, _i32, _fp, _fp, _vp, _sz, _vp]),
     "drsa_amd_drsa_partial_f16": (_i32, [_vp, _vp, _i64, _i32, _i32, _fp, _fp, _vp, _sz, _vp]),
     "drsa_amd_polar": (_i32, [_fp, _i32, _fp, _ip, _vp]),

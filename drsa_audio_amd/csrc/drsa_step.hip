@@ -527,10 +527,11 @@ __device__ __forceinline__ double finish_prologue(const float* __restrict__ gs, 
 
 // mode 0: full step (f, U_out = polar(U + G)); mode 1: objective only
 template <int DP>
-__global__ __launch_bounds__(fin_threads<polar_dim<DP>()>()) void drsa_finish_kernel(
-    const float* __restrict__ gs, double n_total, int d, int K, int DKP, const float* __restrict__ U,
-    float* __restrict__ U_out, float* __restrict__ f_out, int* __restrict__ step_counter, int f_stride_by_counter,
-    int mode, float tol, int max_iter, int* __restrict__ iters_out) {
+__device__ __forceinline__ void finish_body(const float* __restrict__ gs, double n_total, int d, int K, int DKP,
+                                            const float* __restrict__ U, float* __restrict__ U_out,
+                                            float* __restrict__ f_out, int* __restrict__ step_counter,
+                                            int f_stride_by_counter, int mode, float tol, int max_iter,
+                                            int* __restrict__ iters_out) {
   constexpr int PD = polar_dim<DP>(), NT = fin_threads<PD>(), LD = ns_ld<PD>();
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* X = smem;
@@ -555,6 +556,73 @@ __global__ __launch_bounds__(fin_threads<polar_dim<DP>()>()) void drsa_finish_ke
     if (iters_out) *iters_out = it;
     if (f_stride_by_counter) *step_counter = slot + 1;
   }
+}
+
+template <int DP>
+__global__ __launch_bounds__(fin_threads<polar_dim<DP>()>()) void drsa_finish_kernel(
+    const float* __restrict__ gs, double n_total, int d, int K, int DKP, const float* __restrict__ U,
+    float* __restrict__ U_out, float* __restrict__ f_out, int* __restrict__ step_counter, int f_stride_by_counter,
+    int mode, float tol, int max_iter, int* __restrict__ iters_out) {
+  finish_body<DP>(gs, n_total, d, K, DKP, U, U_out, f_out, step_counter, f_stride_by_counter, mode, tol, max_iter,
+                  iters_out);
+}
+
+// ---------------------------------------------------------------------------
+// batched independent problems (task-parallel DRSA grid, optsubspaces.py:17-23): one launch per
+// phase for every problem of a batch that shares the padded geometry.  Problem p's partial runs
+// on G workgroups (blockIdx.y = p, each a contiguous run of its row blocks), its reduce on
+// blockIdx.y = p, its finish on workgroup p.  U ping-pongs between U_io and U_tmp by step parity.
+// ---------------------------------------------------------------------------
+struct BatchDesc {
+  const float* A;
+  const float* C;
+  int64_t N;
+  int64_t rb_total;
+  int d, K, dk, DKP;
+  float* U_io;
+  float* U_tmp;
+  float* f_traj;
+  int* counter;
+  float* partials;
+  float* gs;
+};
+
+template <int DP, int DKP, bool VEC>
+__global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_batched_kernel(
+    const BatchDesc* __restrict__ bd, int parity) {
+  const BatchDesc& q = bd[blockIdx.y];
+  const float* U = parity ? q.U_tmp : q.U_io;
+  const int d = q.d;
+  partial_core<DP, DKP, 0, VEC>(
+      q.A, q.C, q.N, d, q.K, q.dk, q.partials, q.rb_total, [] {},
+      [&](int k, int j, int) { return U[(size_t)k * d + j]; }, [] {});
+}
+
+__global__ __launch_bounds__(256) void drsa_reduce_batched_kernel(const BatchDesc* __restrict__ bd, int G, int E,
+                                                                  int ES) {
+  __shared__ float part[4][64];
+  const BatchDesc& q = bd[blockIdx.y];
+  const int l = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + l;
+  float acc = 0.f;
+  if (e < E) {
+#pragma unroll 8
+    for (int p = grp; p < G; p += 4) acc += q.partials[(size_t)p * ES + e];
+  }
+  part[grp][l] = acc;
+  __syncthreads();
+  if (grp == 0 && e < E) q.gs[e] = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
+}
+
+// mode 0: U_in -> U_out = polar(U_in + G c), f(U_in) -> f_traj[counter++]; mode 1: f only
+template <int DP>
+__global__ __launch_bounds__(fin_threads<polar_dim<DP>()>()) void drsa_finish_batched_kernel(
+    const BatchDesc* __restrict__ bd, int parity, int mode, float tol, int max_iter) {
+  const BatchDesc& q = bd[blockIdx.x];
+  const float* U = parity ? q.U_tmp : q.U_io;
+  float* U_out = parity ? q.U_io : q.U_tmp;
+  finish_body<DP>(q.gs, (double)q.N, q.d, q.K, q.DKP, U, U_out, q.f_traj, q.counter, 1, mode, tol, max_iter,
+                  nullptr);
 }
 
 // One fused DRSA step for DP = 64 (C3, C4): every workgroup first finishes the PREVIOUS step
@@ -1089,6 +1157,162 @@ int drsa_amd_drsa_run_multi(int P, const drsa_amd_problem_t* probs, int steps, i
   for (int p = 0; p < P; ++p) (void)hipStreamSynchronize(side[p]);
   cleanup();
   return DRSA_OK;
+}
+
+// P independent fp32 problems of one padded geometry advanced together, one launch per phase
+// (partial / reduce / finish) for all of them -- the task-parallel DRSA grid of optsubspaces.py:17-23.
+// blocks: workgroups per problem for the partial (0: about 4 waves of workgroups over the chip).
+// Row partition, and so the fp32 summation order, depends on blocks: deterministic for a given
+// value.  Graph-captured two steps at a time like drsa_amd_drsa_run.
+int drsa_amd_drsa_run_batched(int P, const drsa_amd_problem_t* probs, int steps, int blocks, int use_graph,
+                              void* stream) {
+  DRSA_REQUIRE(P >= 1 && probs, "drsa_run_batched: P must be >= 1");
+  DRSA_REQUIRE(steps >= 0, "drsa_run_batched: steps < 0");
+  const Geom g0 = geom(probs[0].d, probs[0].K);
+  DRSA_REQUIRE(g0.ok, "drsa_run_batched: problem 0 unsupported d=%d K=%d", probs[0].d, probs[0].K);
+  bool vec = true;
+  int64_t min_rbt = INT64_MAX;
+  for (int p = 0; p < P; ++p) {
+    const drsa_amd_problem_t& q = probs[p];
+    const Geom g = geom(q.d, q.K);
+    DRSA_REQUIRE(g.ok && g.DP == g0.DP && g.DKp == g0.DKp,
+                 "drsa_run_batched: problem %d (d=%d K=%d) does not share the padded geometry of problem 0", p,
+                 q.d, q.K);
+    DRSA_REQUIRE(q.dtype == 0, "drsa_run_batched: fp32 problems only (problem %d)", p);
+    DRSA_REQUIRE(q.N > 0 && q.A && q.C && q.U_io && q.U_tmp && q.f_traj && q.counter && q.ws,
+                 "drsa_run_batched: problem %d has null pointers or N <= 0", p);
+    DRSA_REQUIRE(q.ws_size >= ws_bytes(q.N, g), "drsa_run_batched: problem %d workspace too small", p);
+    DRSA_REQUIRE(((uintptr_t)q.A % 16) == 0 && ((uintptr_t)q.C % 16) == 0, "drsa_run_batched: A/C 16B alignment");
+    vec = vec && (q.d & 3) == 0;
+    const int64_t rbt = (q.N + 15) / 16;
+    if (rbt < min_rbt) min_rbt = rbt;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    DRSA_REQUIRE(!(hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone),
+                 "drsa_run_batched: not capturable (allocates its descriptor table); use drsa_run_multi");
+  }
+  const int cu = drsa::cu_count();
+  int G = blocks > 0 ? blocks : (4 * cu + P - 1) / P;
+  if (G > cu) G = cu;                         // the workspace holds cu_count slabs per problem
+  if (G > min_rbt) G = (int)min_rbt;
+  if (G < 1) G = 1;
+  const Geom& g = g0;
+  const size_t E = slab_floats(g), ES = slab_stride(g);
+  // descriptor table on the device
+  BatchDesc* hd = (BatchDesc*)malloc(sizeof(BatchDesc) * (size_t)P);
+  DRSA_REQUIRE(hd, "drsa_run_batched: host allocation failed");
+  for (int p = 0; p < P; ++p) {
+    const drsa_amd_problem_t& q = probs[p];
+    const Geom gq = geom(q.d, q.K);
+    hd[p] = BatchDesc{q.A, q.C, q.N, (q.N + 15) / 16, q.d, q.K, q.d / q.K, gq.DKp, q.U_io, q.U_tmp, q.f_traj,
+                      q.counter, (float*)q.ws, ws_gs(q.ws, q.N, gq)};
+  }
+  BatchDesc* dd = nullptr;
+  hipError_t e = hipMalloc((void**)&dd, sizeof(BatchDesc) * (size_t)P);
+  if (e != hipSuccess) { free(hd); DRSA_HIP(e); }
+  int rc = DRSA_OK;
+  auto ok = [&](hipError_t err, const char* what) -> bool {
+    if (err == hipSuccess) return true;
+    drsa::set_error("drsa_run_batched: %s: %s", what, hipGetErrorString(err));
+    rc = (int)err;
+    return false;
+  };
+  if (!ok(hipMemcpyAsync(dd, hd, sizeof(BatchDesc) * (size_t)P, hipMemcpyHostToDevice, s), "copy")) goto done;
+  for (int p = 0; p < P && !rc; ++p) ok(hipMemsetAsync(probs[p].counter, 0, sizeof(int), s), "memset");
+  if (rc) goto done;
+  {
+    // launchers for the geometry
+    auto launch_phase = [&](int parity, int final_obj) -> int {
+      auto part = [&](auto dpt, auto dkt) -> int {
+        constexpr int DP = decltype(dpt)::value, DKP = decltype(dkt)::value;
+        using Cfg = PCfg<DP, DKP>;
+        auto kern = vec ? drsa_partial_batched_kernel<DP, DKP, true> : drsa_partial_batched_kernel<DP, DKP, false>;
+        DRSA_SMEM(kern, Cfg::lds_bytes);
+        hipLaunchKernelGGL(kern, dim3(G, P), dim3(Cfg::NT), Cfg::lds_bytes, s, dd, parity);
+        DRSA_LAUNCH_CHECK();
+        return DRSA_OK;
+      };
+      int r = DRSA_EUNSUPPORTED;
+      using I = std::integral_constant<int, 1>;
+      (void)sizeof(I);
+#define PB_DK(DPV)                                                                                            \
+  switch (g.DKp) {                                                                                            \
+    case 1: r = part(std::integral_constant<int, DPV>{}, std::integral_constant<int, 1>{}); break;            \
+    case 2: r = part(std::integral_constant<int, DPV>{}, std::integral_constant<int, 2>{}); break;            \
+    case 4: r = part(std::integral_constant<int, DPV>{}, std::integral_constant<int, 4>{}); break;            \
+    case 8: r = part(std::integral_constant<int, DPV>{}, std::integral_constant<int, 8>{}); break;            \
+    case 16: r = part(std::integral_constant<int, DPV>{}, std::integral_constant<int, 16>{}); break;          \
+    case 32: if constexpr (DPV >= 32) r = part(std::integral_constant<int, DPV>{}, std::integral_constant<int, (DPV >= 32 ? 32 : 1)>{}); break; \
+    case 64: if constexpr (DPV >= 64) r = part(std::integral_constant<int, DPV>{}, std::integral_constant<int, (DPV >= 64 ? 64 : 1)>{}); break; \
+    default: break;                                                                                           \
+  }
+      switch (g.DP) {
+        case 16: PB_DK(16) break;
+        case 32: PB_DK(32) break;
+        case 64: PB_DK(64) break;
+        case 128: PB_DK(128) break;
+      }
+#undef PB_DK
+      if (r) return r;
+      hipLaunchKernelGGL(drsa_reduce_batched_kernel, dim3((unsigned)((E + 63) / 64), P), dim3(256), 0, s, dd, G,
+                         (int)E, (int)ES);
+      DRSA_LAUNCH_CHECK();
+      auto fin = [&](auto dpt) -> int {
+        constexpr int DP = decltype(dpt)::value;
+        const size_t lds = finish_lds<DP>();
+        DRSA_SMEM(drsa_finish_batched_kernel<DP>, lds);
+        hipLaunchKernelGGL(drsa_finish_batched_kernel<DP>, dim3(P), dim3(fin_threads<polar_dim<DP>()>()), lds, s, dd,
+                           parity, final_obj ? 1 : 0, kPolarTol, kPolarMaxIter);
+        DRSA_LAUNCH_CHECK();
+        return DRSA_OK;
+      };
+      switch (g.DP) {
+        case 16: return fin(std::integral_constant<int, 16>{});
+        case 32: return fin(std::integral_constant<int, 32>{});
+        case 64: return fin(std::integral_constant<int, 64>{});
+        default: return fin(std::integral_constant<int, 128>{});
+      }
+    };
+    int done_steps = 0;
+    if (use_graph && steps >= 2 && s) {
+      hipGraph_t graph = nullptr;
+      hipGraphExec_t exec = nullptr;
+      if (!ok(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal), "capture")) goto done;
+      int r1 = launch_phase(0, 0);
+      int r2 = r1 ? r1 : launch_phase(1, 0);
+      hipError_t ce = hipStreamEndCapture(s, &graph);
+      if (r2) { if (graph) (void)hipGraphDestroy(graph); rc = r2; goto done; }
+      if (!ok(ce, "end capture") || !ok(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0), "instantiate")) {
+        if (graph) (void)hipGraphDestroy(graph);
+        goto done;
+      }
+      for (; done_steps + 2 <= steps; done_steps += 2)
+        if (!ok(hipGraphLaunch(exec, s), "graph launch")) break;
+      (void)hipGraphExecDestroy(exec);
+      (void)hipGraphDestroy(graph);
+      if (rc) goto done;
+    }
+    for (; done_steps < steps; ++done_steps) {
+      int r = launch_phase(done_steps & 1, 0);
+      if (r) { rc = r; goto done; }
+    }
+    if (steps & 1) {   // U_S sits in U_tmp: bring it home
+      for (int p = 0; p < P; ++p)
+        if (!ok(hipMemcpyAsync(probs[p].U_io, probs[p].U_tmp, (size_t)probs[p].d * probs[p].d * sizeof(float),
+                               hipMemcpyDeviceToDevice, s), "copy")) goto done;
+    }
+    {
+      int r = launch_phase(0, 1);   // final objective at U_S -> f_traj[steps]
+      if (r) { rc = r; goto done; }
+    }
+  }
+done:
+  (void)hipStreamSynchronize(s);
+  (void)hipFree(dd);
+  free(hd);
+  return rc;
 }
 
 int drsa_amd_polar(const float* V, int d, float* U_out, int* iters_out, void* stream) {

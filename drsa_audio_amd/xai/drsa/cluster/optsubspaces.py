@@ -77,13 +77,20 @@ def assign(tasks: Sequence[Task], world: int) -> List[List[Task]]:
 
 
 def hip_runner(problems, steps: int):
-    """Product runner: every problem of the chunk in one hipGraph (drsa_run_joint)."""
-    from ..drsa import drsa_run_joint
+    """Product runner.  Problems sharing one padded geometry run batched -- one launch per phase
+    for all of them (drsa_run_batched); mixed geometries or 16-bit inputs advance together in one
+    hipGraph of per-problem chains (drsa_run_joint)."""
+    from ..drsa import batched_geometry, drsa_run_batched, drsa_run_joint
     dev = problems[0][0].device
     side = torch.cuda.Stream(dev)             # graph capture needs a non-default stream
     side.wait_stream(torch.cuda.current_stream(dev))
+    geoms = {batched_geometry(A.size(1), K) for A, _, _, K in problems}
+    fp32 = all(A.dtype == torch.float32 for A, _, _, _ in problems)
     with torch.cuda.stream(side):
-        out = drsa_run_joint(problems, steps)
+        if len(geoms) == 1 and fp32:
+            out = drsa_run_batched(problems, steps)
+        else:
+            out = drsa_run_joint(problems, steps)
     torch.cuda.current_stream(dev).wait_stream(side)
     return out
 
@@ -99,7 +106,7 @@ def _write_run(path: str, U: np.ndarray, traj: np.ndarray) -> None:
 
 def optimize_grid(datasets: Dict[Tuple[str, int], Tuple[torch.Tensor, torch.Tensor]], model_root: Optional[str],
                   num_concepts: int = 4, steps: int = 5000, runs: int = 3, seed: int = 42, device=None,
-                  group=None, runner: Optional[Callable] = None, max_joint: int = 48,
+                  group=None, runner: Optional[Callable] = None, max_joint: int = 128,
                   dtype: torch.dtype = torch.float32) -> Dict[Tuple[str, int, int], Dict]:
     """Optimise every (class, layer, run) DRSA problem of ``datasets`` over the process group.
 
@@ -122,8 +129,13 @@ def optimize_grid(datasets: Dict[Tuple[str, int], Tuple[torch.Tensor, torch.Tens
     U0s = {k: by_d[d] for k, (N, d) in shapes.items()}
     local: Dict[Tuple[str, int, int], Dict] = {}
     dev_data: Dict[Tuple[str, int], Tuple[torch.Tensor, torch.Tensor]] = {}
-    for i in range(0, len(mine), max(1, max_joint)):
-        chunk = mine[i:i + max_joint]
+    # tasks of one padded geometry run batched (one launch per phase for all of them): group first
+    from ..drsa import batched_geometry
+    by_geom: Dict[Tuple[int, int], List[Task]] = {}
+    for t in mine:
+        by_geom.setdefault(batched_geometry(t.d, num_concepts), []).append(t)
+    chunks = [grp[i:i + max(1, max_joint)] for grp in by_geom.values() for i in range(0, len(grp), max(1, max_joint))]
+    for chunk in chunks:
         probs = []
         for t in chunk:
             k = (t.sample_class, t.layer_idx)

@@ -27,7 +27,7 @@ import torch
 from ... import _capi
 
 __all__ = ["SubspaceOptimizer", "generalized_fmean", "project_grad", "orthogonalize",
-           "objective_fn", "main", "DrsaWorkspace", "slab_floats"]
+           "objective_fn", "main", "DrsaWorkspace", "slab_floats", "drsa_run_batched"]
 
 
 def _dev(device) -> torch.device:
@@ -160,6 +160,46 @@ def drsa_run_joint(problems, steps: int, use_graph: bool = True):
     graph = bool(use_graph) and stream.cuda_stream != 0
     _capi.call("drsa_amd_drsa_run_multi", len(structs), ctypes.addressof(arr), int(steps), 1 if graph else 0,
                stream.cuda_stream)
+    return outs
+
+
+def batched_geometry(d: int, K: int):
+    """(padded d, padded concept width) of a problem: problems sharing it can run batched."""
+    dk = d // K
+    dkp = 1 << max(0, (dk - 1).bit_length())
+    need = max(16, K * dkp)
+    return 1 << (need - 1).bit_length(), dkp
+
+
+def drsa_run_batched(problems, steps: int, blocks: int = 0, use_graph: bool = True):
+    """Many independent fp32 DRSA problems of one padded geometry (e.g. the reference's task grid:
+    GTZAN classes x layers 19 / 26 / 33 x runs, d = 100 / 128 -> padded 128, concept width 32)
+    advanced with one launch per phase for all of them (drsa_amd_drsa_run_batched).  ``blocks``:
+    partial workgroups per problem (0 = automatic); the row partition sets the fp32 summation
+    order.  Returns [(U_S, trajectory [S+1])]."""
+    import ctypes
+    if not problems:
+        return []
+    dev = problems[0][0].device
+    keep, structs, outs = [], [], []
+    for A, C, U0, K in problems:
+        _check_problem(A, C, U0, K)
+        if A.dtype != torch.float32:
+            raise ValueError("drsa_run_batched: fp32 problems only (use drsa_run_joint for bf16 / fp16)")
+        N, d = A.shape
+        ws = DrsaWorkspace(N, d, K, dev)
+        U = U0.detach().clone().contiguous()
+        U_tmp = torch.empty_like(U)
+        traj = torch.empty(steps + 1, dtype=torch.float32, device=dev)
+        keep += [ws, U_tmp, A, C]
+        outs.append((U, traj))
+        structs.append(_capi.DrsaProblem(A.data_ptr(), C.data_ptr(), N, d, int(K), U.data_ptr(), U_tmp.data_ptr(),
+                                         traj.data_ptr(), ws.counter.data_ptr(), ws.ptr, ws.nbytes, 0))
+    arr = (_capi.DrsaProblem * len(structs))(*structs)
+    stream = torch.cuda.current_stream(dev)
+    graph = bool(use_graph) and stream.cuda_stream != 0
+    _capi.call("drsa_amd_drsa_run_batched", len(structs), ctypes.addressof(arr), int(steps), int(blocks),
+               1 if graph else 0, stream.cuda_stream)
     return outs
 
 
