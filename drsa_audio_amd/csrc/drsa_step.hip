@@ -152,7 +152,7 @@ constexpr int partial_threads() { return PCfg<DP, DKP>::NT; }
 template <int DP, int DKP, int DT, bool VEC, class Pre, class UVal, class Mid>
 __device__ __forceinline__ void partial_core(const void* __restrict__ A_, const void* __restrict__ C_, int64_t N,
                                              int d, int K, int dk, float* __restrict__ partials, int64_t rb_total,
-                                             Pre pre, UVal uval, Mid mid) {
+                                             Pre pre, UVal uval, Mid mid, int nblk) {
   using Cfg = PCfg<DP, DKP>;
   constexpr bool BF = DT != 0;   // 16-bit A/C (bf16 or fp16)
   constexpr int CW = Cfg::CW, CG = Cfg::CG, NCB = Cfg::NCB, NIB = Cfg::NIB, NW = Cfg::NW, NT = Cfg::NT;
@@ -169,8 +169,8 @@ __device__ __forceinline__ void partial_core(const void* __restrict__ A_, const 
   const uint16_t* Ab = reinterpret_cast<const uint16_t*>(A_);
   const uint16_t* Cb = reinterpret_cast<const uint16_t*>(C_);
 
-  const int64_t rb0 = (int64_t)blockIdx.x * rb_total / gridDim.x;
-  const int64_t rb1 = (int64_t)(blockIdx.x + 1) * rb_total / gridDim.x;
+  const int64_t rb0 = (int64_t)blockIdx.x * rb_total / nblk;       // nblk workgroups share the rows
+  const int64_t rb1 = (int64_t)(blockIdx.x + 1) * rb_total / nblk;
   const int ntile = (int)((rb1 - rb0 + RT / 16 - 1) / (RT / 16));
 
   // ---- tile staging: global -> registers (prefetch) -> LDS; rows >= N and columns >= d are 0 ----
@@ -449,7 +449,7 @@ __global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_ker
     const float* __restrict__ U, float* __restrict__ partials, int64_t rb_total) {
   partial_core<DP, DKP, DT, VEC>(
       A_, C_, N, d, K, dk, partials, rb_total, [] {},
-      [&](int k, int j, int) { return U[(size_t)k * d + j]; }, [] {});
+      [&](int k, int j, int) { return U[(size_t)k * d + j]; }, [] {}, (int)gridDim.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -579,6 +579,7 @@ struct BatchDesc {
   int64_t N;
   int64_t rb_total;
   int d, K, dk, DKP;
+  int G;                // partial workgroups of this problem (<= gridDim.x)
   float* U_io;
   float* U_tmp;
   float* f_traj;
@@ -591,17 +592,18 @@ template <int DP, int DKP, bool VEC>
 __global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_batched_kernel(
     const BatchDesc* __restrict__ bd, int parity) {
   const BatchDesc& q = bd[blockIdx.y];
+  if ((int)blockIdx.x >= q.G) return;    // uniform per workgroup: before any barrier
   const float* U = parity ? q.U_tmp : q.U_io;
   const int d = q.d;
   partial_core<DP, DKP, 0, VEC>(
       q.A, q.C, q.N, d, q.K, q.dk, q.partials, q.rb_total, [] {},
-      [&](int k, int j, int) { return U[(size_t)k * d + j]; }, [] {});
+      [&](int k, int j, int) { return U[(size_t)k * d + j]; }, [] {}, q.G);
 }
 
-__global__ __launch_bounds__(256) void drsa_reduce_batched_kernel(const BatchDesc* __restrict__ bd, int G, int E,
-                                                                  int ES) {
+__global__ __launch_bounds__(256) void drsa_reduce_batched_kernel(const BatchDesc* __restrict__ bd, int E, int ES) {
   __shared__ float part[4][64];
   const BatchDesc& q = bd[blockIdx.y];
+  const int G = q.G;
   const int l = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + l;
   float acc = 0.f;
@@ -664,7 +666,7 @@ __global__ __launch_bounds__(fin_threads<polar_dim<DP>()>()) void drsa_fused_ste
   };
   partial_core<DP, DKP, 0, VEC>(
       A, C, N, d, K, dk, partials, rb_total, pre, [&](int k, int, int jp) { return X[k * LD + jp]; },
-      [] { __syncthreads(); });   // every wave has read U from X before the tile store overwrites it
+      [] { __syncthreads(); }, (int)gridDim.x);   // mid: every wave has read U from X before the tile store overwrites it
 }
 
 template <int DP, int DKP>
@@ -1196,8 +1198,8 @@ int drsa_amd_drsa_run_batched(int P, const drsa_amd_problem_t* probs, int steps,
   const int cu = drsa::cu_count();
   int G = blocks > 0 ? blocks : (4 * cu + P - 1) / P;
   if (G > cu) G = cu;                         // the workspace holds cu_count slabs per problem
-  if (G > min_rbt) G = (int)min_rbt;
   if (G < 1) G = 1;
+  (void)min_rbt;
   const Geom& g = g0;
   const size_t E = slab_floats(g), ES = slab_stride(g);
   // descriptor table on the device
@@ -1206,8 +1208,10 @@ int drsa_amd_drsa_run_batched(int P, const drsa_amd_problem_t* probs, int steps,
   for (int p = 0; p < P; ++p) {
     const drsa_amd_problem_t& q = probs[p];
     const Geom gq = geom(q.d, q.K);
-    hd[p] = BatchDesc{q.A, q.C, q.N, (q.N + 15) / 16, q.d, q.K, q.d / q.K, gq.DKp, q.U_io, q.U_tmp, q.f_traj,
-                      q.counter, (float*)q.ws, ws_gs(q.ws, q.N, gq)};
+    const int64_t rbt = (q.N + 15) / 16;
+    const int Gp = (int)(G < rbt ? G : rbt);   // as plan_partial: never more workgroups than row blocks
+    hd[p] = BatchDesc{q.A, q.C, q.N, rbt, q.d, q.K, q.d / q.K, gq.DKp, Gp, q.U_io, q.U_tmp, q.f_traj, q.counter,
+                      (float*)q.ws, ws_gs(q.ws, q.N, gq)};
   }
   BatchDesc* dd = nullptr;
   hipError_t e = hipMalloc((void**)&dd, sizeof(BatchDesc) * (size_t)P);
@@ -1256,7 +1260,7 @@ int drsa_amd_drsa_run_batched(int P, const drsa_amd_problem_t* probs, int steps,
       }
 #undef PB_DK
       if (r) return r;
-      hipLaunchKernelGGL(drsa_reduce_batched_kernel, dim3((unsigned)((E + 63) / 64), P), dim3(256), 0, s, dd, G,
+      hipLaunchKernelGGL(drsa_reduce_batched_kernel, dim3((unsigned)((E + 63) / 64), P), dim3(256), 0, s, dd,
                          (int)E, (int)ES);
       DRSA_LAUNCH_CHECK();
       auto fin = [&](auto dpt) -> int {
