@@ -417,7 +417,8 @@ def drsa_grid_bench(device, world, rank, steps=100, N=20000, classes=None):
     """Task-parallel DRSA over the reference's problem grid (optsubspaces.py:17-23): 10 classes x
     layers [19 (d=100), 26 (d=128), 33 (d=128)] x 3 runs = 90 independent problems, K=4, N rows
     each (synthetic normalised A=|N(0,1)|, C~N(0,1)); LPT-assigned over the ranks, each rank's
-    problems advanced together in hipGraphs (drsa_run_multi).  Strong scaling: the grid is fixed.
+    problems batched (drsa_run_batched: one partial / reduce / finish launch per step for all of
+    them, graph-replayed).  Strong scaling: the grid is fixed.
     The reference runs 5000 steps per problem; this leg times `steps` and projects."""
     import torch.distributed as dist
     from drsa_audio_amd.xai.drsa.cluster.optsubspaces import GTZAN_CLASSES, GTZAN_LAYERS, optimize_grid
@@ -454,7 +455,7 @@ def drsa_grid_bench(device, world, rank, steps=100, N=20000, classes=None):
         per_rank[v["rank"]] = per_rank.get(v["rank"], 0) + 1
     return {"config": f"task-parallel DRSA grid: {len(classes)} classes x layers {list(GTZAN_LAYERS)} (d=100/128/128) "
                       f"x 3 runs = {P} problems, K=4, N={N} each, {world} rank(s), LPT assignment, "
-                      "per-rank problems in one hipGraph (drsa_run_multi)",
+                      "each rank's problems batched: one launch per phase for all (drsa_run_batched)",
             "scaling": "strong", "steps": steps, "problems": P, "problems_per_rank": [per_rank.get(r, 0) for r in range(world)],
             "problem_steps_per_s": P * steps / dt, "vector_steps_per_s": P * N * steps / dt,
             "rank_seconds": dts,
