@@ -33,6 +33,8 @@ Reference defects handled (new D14-D16):
   sep_and_peak's RU are the subspace heatmaps of the same two sources.
 * D16: sep_and_peak calls ``frob(RU, num_concepts)`` with the whole list of K values (an error);
   here frob gets the current K (its value is unused by the reference's outputs).
+* D17: perform_cf writes to ``os.path.join(out, f'{prefix}/{k}_concepts')``, which for the default
+  prefix '' is the absolute path ``/{k}_concepts``; here ``{out}/{prefix}/{k}_concepts``.
 * ``case=`` (D5) selects the toy class map as in the reference; HeatmapGenerator infers it from
   the class name.
 """
@@ -167,7 +169,7 @@ def cf_random_subspace(model, input_batch, name_map, layer_idx, dim, case=None, 
                      device=device)
     R = torch.cat([_subspace_heatmaps(model, x[i * spc:(i + 1) * spc], U, name_map, g, num_concepts, layer_idx, device)
                    for i, g in enumerate(mapper)], 0)
-    return R if as_tensor else np.array(R.cpu())
+    return R if as_tensor else R.cpu().numpy()
 
 
 def _subspace_source(model, x, name_map, layer_idx, k, dim, prefix, path, case, device):
@@ -197,7 +199,7 @@ def perform_cf(model, input_batch, name_map, out, path=None, layer_idcs=(1, 4, 7
             else:
                 aupc, _, _ = concept_flipping(model, x, name_map, layer_idx, os.path.join(path, f"{k}_concepts"),
                                               num_concepts=k, case=case, device=device)
-            conf_out = os.path.join(out, f"{prefix}/{k}_concepts")
+            conf_out = os.path.join(out, prefix, f"{k}_concepts")   # D17
             os.makedirs(conf_out, exist_ok=True)
             with open(os.path.join(conf_out, f"aupcs_layer_{layer_idx}.pkl"), "wb") as fh:
                 pickle.dump(np.stack(aupc, axis=0), fh)
@@ -228,8 +230,8 @@ def sep_and_peak(model, input_batch, name_map, out, path=None, layer_idcs=(1, 4,
         sep, seperr, peak, peakerr = [], [], [], []
         for i, layer_idx in enumerate(layer_idcs):
             print(f"Performing concept patch flipping for {k} subspaces at layer {layer_idx}")
-            RU = np.array(_subspace_source(model, x, name_map, layer_idx, k, dims[i], prefix,
-                                           None if path is None else os.path.join(path, prefix), case, device).cpu())
+            RU = _subspace_source(model, x, name_map, layer_idx, k, dims[i], prefix,
+                                  None if path is None else os.path.join(path, prefix), case, device).cpu().numpy()
             frob(RU, k)                                    # computed as the reference does; unused (D16)
             s, se, p, pe = separability_peakness(RU)
             sep.append(s)
