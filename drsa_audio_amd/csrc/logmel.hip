@@ -46,6 +46,7 @@ struct LogmelArgs {
   float* out;                // [n_chunks][n_mels][width]
   // LDS carve (floats), computed on the host
   int o_tw, o_ptw, o_win, o_blo, o_bn, o_boff, o_bw, o_samp, o_fft, o_mel, o_red, smem_floats;
+  int o_bwt;                 // n_fft = 800 kernel: band weights transposed [LF_NBT][n_mels + 1]
 };
 
 struct cf {
@@ -251,227 +252,277 @@ __global__ __launch_bounds__(LM_THREADS) void logmel_kernel(LogmelArgs a) {
 }
 
 // ===========================================================================
-// Fast path for n_fft = 800 (GTZAN, AUDIO_PARAMS['gtzan']): the 400-point complex FFT of a
-// frame as 20 x 20 (n = 20 n1 + n2, k = k1 + 20 k2), each 20-point DFT in registers (4 x 5).
-// Three frames per wave, one lane per (frame, n2) in pass A and per (frame, k1) in pass B
-// (60 of 64 lanes busy): two LDS hand-offs per frame instead of the generic kernel's
-// Stockham stages.  Samples come straight from global memory (frames overlap 55 %, served by
-// L1/L2); one workgroup per chunk keeps the peak division and the coalesced output rows.
+// Fast path for n_fft = 800 (GTZAN, AUDIO_PARAMS['gtzan']).  One workgroup of 12 waves per chunk,
+// three frames per wave per round (36 frames per round).
+//   pass A: lane (frame, n2) loads z[20 n1 + n2] = x[2n] w[2n] + i x[2n+1] w[2n+1] (n1 < 20),
+//           DFT20 over n1 in registers, twiddle W_400^{n2 k1};
+//   transpose through a per-frame 420-float LDS slab, real and imaginary parts in turn (half
+//           the LDS of a complex slab, so 12 waves fit beside the [n_mels][width + 1] mel tile);
+//   pass B: lane (frame, k1) DFT20 over n2 -> Z[k1 + 20 k2];
+//   split:  Z[400 - k] from the partner lane (ds_bpermute), X[k] = (A + V_k B) / 2 with
+//           A = Z_k + conj Z_{M-k}, B = Z_k - conj Z_{M-k}, V_k = -i W_800^k;
+//   mel:    |X| into the wave's own slabs, lanes over (mel, frame) pairs with consecutive mels
+//           (similar band widths) in one pass; weights transposed [j][m] in LDS.
+// Every wave runs its rounds independently (no workgroup barrier before the peak), so the waves
+// drift apart and hide each other's latency.  STFT, filterbank and |.| are homogeneous, so the
+// chunk's peak division is applied to the mel energies at the end.  Measured (64 songs x 8 chunks):
+// 0.181 ms (round 2: 8 waves at 224 VGPRs, per-lane divergent mel loop with weights contiguous)
+// -> 0.122-0.127 ms.  LDS-bound (PMC: LDS active ~55 % of the kernel, VALU ~40 %).
 // ===========================================================================
-constexpr int LF_M = 400, LF_R = 20, LF_FPW = 3;   // complex points, radix, frames per wave
-// T layout: pass-A rows k1 at stride LF_RS = 21 (pass-B lanes k1 read a row each: 42-bank
-// stride, conflict-free); frames at LF_FS = 421 complex
-constexpr int LF_RS = 21, LF_FS = 421;
-#ifndef LF_UNROLL_MEL
-#define LF_UNROLL_MEL 0
-#endif
-#ifndef LF_VEC_LOADS
-#define LF_VEC_LOADS 0
-#endif
-constexpr int LF_MAXB = 20;                          // unrolled mel band width (wider: loop)
+typedef float v2f __attribute__((ext_vector_type(2)));
+// 12 waves (3 per SIMD): the kernel needs ~156 VGPRs; at 16 waves (128 VGPRs) it spilled and ran 4 %
+// slower
+constexpr int LF_M = 400, LF_R = 20, LF_FPW = 3, LF_WAVES = 12, LF_THREADS = LF_WAVES * 64;
+constexpr int LF_FPR = LF_WAVES * LF_FPW;   // frames per round
+constexpr int LF_RS = 21;          // transpose row stride: 21 * q distinct mod 32 for q < 20
+constexpr int LF_FS = 420;         // frame slab (== 4 mod 32: the three frames' pass-B reads are conflict-free)
+constexpr int LF_WB = LF_FPW * LF_FS;
+constexpr int LF_NBT = 16;         // band positions held transposed (wider bands read the rest from bw)
+// magnitude row of frame f at slab offset LF_MOFF(f) (0, 11, 5): with the transposed weights and the
+// padded mel tile, the mel stage's LDS accesses run at ~1.6 cycles per group instead of ~3
+__device__ __forceinline__ int lf_moff(int f) { return f == 0 ? 0 : (f == 1 ? 11 : 5); }
 
-__device__ __constant__ cf kW20[13] = {
-    {1.0f, 0.0f},
-    {9.51056516295153531e-01f, -3.09016994374947396e-01f},
-    {8.09016994374947451e-01f, -5.87785252292473137e-01f},
-    {5.87785252292473137e-01f, -8.09016994374947451e-01f},
-    {3.09016994374947451e-01f, -9.51056516295153531e-01f},
-    {0.0f, -1.0f},
-    {-3.09016994374947340e-01f, -9.51056516295153642e-01f},
-    {-5.87785252292473026e-01f, -8.09016994374947451e-01f},
-    {-8.09016994374947340e-01f, -5.87785252292473248e-01f},
-    {-9.51056516295153531e-01f, -3.09016994374947507e-01f},
-    {-1.0f, 0.0f},
-    {-9.51056516295153753e-01f, 3.09016994374946896e-01f},
-    {-8.09016994374947562e-01f, 5.87785252292473026e-01f}};
+// b (complex) from LDS tables: a * b
+__device__ __forceinline__ cf cmulv(cf a, cf b) { return {fmaf(a.x, b.x, -(a.y * b.y)), fmaf(a.x, b.y, a.y * b.x)}; }
 
-// forward 20-point DFT in place: v[n] -> v[k] (4 x 5: n = 5 n1 + n2, k = k1 + 4 k2)
-__device__ __forceinline__ void dft20(cf* v) {
-  cf y[4][5];
+// 20-point DFT on float2 vectors (v_pk_{add,mul,fma}_f32: fewer VALU instructions than scalar
+// complex code, which measured 2-3 % slower)
+__device__ __forceinline__ v2f vfma(v2f a, v2f b, v2f c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ v2f vsplat(float s) { return (v2f){s, s}; }
+__device__ __forceinline__ v2f vcmul(v2f a, v2f b) { return vfma(vsplat(a.y), (v2f){-b.y, b.x}, vsplat(a.x) * b); }
+__device__ __forceinline__ v2f vnegi(v2f a) { return (v2f){a.y, -a.x}; }   // -i a
+__device__ __forceinline__ void vbfly4(v2f& a0, v2f& a1, v2f& a2, v2f& a3) {
+  const v2f t0 = a0 + a2, t1 = a0 - a2, t2 = a1 + a3, t3 = vnegi(a1 - a3);
+  a0 = t0 + t2;
+  a2 = t0 - t2;
+  a1 = t1 + t3;
+  a3 = t1 - t3;
+}
+__device__ __forceinline__ void vbfly5(v2f& a0, v2f& a1, v2f& a2, v2f& a3, v2f& a4) {
+  const float c1 = 0.30901699437494742410f, c2 = -0.80901699437494742410f;
+  const float s1 = 0.95105651629515357212f, s2 = 0.58778525229247312917f;
+  const v2f b1 = a1 + a4, b2 = a2 + a3, d1 = a1 - a4, d2 = a2 - a3;
+  const v2f r1 = vfma(vsplat(c2), b2, vfma(vsplat(c1), b1, a0));
+  const v2f r2 = vfma(vsplat(c1), b2, vfma(vsplat(c2), b1, a0));
+  const v2f q1 = vnegi(vfma(vsplat(s2), d2, vsplat(s1) * d1));
+  const v2f q2 = vnegi(vfma(vsplat(-s1), d2, vsplat(s2) * d1));
+  a0 = a0 + (b1 + b2);
+  a1 = r1 + q1;
+  a4 = r1 - q1;
+  a2 = r2 + q2;
+  a3 = r2 - q2;
+}
+// forward 20-point DFT in place, natural order in and out (n = 5 a + b, k = c + 4 d)
+__device__ __forceinline__ void dft20(cf (&vc)[20]) {
+  const v2f W[13] = {{1.0f, 0.0f},
+                     {9.51056516295153531e-01f, -3.09016994374947396e-01f},
+                     {8.09016994374947451e-01f, -5.87785252292473137e-01f},
+                     {5.87785252292473137e-01f, -8.09016994374947451e-01f},
+                     {3.09016994374947451e-01f, -9.51056516295153531e-01f},
+                     {0.0f, -1.0f},
+                     {-3.09016994374947340e-01f, -9.51056516295153642e-01f},
+                     {-5.87785252292473026e-01f, -8.09016994374947451e-01f},
+                     {-8.09016994374947340e-01f, -5.87785252292473248e-01f},
+                     {-9.51056516295153531e-01f, -3.09016994374947507e-01f},
+                     {-1.0f, 0.0f},
+                     {-9.51056516295153753e-01f, 3.09016994374946896e-01f},
+                     {-8.09016994374947562e-01f, 5.87785252292473026e-01f}};
+  v2f v[20];
 #pragma unroll
-  for (int n2 = 0; n2 < 5; ++n2) {
-    cf t[4] = {v[n2], v[5 + n2], v[10 + n2], v[15 + n2]};
-    bfly4(t);
+  for (int i = 0; i < 20; ++i) v[i] = (v2f){vc[i].x, vc[i].y};
 #pragma unroll
-    for (int k1 = 0; k1 < 4; ++k1) y[k1][n2] = (n2 * k1 == 0) ? t[k1] : cmul(t[k1], kW20[n2 * k1]);
+  for (int b = 0; b < 5; ++b) {
+    vbfly4(v[b], v[5 + b], v[10 + b], v[15 + b]);
+#pragma unroll
+    for (int c = 1; c < 4; ++c)
+      if (b > 0) v[5 * c + b] = vcmul(v[5 * c + b], W[b * c]);
   }
 #pragma unroll
-  for (int k1 = 0; k1 < 4; ++k1) {
-    bfly5(y[k1]);
+  for (int c = 0; c < 4; ++c) {
+    vbfly5(v[5 * c], v[5 * c + 1], v[5 * c + 2], v[5 * c + 3], v[5 * c + 4]);
 #pragma unroll
-    for (int k2 = 0; k2 < 5; ++k2) v[k1 + 4 * k2] = y[k1][k2];
+    for (int d = 0; d < 5; ++d) vc[c + 4 * d] = {v[5 * c + d].x, v[5 * c + d].y};
   }
 }
 
-__global__ __launch_bounds__(LM_THREADS) void logmel800_kernel(LogmelArgs a) {
+__global__ __launch_bounds__(LF_THREADS) void logmel800_kernel(LogmelArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
   const int chunk = blockIdx.x;
   const float* x = a.wav + (int64_t)(chunk / a.chunks_per_song) * a.song_stride +
                    (int64_t)(chunk % a.chunks_per_song) * a.chunk_hop;
-  cf* tw = reinterpret_cast<cf*>(sm + a.o_tw);      // [k1][n2] = W_400^{n2 k1} (lanes n2 adjacent)
-  cf* ptw = reinterpret_cast<cf*>(sm + a.o_ptw);    // W_800^k, k <= 400
-  float* win = sm + a.o_win;
+  cf* tw = reinterpret_cast<cf*>(sm + a.o_tw);      // [k1][n2] = W_400^{n2 k1}
+  cf* vtw = reinterpret_cast<cf*>(sm + a.o_ptw);    // V_k = -i W_800^k, k <= 400
+  const float2* win2 = reinterpret_cast<const float2*>(sm + a.o_win);   // window pairs (w[2n], w[2n+1])
   int* blo = reinterpret_cast<int*>(sm + a.o_blo);
   int* bn = reinterpret_cast<int*>(sm + a.o_bn);
   int* boff = reinterpret_cast<int*>(sm + a.o_boff);
   float* bw = sm + a.o_bw;
-  cf* T = reinterpret_cast<cf*>(sm + a.o_fft) + (size_t)w * LF_FPW * LF_FS;  // [3][LF_FS] per wave
+  float* bwt = sm + a.o_bwt;                          // [j][m] at row stride n_mels + 1
+  float* buf = sm + a.o_fft;                          // [16 waves][3 frames][420]: transposes, then |X|
   float* mel = sm + a.o_mel;
   float* red = sm + a.o_red;
 
-  for (int j = tid; j < LF_M; j += LM_THREADS) {
+  for (int j = tid; j < LF_M; j += LF_THREADS) {
     double s, c;
     const int e = ((j / LF_R) * (j % LF_R)) % LF_M;
     sincospi(2.0 * (double)e / (double)LF_M, &s, &c);
     tw[j] = {(float)c, (float)-s};
   }
-  for (int k = tid; k <= LF_M; k += LM_THREADS) {
+  for (int k = tid; k <= LF_M; k += LF_THREADS) {
     double s, c;
-    sincospi((double)k / (double)LF_M, &s, &c);
-    ptw[k] = {(float)c, (float)-s};
+    sincospi((double)k / (double)LF_M, &s, &c);      // W_800^k = (c, -s);  -i W = (-s, -c)
+    vtw[k] = {(float)-s, (float)-c};
   }
-  for (int i = tid; i < 800; i += LM_THREADS) win[i] = a.window[i];
-  for (int m = tid; m < a.n_mels; m += LM_THREADS) {
+  for (int i = tid; i < 800; i += LF_THREADS) sm[a.o_win + i] = a.window[i];
+  for (int m = tid; m < a.n_mels; m += LF_THREADS) {
     blo[m] = a.band_lo[m];
     bn[m] = a.band_n[m];
     boff[m] = a.band_off[m];
   }
-  for (int i = tid; i < a.nnz; i += LM_THREADS) bw[i] = a.band_w[i];
+  for (int i = tid; i < a.nnz; i += LF_THREADS) bw[i] = a.band_w[i];
+  for (int i = tid; i < LF_NBT * a.n_mels; i += LF_THREADS) {
+    const int j = i / a.n_mels, m = i % a.n_mels;
+    bwt[j * (a.n_mels + 1) + m] = (j < a.band_n[m]) ? a.band_w[a.band_off[m] + j] : 0.f;
+  }
+  const int MW = a.width + 1;                         // padded mel-tile row (conflict-free column writes)
   __syncthreads();
 
-  const int fl = lane / LF_R, q = lane % LF_R;       // frame slot in the wave, n2 / k1
+  const int fl = lane / LF_R, q = lane % LF_R;        // frame slot in the wave, n2 (pass A) / k1 (pass B)
   const bool lact = lane < LF_FPW * LF_R;
+  const int partner = lact ? fl * LF_R + (q == 0 ? 0 : LF_R - q) : lane;
+  // float2 sample loads when every frame start is 8-byte aligned (even hop and an aligned chunk)
+  const bool vec_ok = (a.hop & 1) == 0 && ((((uintptr_t)x) & 7) == 0);
+  float* B = buf + w * LF_WB + (lact ? fl : 0) * LF_FS;
   float pk = 0.f;
-  constexpr int FPR = LM_WAVES * LF_FPW;             // frames per workgroup round
-  for (int tb = 0; tb < a.width; tb += FPR) {
-    const int fi = tb + w * LF_FPW + fl;             // frame slot index in [0, width)
-    const bool fok = lact && fi < a.width;
-    cf v[LF_R];
-    // ---- pass A: lane (frame, n2) loads z[20 n1 + n2] = x[2n] w[2n] + i x[2n+1] w[2n+1] ----
+  for (int tb = 0; tb < a.width; tb += LF_FPR) {
+    const int nfr = min(LF_FPR, a.width - tb);
+    const int s = LF_FPW * w + fl;                    // frame slot in the round
+    const bool fok = lact && s < nfr;
+    cf y[20];
+    // ---- pass A ----
     {
-      const int base = (a.frame0 + (fok ? fi : 0)) * a.hop - 400;
-      if (LF_VEC_LOADS && base >= 0 && base + 800 <= a.L && ((base + (int)((uintptr_t)x >> 2)) & 1) == 0) {
-        // interior frame, 8-byte aligned pairs: one float2 load per n1
-        const float2* xp = reinterpret_cast<const float2*>(x + base) + q;
+      const int base = (a.frame0 + tb + (fok ? s : 0)) * a.hop - 400;
+      const bool interior = base >= 0 && base + 800 <= a.L;
+      if (__all(interior)) {
+        if (vec_ok) {
+          const float2* xp = reinterpret_cast<const float2*>(x + base) + q;
+          float2 xv[LF_R];
 #pragma unroll
-        for (int n1 = 0; n1 < LF_R; ++n1) {
-          const float2 xv = xp[20 * n1];
-          const int s0 = 40 * n1 + 2 * q;
-          pk = fok ? fmaxf(pk, fmaxf(fabsf(xv.x), fabsf(xv.y))) : pk;
-          v[n1] = {xv.x * win[s0], xv.y * win[s0 + 1]};
+          for (int n1 = 0; n1 < LF_R; ++n1) xv[n1] = xp[LF_R * n1];
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int n1 = 0; n1 < LF_R; ++n1) {
+            pk = fmaxf(pk, fmaxf(fabsf(xv[n1].x), fabsf(xv[n1].y)));
+            { const float2 wv = win2[LF_R * n1 + q]; y[n1] = {xv[n1].x * wv.x, xv[n1].y * wv.y}; }
+            // window reads in groups of 4 (hoisting all 20 next to the 20 sample loads spills)
+            if (n1 % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+          }
+        } else {
+          const float* xp = x + base + 2 * q;
+#pragma unroll
+          for (int n1 = 0; n1 < LF_R; ++n1) {
+            const float x0 = xp[40 * n1], x1 = xp[40 * n1 + 1];
+            pk = fmaxf(pk, fmaxf(fabsf(x0), fabsf(x1)));
+            { const float2 wv = win2[LF_R * n1 + q]; y[n1] = {x0 * wv.x, x1 * wv.y}; }
+          }
         }
       } else {
 #pragma unroll
         for (int n1 = 0; n1 < LF_R; ++n1) {
           const int s0 = 40 * n1 + 2 * q;
           int j0 = base + s0, j1 = base + s0 + 1;
-          j0 = j0 < 0 ? -j0 : j0;
+          j0 = j0 < 0 ? -j0 : j0;                        // reflect (torch pad_mode="reflect")
           j0 = j0 >= a.L ? 2 * (a.L - 1) - j0 : j0;
           j1 = j1 < 0 ? -j1 : j1;
           j1 = j1 >= a.L ? 2 * (a.L - 1) - j1 : j1;
           const float x0 = x[j0], x1 = x[j1];
-          pk = fok ? fmaxf(pk, fmaxf(fabsf(x0), fabsf(x1))) : pk;
-          v[n1] = {x0 * win[s0], x1 * win[s0 + 1]};
+          pk = fmaxf(pk, fmaxf(fabsf(x0), fabsf(x1)));
+          { const float2 wv = win2[LF_R * n1 + q]; y[n1] = {x0 * wv.x, x1 * wv.y}; }
         }
       }
-      dft20(v);
-      // twiddle W_400^{n2 k1}, store T[k1][n2]
+      dft20(y);
 #pragma unroll
-      for (int k1 = 0; k1 < LF_R; ++k1) {
-        const cf t = (k1 == 0) ? v[0] : cmul(v[k1], tw[k1 * LF_R + q]);
-        if (lact) T[fl * LF_FS + k1 * LF_RS + q] = t;
-      }
+      for (int k1 = 1; k1 < LF_R; ++k1) y[k1] = cmulv(y[k1], tw[k1 * LF_R + q]);
     }
-    wave_lds_sync();
-    // ---- pass B: lane (frame, k1) reads T[k1][n2], DFT over n2 -> Z[k1 + 20 k2] ----
+    // ---- transpose (real parts, then imaginary parts) ----
+    cf v[20];
     if (lact) {
 #pragma unroll
-      for (int n2 = 0; n2 < LF_R; ++n2) v[n2] = T[fl * LF_FS + q * LF_RS + n2];
+      for (int k1 = 0; k1 < LF_R; ++k1) B[k1 * LF_RS + q] = y[k1].x;
     }
+    wave_lds_sync();
+    if (lact) {
+#pragma unroll
+      for (int n2 = 0; n2 < LF_R; ++n2) v[n2].x = B[q * LF_RS + n2];
+    }
+    wave_lds_sync();
+    if (lact) {
+#pragma unroll
+      for (int k1 = 0; k1 < LF_R; ++k1) B[k1 * LF_RS + q] = y[k1].y;
+    }
+    wave_lds_sync();
+    if (lact) {
+#pragma unroll
+      for (int n2 = 0; n2 < LF_R; ++n2) v[n2].y = B[q * LF_RS + n2];
+    } else {
+#pragma unroll
+      for (int n2 = 0; n2 < LF_R; ++n2) v[n2] = {0.f, 0.f};
+    }
+    // ---- pass B: Z[q + 20 k2] = v[k2] ----
     dft20(v);
-    wave_lds_sync();
-    if (lact) {
+    // ---- real-input split + |X| straight into the frame's slab (its transpose reads are done:
+    //      LDS ops of one wave stay in order) ----
 #pragma unroll
-      for (int k2 = 0; k2 < LF_R; ++k2) T[fl * LF_FS + q + LF_R * k2] = v[k2];
+    for (int k2 = 0; k2 < LF_R; ++k2) {
+      const cf zp = {__shfl(v[LF_R - 1 - k2].x, partner, 64), __shfl(v[LF_R - 1 - k2].y, partner, 64)};
+      const cf zr = (q == 0) ? v[(LF_R - k2) % LF_R] : zp;
+      const cf zk = v[k2];
+      const cf A = {zk.x + zr.x, zk.y - zr.y};
+      const cf Bv = {zk.x - zr.x, zk.y + zr.y};
+      const cf X2 = cadd(cmulv(Bv, vtw[q + LF_R * k2]), A);
+      if (lact) B[lf_moff(fl) + q + LF_R * k2] = 0.5f * sqrtf(X2.x * X2.x + X2.y * X2.y);
+      // groups of 5 bins: the scheduler would otherwise hoist all 40 partner shuffles (and the V
+      // reads) to the top and spill
+      if (k2 % 5 == 4) __builtin_amdgcn_sched_barrier(0);
     }
+    if (lact && q == 0) B[lf_moff(fl) + LF_M] = fabsf(v[0].x - v[0].y);   // X[400] = Re Z0 - Im Z0
     wave_lds_sync();
-    // ---- real split + |X|: 3 x 401 bins over the wave; magnitudes held in registers until
-    //      every lane has read its Z pairs, then written over T (as floats) ----
-    constexpr int NB = LF_FPW * (LF_M + 1);
-    constexpr int NIT = (NB + 63) / 64;
-    float mg[NIT];
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int i = lane + 64 * it;
-      const int f = i / (LF_M + 1), k = i % (LF_M + 1);
-      float m = 0.f;
-      if (i < NB) {
-        const cf* Z = T + f * LF_FS;
-        const cf zk = Z[k == LF_M ? 0 : k];
-        const cf zr = Z[k == 0 ? 0 : LF_M - k];
-        const cf zc = {zr.x, -zr.y};
-        const cf e = cscale(cadd(zk, zc), 0.5f);
-        const cf d = csub(zk, zc);
-        const cf o = {0.5f * d.y, -0.5f * d.x};
-        const cf X = cadd(e, cmul(ptw[k], o));
-        m = sqrtf(X.x * X.x + X.y * X.y);
-      }
-      mg[it] = m;
+    // ---- mel filters: lane pair p = (mel p / 3, frame p % 3), consecutive mels (similar band
+    //      widths) in one pass ----
+    for (int p0 = 0; p0 < LF_FPW * a.n_mels; p0 += 64) {
+      const int p = p0 + lane;
+      const int m = p / LF_FPW, f = p % LF_FPW;
+      const int t = tb + LF_FPW * w + f;
+      const bool ok = p < LF_FPW * a.n_mels && t < a.width;
+      const int mc = ok ? m : 0;
+      const int lo = blo[mc], nb = ok ? bn[mc] : 0;
+      const float* wm = bw + boff[mc];
+      const float* mp = buf + w * LF_WB + f * LF_FS + lf_moff(f) + lo;
+      const float* wt = bwt + mc;
+      float acc = 0.f;
+      for (int j = 0; j < nb; ++j) acc = fmaf(j < LF_NBT ? wt[j * (a.n_mels + 1)] : wm[j], mp[j], acc);
+      if (ok) mel[m * MW + t] = acc;
     }
-    wave_lds_sync();
-    float* magb = reinterpret_cast<float*>(T);      // [3][401] floats
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int i = lane + 64 * it;
-      if (i < NB) magb[i] = mg[it];
-    }
-    wave_lds_sync();
-    // ---- banded mel filters, lanes over (frame, mel) ----
-    for (int i = lane; i < LF_FPW * a.n_mels; i += 64) {
-      const int f = i / a.n_mels, m = i % a.n_mels;
-      const int t = tb + w * LF_FPW + f;
-      if (t < a.width) {
-        const float* wm = bw + boff[m];
-        const float* mgp = magb + f * (LF_M + 1) + blo[m];
-        const int nb = bn[m];
-        float acc = 0.f;
-        if (LF_UNROLL_MEL && nb <= LF_MAXB) {
-          // all band reads issued together (masked, clamped), then the ordered chain
-          float wv[LF_MAXB], mv[LF_MAXB];
-#pragma unroll
-          for (int qq = 0; qq < LF_MAXB; ++qq) {
-            const int qc = qq < nb ? qq : 0;
-            wv[qq] = wm[qc];
-            mv[qq] = mgp[qc];
-          }
-#pragma unroll
-          for (int qq = 0; qq < LF_MAXB; ++qq)
-            if (qq < nb) acc += wv[qq] * mv[qq];
-        } else {
-          for (int qq = 0; qq < nb; ++qq) acc += wm[qq] * mgp[qq];
-        }
-        mel[m * a.width + t] = acc;
-      }
-    }
-    wave_lds_sync();
+    wave_lds_sync();                                   // magnitudes consumed before the next round's transposes
   }
+  __syncthreads();
   {
     const int c0 = max(0, a.frame0 * a.hop - 400);
     const int c1 = min(a.L, (a.frame0 + a.width - 1) * a.hop + 400);
-    for (int i = tid; i < c0; i += LM_THREADS) pk = fmaxf(pk, fabsf(x[i]));
-    for (int i = c1 + tid; i < a.L; i += LM_THREADS) pk = fmaxf(pk, fabsf(x[i]));
+    for (int i = tid; i < c0; i += LF_THREADS) pk = fmaxf(pk, fabsf(x[i]));
+    for (int i = c1 + tid; i < a.L; i += LF_THREADS) pk = fmaxf(pk, fabsf(x[i]));
   }
   for (int o = 32; o > 0; o >>= 1) pk = fmaxf(pk, shfl_xor(pk, o));
   if (lane == 0) red[w] = pk;
   __syncthreads();
   float p = red[0];
-  for (int i = 1; i < LM_WAVES; ++i) p = fmaxf(p, red[i]);
+  for (int i = 1; i < LF_WAVES; ++i) p = fmaxf(p, red[i]);
   const float inv_scale = a.peak_norm ? p : 1.f;
   float* o = a.out + (size_t)chunk * a.n_mels * a.width;
   const int total = a.n_mels * a.width;
-  for (int i = tid; i < total; i += LM_THREADS) {
-    float vv = log10f(mel[i] / inv_scale + a.log_eps);
+  for (int i = tid; i < total; i += LF_THREADS) {
+    float vv = log10f(mel[(i / a.width) * MW + i % a.width] / inv_scale + a.log_eps);
     if (a.do_clamp) vv = (vv < a.clamp_min) ? a.clamp_min : vv;
     o[i] = vv;
   }
@@ -549,27 +600,32 @@ extern "C" int drsa_amd_logmel(const float* wav, int64_t n_songs, int64_t song_s
   a.out = out;
   const int M = n_fft / 2;
   static const int no_fast = getenv("DRSA_AMD_LOGMEL_GENERIC") ? atoi(getenv("DRSA_AMD_LOGMEL_GENERIC")) : 0;
-  const bool fast = n_fft == 800 && !no_fast;
-  int off = 0;
-  auto take = [&](int n) { int o = off; off += (n + 3) & ~3; return o; };
-  a.o_tw = take(2 * M);
-  a.o_ptw = take(2 * (M + 1));
-  a.o_win = take(n_fft);
-  a.o_blo = take(n_mels);
-  a.o_bn = take(n_mels);
-  a.o_boff = take(n_mels);
-  a.o_bw = take(band_nnz);
-  a.o_samp = take(fast ? 0 : (LM_WAVES - 1) * hop + n_fft);
-  a.o_fft = take(fast ? LM_WAVES * LF_FPW * 2 * LF_FS : LM_WAVES * 4 * M);
-  a.o_mel = take(n_mels * width);
-  a.o_red = take(LM_WAVES);
-  a.smem_floats = off;
-  const size_t smem = (size_t)off * 4;
+  auto carve = [&](bool fast) {
+    int off = 0;
+    auto take = [&](int n) { int o = off; off += (n + 3) & ~3; return o; };
+    a.o_tw = take(2 * M);
+    a.o_ptw = take(2 * (M + 1));
+    a.o_win = take(n_fft);
+    a.o_blo = take(n_mels);
+    a.o_bn = take(n_mels);
+    a.o_boff = take(n_mels);
+    a.o_bw = take(band_nnz);
+    a.o_samp = take(fast ? 0 : (LM_WAVES - 1) * hop + n_fft);
+    a.o_fft = take(fast ? LF_WAVES * LF_WB : LM_WAVES * 4 * M);
+    a.o_mel = take(fast ? n_mels * (width + 1) : n_mels * width);
+    a.o_bwt = take(fast ? LF_NBT * (n_mels + 1) : 0);
+    a.o_red = take(fast ? LF_WAVES : LM_WAVES);
+    a.smem_floats = off;
+    return (size_t)off * 4;
+  };
+  // the 16-wave n_fft = 800 kernel when its tables + mel tile fit in LDS, else the generic kernel
+  bool fast = n_fft == 800 && !no_fast && carve(true) <= 160 * 1024;
+  const size_t smem = carve(fast);
   DRSA_REQUIRE(smem <= 160 * 1024, "logmel: LDS footprint %zu B exceeds 160 KB (n_mels*width too large)", smem);
   const void* fn = fast ? (const void*)logmel800_kernel : (const void*)logmel_kernel;
   DRSA_SMEM(fn, smem);
   if (fast)
-    hipLaunchKernelGGL(logmel800_kernel, dim3((unsigned)n_chunks), dim3(LM_THREADS), smem, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(logmel800_kernel, dim3((unsigned)n_chunks), dim3(LF_THREADS), smem, (hipStream_t)stream, a);
   else
     hipLaunchKernelGGL(logmel_kernel, dim3((unsigned)n_chunks), dim3(LM_THREADS), smem, (hipStream_t)stream, a);
   DRSA_LAUNCH_CHECK();
