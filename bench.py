@@ -34,6 +34,7 @@ import numpy as np
 import torch
 
 FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: dense fp32 MFMA (= vector) peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0     # MI355X_MICROARCH.md: dense bf16 MFMA peak (no sparsity)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -326,8 +327,10 @@ def drsa_joint_bench(device, steps=200):
 def vggish_lrp_bench(device, B=32, iters=5):
     """C5 model: VGGish-BN, 128x256 log-mel.  Standard LRP (compute_relevances), the engine forward
     alone, and the C5 CNN leg (DRSA data capture at j = 26: forward + relevance backward to the
-    layer), each on the fp32 plan and on the bf16 plan (model.bfloat16(): conv forwards on
-    v_mfma_f32_32x32x16_bf16, relevance backward fp32; parity tests/test_bf16_gpu.py)."""
+    layer), each on the fp32 plan, on the bf16 plan (model.bfloat16(): conv forwards on
+    v_mfma_f32_32x32x16_bf16, relevance backward fp32; parity tests/test_bf16_gpu.py) and on the
+    bf16 plan with the bf16 relevance backward (tests/test_bf16_bwd_gpu.py), with a roofline line
+    for each standard-LRP pass's dominant kernel."""
     import copy
     from drsa_audio_amd.engine import get_engine
     from drsa_audio_amd.model.create_model import VGGType
@@ -352,12 +355,47 @@ def vggish_lrp_bench(device, B=32, iters=5):
         torch.cuda.synchronize(device)
         return B * iters / (time.perf_counter() - t0)
 
-    out = {"config": f"VGGish-BN (64,64,100,128,128), block_depth 2, 128x256, B={B}; samples/s"}
-    for prec, m, x in (("fp32", m32, x32), ("bf16", copy.deepcopy(m32).bfloat16(), x32.bfloat16())):
-        eng = get_engine(m, comp)
-        out[prec] = {"standard_lrp": timed(lambda: compute_relevances(m, x, comp, class_idx=1)),
-                     "forward": timed(lambda: eng.forward(x)),
-                     "capture_j26": timed(lambda: get_intermediate(m, x, comp, 26, 1))}
+    out = {"config": f"VGGish-BN (64,64,100,128,128), block_depth 2, 128x256, B={B}; samples/s",
+           "legs": "fp32 plan; bf16 plan (bf16 conv forwards, fp32 relevance backward); bf16_bwd (bf16 plan "
+                   "with the bf16 relevance backward, DRSA_AMD_BF16_BACKWARD=1)"}
+    prev = os.environ.get("DRSA_AMD_BF16_BACKWARD")
+    try:
+        for prec, m, x in (("fp32", m32, x32), ("bf16", copy.deepcopy(m32).bfloat16(), x32.bfloat16()),
+                           ("bf16_bwd", copy.deepcopy(m32).bfloat16(), x32.bfloat16())):
+            os.environ["DRSA_AMD_BF16_BACKWARD"] = "1" if prec == "bf16_bwd" else "0"
+            eng = get_engine(m, comp)
+            out[prec] = {"standard_lrp": timed(lambda: compute_relevances(m, x, comp, class_idx=1)),
+                         "forward": timed(lambda: eng.forward(x)),
+                         "capture_j26": timed(lambda: get_intermediate(m, x, comp, 26, 1))}
+            # roofline of the standard-LRP pass's dominant kernel (HIP events on the launch stream)
+            eng.trace = []
+            for _ in range(3):
+                compute_relevances(m, x, comp, class_idx=1)
+            torch.cuda.synchronize(device)
+            per = {}
+            for tag, e0, e1 in eng.trace:
+                per.setdefault(tag, []).append(e0.elapsed_time(e1))
+            eng.trace = None
+            macs = kernel_macs(eng, B, 0)
+            top = max(per, key=lambda k: float(np.mean(per[k])))
+            # the roofline line: the slowest MFMA conv kernel (the top kernel can be the VALU
+            # first-layer backward, reported beside it)
+            dom = max((k for k in per if k.startswith(("conv_fwd:", "conv_bwd:"))), key=lambda k: float(np.mean(per[k])))
+            avg = float(np.mean(per[dom]))
+            st = next((s_ for s_ in eng.stages if dom.endswith(":" + s_.name)), None)
+            on_bf16 = st is not None and st.cin > 1 and (
+                (dom.startswith("conv_fwd") and eng.bf16) or (dom.startswith("conv_bwd") and st.wts_bwd_bf is not None))
+            peak = BF16_MFMA_PEAK_TFLOPS if on_bf16 else FP32_MFMA_PEAK_TFLOPS
+            ach = 2.0 * macs.get(dom, 0) / (avg * 1e-3) / 1e12
+            out[prec]["roofline"] = {"bound": "mfma", "kernel": dom, "operands": "bf16" if on_bf16 else "fp32",
+                                     "avg_ms": avg, "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak}
+            out[prec]["top_kernel"] = {"tag": top, "avg_ms": float(np.mean(per[top]))}
+            out[prec]["kernels_ms"] = {k: float(np.mean(v)) for k, v in per.items()}
+    finally:
+        if prev is None:
+            os.environ.pop("DRSA_AMD_BF16_BACKWARD", None)
+        else:
+            os.environ["DRSA_AMD_BF16_BACKWARD"] = prev
     out["samples_per_s"] = out["fp32"]["standard_lrp"]
     return out
 

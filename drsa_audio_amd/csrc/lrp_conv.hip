@@ -10,7 +10,7 @@
 // ---------------------------------------------------------------------------
 namespace drsa_conv {
 extern const Table kTableFwdA, kTableFwdB, kTableFwdC, kTableFwdD, kTableFwdE, kTableBwdA, kTableBwdB, kTableBwdC,
-    kTableBwdcA, kTableBwdcB, kTableFwdBfA, kTableFwdBfB, kTableFwdBfC, kTableFwdP4;
+    kTableBwdcA, kTableBwdcB, kTableFwdBfA, kTableFwdBfB, kTableFwdBfC, kTableFwdP4, kTableBwdBfA, kTableBwdBfB;
 }
 
 namespace {
@@ -21,7 +21,8 @@ const drsa_conv::Table* kTables[] = {&drsa_conv::kTableFwdA, &drsa_conv::kTableF
                                      &drsa_conv::kTableFwdD, &drsa_conv::kTableFwdE, &drsa_conv::kTableBwdA,
                                      &drsa_conv::kTableBwdB, &drsa_conv::kTableBwdC, &drsa_conv::kTableBwdcA,
                                      &drsa_conv::kTableBwdcB, &drsa_conv::kTableFwdBfA, &drsa_conv::kTableFwdBfB,
-                                     &drsa_conv::kTableFwdBfC, &drsa_conv::kTableFwdP4};
+                                     &drsa_conv::kTableFwdBfC, &drsa_conv::kTableFwdP4, &drsa_conv::kTableBwdBfA,
+                                     &drsa_conv::kTableBwdBfB};
 
 int pad32(int c) { return (c + 31) / 32 * 32; }
 
@@ -155,6 +156,32 @@ int drsa_amd_conv_bwd(const float* g, const uint8_t* g_amax, const float* wts, c
     drsa::set_error("conv_bwd: no kernel for cin=%d cout=%d W=%d ng=%d sparse=%d", cin, cout, W, ng, g_amax != nullptr);
     return DRSA_EUNSUPPORTED;
   }
+  return launch(e, a, Bq, (hipStream_t)stream);
+}
+
+int drsa_amd_conv_bwd_has_kernel_bf16(int cin, int cout, int W, int ng, int sparse) {
+  if (cin < 16 || ng != 1) return 0;
+  return find(pad32(cin), pad32(cout), W, ng, sparse ? A_POOLSPARSE : A_DENSE, EPI_BWD, 1) != nullptr;
+}
+
+int drsa_amd_conv_bwd_bf16(const float* g, const uint8_t* g_amax, const uint16_t* wts, const float* x, const float* den,
+                           float* out, int Bq, int clones, int cin, int cout, int H, int W, int ng, int xmode,
+                           int post, float eps, void* stream) {
+  DRSA_REQUIRE(Bq > 0 && clones > 0 && Bq % clones == 0, "conv_bwd_bf16: bad batch/clones");
+  DRSA_REQUIRE(ng == 1, "conv_bwd_bf16: ng must be 1 (the Gamma x-/W- term is for the fp32 first layer)");
+  DRSA_REQUIRE(cin >= 16, "conv_bwd_bf16: cin >= 16 (16-channel bf16 chunks)");
+  DRSA_REQUIRE(H % 2 == 0 && W % 4 == 0, "conv_bwd_bf16: H must be even and W %% 4 == 0 (got %dx%d)", H, W);
+  DRSA_REQUIRE(xmode == XM_NONE || x, "conv_bwd_bf16: xmode needs x");
+  DRSA_REQUIRE(post == POST_NONE || (x && (den || post == POST_MASK)), "conv_bwd_bf16: POST_DIV needs x and den");
+  DRSA_REQUIRE(((uintptr_t)wts & 15) == 0, "conv_bwd_bf16: weights must be 16-byte aligned");
+  const Entry* e = find(pad32(cin), pad32(cout), W, ng, g_amax ? A_POOLSPARSE : A_DENSE, EPI_BWD, 1);
+  if (!e) {
+    drsa::set_error("conv_bwd_bf16: no kernel for cin=%d cout=%d W=%d sparse=%d", cin, cout, W, g_amax != nullptr);
+    return DRSA_EUNSUPPORTED;
+  }
+  ConvArgs a{};
+  a.in = g; a.in_amax = g_amax; a.wts = reinterpret_cast<const float*>(wts); a.x = x; a.den = den; a.out = out;
+  a.H = H; a.W = W; a.cin = cin; a.cout = cout; a.clones = clones; a.xmode = xmode; a.post = post; a.eps = eps;
   return launch(e, a, Bq, (hipStream_t)stream);
 }
 

@@ -143,7 +143,8 @@ struct ConvCfg {
   static_assert(COUT % 32 == 0, "COUT must be padded to 32");
   static_assert(CIN % CIC == 0, "CIN must be a multiple of the chunk");
   static_assert(MT % WM == 0 && NT % WN == 0 && WM * WN <= 4, "wave split");
-  static_assert(!BF || (CIC == 16 && EPI < EPI_BWD && AMODE == A_DENSE), "bf16: dense forward, 16-channel chunks");
+  static_assert(!BF || (CIC == 16 && (EPI < EPI_BWD ? AMODE == A_DENSE : EPI == EPI_BWD)),
+                "bf16: 16-channel chunks; dense forward, or the per-clone backward (dense or pool-sparse g)");
   static_assert(PW == 2 || (PW == 4 && EPI == EPI_FWD_POOL), "2x4 pool windows: forward pool epilogue only");
 };
 
@@ -414,21 +415,46 @@ struct StagerBF {
   float st_f[IT][8];
   uint4 st_w[WIT];
 
-  __device__ __forceinline__ void load(const ConvArgs& a, int c0, int tid, int ty0, int tx0, int bq, int) {
+  __device__ __forceinline__ void load(const ConvArgs& a, int c0, int tid, int ty0, int tx0, int bq, int bs) {
     const int H = a.H, W = a.W;
     const size_t HW = (size_t)H * W;
+    if constexpr (Cfg::AMODE_ == A_POOLSPARSE) {
+      // backward input at 2x2-pool resolution + argmax byte (the pool backward): halo pixel
+      // (gy, gx) holds g[cell] where the cell's argmax is this pixel, else 0
+      const int H2 = H >> 1, W2 = W >> 1;
+      const size_t HW2 = (size_t)H2 * W2;
 #pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int i = tid + it * NT_;
-      const int hx = i % HX, r = i / HX, hy = r % HY, half = r / HY;
-      const int gy = ty0 - 1 + hy, gx = tx0 - 1 + hx, cb = c0 + 8 * half;
-      const bool ok = i < NITEM && gy >= 0 && gy < H && gx >= 0 && gx < W;
-      const size_t base = ok ? ((size_t)bq * a.cin + cb) * HW + (size_t)gy * W + gx : 0;
+      for (int it = 0; it < IT; ++it) {
+        const int i = tid + it * NT_;
+        const int hx = i % HX, r = i / HX, hy = r % HY, half = r / HY;
+        const int gy = ty0 - 1 + hy, gx = tx0 - 1 + hx, cb = c0 + 8 * half;
+        const bool ok = i < NITEM && gy >= 0 && gy < H && gx >= 0 && gx < W;
+        const size_t cell = ok ? (size_t)(gy >> 1) * W2 + (gx >> 1) : 0;
+        const size_t base = ok ? ((size_t)bq * a.cin + cb) * HW2 + cell : 0;
+        const size_t abase = ok ? ((size_t)bs * a.cin + cb) * HW2 + cell : 0;
+        const uint32_t sub = (uint32_t)(((gy & 1) << 1) | (gx & 1));
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const bool okc = ok && cb + j < a.cin;
-        const float v = a.in[okc ? base + j * HW : 0];
-        st_f[it][j] = okc ? v : 0.f;
+        for (int j = 0; j < 8; ++j) {
+          const bool okc = ok && cb + j < a.cin;
+          const float v = a.in[okc ? base + j * HW2 : 0];
+          const uint32_t am = a.in_amax[okc ? abase + j * HW2 : 0];
+          st_f[it][j] = (okc && am == sub) ? v : 0.f;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int i = tid + it * NT_;
+        const int hx = i % HX, r = i / HX, hy = r % HY, half = r / HY;
+        const int gy = ty0 - 1 + hy, gx = tx0 - 1 + hx, cb = c0 + 8 * half;
+        const bool ok = i < NITEM && gy >= 0 && gy < H && gx >= 0 && gx < W;
+        const size_t base = ok ? ((size_t)bq * a.cin + cb) * HW + (size_t)gy * W + gx : 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const bool okc = ok && cb + j < a.cin;
+          const float v = a.in[okc ? base + j * HW : 0];
+          st_f[it][j] = okc ? v : 0.f;
+        }
       }
     }
     const uint4* wq = reinterpret_cast<const uint4*>(a.wts);
@@ -654,7 +680,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
     stg.store(halo, wl, tid);
     __syncthreads();
     epi_loads(0, 0, pre_x, pre_d, true, DRSA_CONV_PRE_D, 0, kPreN);
-    if (active && !(a.dbg & 4)) mfma_chunk<Cfg, Cfg::PD>(halo, wl, pix_off, lane, wn, acc);
+    if (active && !(a.dbg & 4)) {
+      if constexpr (Cfg::BF)
+        mfma_chunk_bf<Cfg>(reinterpret_cast<const uint4*>(halo), reinterpret_cast<const uint4*>(wl), pix_off, lane, wn,
+                           acc);
+      else
+        mfma_chunk<Cfg, Cfg::PD>(halo, wl, pix_off, lane, wn, acc);
+    }
   }
 
   // the pool cells of the staged tile T (2 x PWc windows), one per thread and iteration `it`
@@ -986,6 +1018,19 @@ struct Entry {
   drsa_conv::Entry{CIN, COUT, TH, TW, MW, CIC, NG, AM, EP,                                                 \
                    drsa_conv::conv3x3_kernel<CIN, COUT, TH, TW, MW, CIC, NG, AM, EP>,                      \
                    drsa_conv::ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AM, EP>::lds_floats * sizeof(float)}
+
+#define CONV_ENTRY_BFA(CIN, COUT, TH, TW, MW, NG, AM, EP)                                                 \
+  drsa_conv::Entry{CIN, COUT, TH, TW, MW, 16, NG, AM, EP,                                                 \
+                   drsa_conv::conv3x3_kernel<CIN, COUT, TH, TW, MW, 16, NG, AM, EP, 1>,                   \
+                   drsa_conv::ConvCfg<CIN, COUT, TH, TW, MW, 16, NG, AM, EP, 1>::lds_floats * sizeof(float), 1}
+// bf16-operand per-clone backward (ET = 1), dense and pool-sparse g, one weight set
+#define BWD_SET_BF(CIN, COUT)                                                                    \
+  CONV_ENTRY_BFA(CIN, COUT, 8, 32, 8, 1, drsa_conv::A_DENSE, drsa_conv::EPI_BWD),                \
+  CONV_ENTRY_BFA(CIN, COUT, 8, 16, 8, 1, drsa_conv::A_DENSE, drsa_conv::EPI_BWD),                \
+  CONV_ENTRY_BFA(CIN, COUT, 8, 8, 4, 1, drsa_conv::A_DENSE, drsa_conv::EPI_BWD),                 \
+  CONV_ENTRY_BFA(CIN, COUT, 8, 32, 8, 1, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD),           \
+  CONV_ENTRY_BFA(CIN, COUT, 8, 16, 8, 1, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD),           \
+  CONV_ENTRY_BFA(CIN, COUT, 8, 8, 4, 1, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD)
 
 #define CONV_ENTRY_BF(CIN, COUT, TH, TW, MW, NG, EP)                                                     \
   drsa_conv::Entry{CIN, COUT, TH, TW, MW, 16, NG, drsa_conv::A_DENSE, EP,                                 \

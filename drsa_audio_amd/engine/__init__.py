@@ -16,7 +16,7 @@ import weakref
 from collections import OrderedDict
 
 from .hooks import HookedAutograd, has_custom_hooks
-from .plan import EngineError, LRPEngine
+from .plan import EngineError, LRPEngine, bf16_backward_default
 
 _MAX = max(1, int(os.environ.get("DRSA_AMD_ENGINE_CACHE", "8")))
 _CACHE: "OrderedDict[tuple, _Entry]" = OrderedDict()
@@ -54,7 +54,7 @@ def _evict(key) -> None:
 def get_engine(model, composite) -> LRPEngine:
     """Compiled plan for (model, composite), cached while the model's parameters are unchanged."""
     key = (id(model), id(composite))
-    fp = _fingerprint(model)
+    fp = (_fingerprint(model), bf16_backward_default())   # the option selects different kernels
     e = _CACHE.get(key)
     if e is not None:
         if e.model_ref() is model and e.comp_ref() is composite and e.fp == fp:

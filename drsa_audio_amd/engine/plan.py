@@ -26,7 +26,10 @@ Precision: a model whose parameters are bfloat16 (``model.bfloat16()``) compiles
 backward) is rounded to bf16, the network input is rounded to bf16, and every conv with Cin > 1
 runs forward on ``drsa_amd_conv_fwd_bf16`` (inputs rounded to bf16 as they are staged,
 v_mfma_f32_32x32x16_bf16, fp32 accumulation).  Biases, activations, denominators, the dense head
-and the whole relevance backward stay fp32 (oracle: ``lrp_ref.lrp(mode="bf16")``).
+and the whole relevance backward stay fp32 (oracle: ``lrp_ref.lrp(mode="bf16")``).  With
+``bf16_backward`` (``DRSA_AMD_BF16_BACKWARD=1``) every backward conv with Cin > 1 (ng = 1) also runs
+on bf16 operands: ``drsa_amd_conv_bwd_bf16`` rounds the quotient g = R / stab(den) to bf16 as it is
+staged, accumulates in fp32, and keeps the epilogue fp32 (oracle: ``mode="bf16bwd"``).
 """
 from __future__ import annotations
 
@@ -103,6 +106,7 @@ class ConvStage:
     wts_bwd_n: torch.Tensor = None
     wts_fwd_bf: torch.Tensor = None      # bf16 plan: [ng][cin_p/16][9][2][cout_p][8] bfloat16
     wts_fwd_n_bf: torch.Tensor = None
+    wts_bwd_bf: torch.Tensor = None       # bf16 backward: [cout_p/16][9][2][pad32(cin)][8] bfloat16
     alpha: float = 1.0
     beta: float = 0.0
     ng_bwd: int = 1
@@ -131,7 +135,7 @@ class EngineError(NotImplementedError):
 
 class LRPEngine:
     def __init__(self, model: nn.Module, composite, device: Optional[torch.device] = None,
-                 precision: Optional[str] = None):
+                 precision: Optional[str] = None, bf16_backward: Optional[bool] = None):
         _capi.load()
         # no strong references to the model / composite: the plan owns prepared copies of what it
         # needs, and get_engine's cache is keyed by weak references (engine/__init__.py)
@@ -145,6 +149,11 @@ class LRPEngine:
             raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
         self.precision = precision
         self.bf16 = precision == "bf16"
+        # bf16 plan option: the relevance backward convs on bf16 operands too (g rounded to bf16 as it
+        # is staged, fp32 accumulation and epilogue); default from DRSA_AMD_BF16_BACKWARD (off)
+        if bf16_backward is None:
+            bf16_backward = bf16_backward_default()
+        self.bf16_backward = bool(bf16_backward) and self.bf16
         if self.device.type != "cuda":
             raise _capi.DrsaAmdError("the LRP engine runs on the GPU only; move the model to a HIP device")
         rules = composite.rules(model) if composite is not None else {}
@@ -427,6 +436,9 @@ class LRPEngine:
             st.wts_fwd_bf = _bf16_layout(st.wts_fwd, cin_p, cout_p)
             if st.wts_fwd_n is not None:
                 st.wts_fwd_n_bf = _bf16_layout(st.wts_fwd_n, cin_p, cout_p)
+        if (self.bf16_backward and st.cin > 1 and st.ng_bwd == 1 and st.den_kind != "ab" and
+                _capi.lib().drsa_amd_conv_bwd_has_kernel_bf16(st.cout, st.cin, 32, 1, 0)):
+            st.wts_bwd_bf = _bf16_layout(st.wts_bwd, cout_p, _pad32(st.cin))
         if st.proj is not None and st.proj.U.size(0) != st.cout:
             raise EngineError("engine: projection width differs from the conv channels")
 
@@ -686,7 +698,10 @@ class LRPEngine:
                            clones, st.cin * h * w, post, float(eps), s)
             else:
                 out = self._buf((li, "R"), (Bq, st.cin, h, w))
-                self._call(f"conv_bwd:{st.name}", "drsa_amd_conv_bwd", g.data_ptr(), _capi.ptr(amax_in), st.wts_bwd.data_ptr(),
+                bf = st.wts_bwd_bf is not None and _capi.lib().drsa_amd_conv_bwd_has_kernel_bf16(
+                    st.cout, st.cin, w, 1, int(amax_in is not None))
+                self._call(f"conv_bwd:{st.name}", "drsa_amd_conv_bwd_bf16" if bf else "drsa_amd_conv_bwd", g.data_ptr(),
+                           _capi.ptr(amax_in), (st.wts_bwd_bf if bf else st.wts_bwd).data_ptr(),
                            x_in.data_ptr() if (st.xmode_bwd != XM_NONE or post != POST_NONE) else None,
                            _capi.ptr(den), out.data_ptr(), Bq, clones, st.cout, st.cin, h, w, st.ng_bwd,
                            st.xmode_bwd, post, float(eps), s)
@@ -764,6 +779,11 @@ class LRPEngine:
                    out["subspace_heatmaps"].data_ptr(), out["subspace_relevances"].data_ptr(), out["mask"].data_ptr(),
                    _capi.stream_ptr(self.device))
         return out
+
+
+def bf16_backward_default() -> bool:
+    """DRSA_AMD_BF16_BACKWARD=1: bf16 plans also run the relevance backward convs on bf16 operands."""
+    return os.environ.get("DRSA_AMD_BF16_BACKWARD", "0") not in ("", "0")
 
 
 def _bf16r(t: torch.Tensor) -> torch.Tensor:

@@ -149,6 +149,22 @@ int drsa_amd_conv_bwd(const float* g, const uint8_t* g_amax, const float* wts, c
                       float* out, int Bq, int clones, int cin, int cout, int H, int W, int ng, int xmode,
                       int post, float eps, void* stream);
 
+/* bf16-operand variant of drsa_amd_conv_bwd (SURVEY C5 "VGGish-depth CNN bf16": the relevance
+ * backward of a bf16 plan; the reference has no bf16 path).  g (the quotient R / stab(den) entering
+ * the transposed conv, after the pool backward) is rounded to bf16 (nearest even) as it is staged,
+ * the weights come pre-rounded in the forward bf16 layout of the backward weight set:
+ * [cin_p/16][9 taps][2][cout_p][8] bf16 with cin = g channels (the forward cout), cout = output
+ * channels (the forward cin), both padded to 32 (drsa_amd_conv_weight_bf16_elems(cin, cout, 1)
+ * elements, 16-byte aligned); products are summed in fp32 on v_mfma_f32_32x32x16_bf16 and the
+ * epilogue (x-multiply, the next layer's division) is fp32 as in drsa_amd_conv_bwd.  ng = 1 and
+ * cin >= 16 only (the first layer keeps the fp32 kernel).  Replaces the same zennit rule
+ * backward as drsa_amd_conv_bwd (constants.py:27-51). */
+int drsa_amd_conv_bwd_bf16(const float* g, const uint8_t* g_amax, const uint16_t* wts, const float* x, const float* den,
+                           float* out, int Bq, int clones, int cin, int cout, int H, int W, int ng, int xmode,
+                           int post, float eps, void* stream);
+/* 1 if drsa_amd_conv_bwd_bf16 has a kernel for this shape (sparse: g at 2x2-pool resolution). */
+int drsa_amd_conv_bwd_has_kernel_bf16(int cin, int cout, int W, int ng, int sparse);
+
 /* Dense layer forward: z = x W^T + b [, relu(z)]  (classifier Linear layers). */
 int drsa_amd_linear_fwd(const float* x, const float* W, const float* bias, float* z_out, float* relu_out, int M,
                         int N, int K, void* stream);

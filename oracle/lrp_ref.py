@@ -47,6 +47,8 @@ Five execution modes share that arithmetic:
   move subspace relevances by up to ~6 %), so only a pinned order can pin it.
 * ``mode="bf16"``     — float64 with every conv's input and weights rounded to bf16 (class
   ``Bf16Ops``): the definition of the product's bf16 plan (no reference bf16 path).
+* ``mode="bf16bwd"``  — ``bf16`` plus the transposed convs' g rounded to bf16 for layers with
+  more than one input channel (``Bf16BwdOps``): the plan's ``bf16_backward`` option.
 """
 from __future__ import annotations
 
@@ -324,10 +326,24 @@ class Bf16Ops(TorchOps):
         return ExactOps.inv_projection(L, h, a_map).to(a_map.dtype)
 
 
+class Bf16BwdOps(Bf16Ops):
+    """Bf16Ops plus the bf16 relevance backward (engine option bf16_backward,
+    drsa_amd_conv_bwd_bf16): every transposed conv of a layer with more than one input channel
+    also rounds its input g (the quotient R / stab(den), after the pool backward) to bf16; the
+    first layer (one input channel) keeps a full-precision g, as the product's fp32 kernel does."""
+    name = "bf16bwd"
+
+    @staticmethod
+    def conv_t(m, x_shape, w, g):
+        gi = _bf16r(g) if m.in_channels > 1 else g
+        return TorchOps.conv_t(m, x_shape, _bf16r(w), gi)
+
+
 # "f64": the analytic structure evaluated in float64 (model and input promoted): the accuracy
 # anchor that fp32 implementations (the reference's own path, the HIP kernels) are measured against.
 # "bf16": the same in float64 with Bf16Ops (input rounded to bf16 first).
-OPS = {"analytic": TorchOps, "zennit": TorchOps, "exact": ExactOps, "f64": TorchOps, "bf16": Bf16Ops}
+OPS = {"analytic": TorchOps, "zennit": TorchOps, "exact": ExactOps, "f64": TorchOps, "bf16": Bf16Ops,
+       "bf16bwd": Bf16BwdOps}
 
 
 def _aff(L: Layer, x, w, b, ops=TorchOps):
@@ -572,10 +588,10 @@ def lrp(model: nn.Module, rules: Dict[str, RuleSpec], x: torch.Tensor, class_idx
     values (the product's own activations, which differ from this forward's by accumulation-order
     rounding only), so that a bf16 rounding decision taken on them is the product's; the rest of
     the forward and the whole backward are evaluated here."""
-    if mode in ("f64", "bf16"):
+    if mode in ("f64", "bf16", "bf16bwd"):
         import copy
         model = copy.deepcopy(model).double()
-    if mode == "bf16":
+    if mode in ("bf16", "bf16bwd"):
         # the plan's weights are bf16 values (after any BN merge); rule-modified sets derived from
         # them are rounded again by Bf16Ops
         for mod in model.modules():
@@ -584,8 +600,8 @@ def lrp(model: nn.Module, rules: Dict[str, RuleSpec], x: torch.Tensor, class_idx
     layers = sequential_layers(model)
     ops = OPS[mode]
     acts: List[Tuple[torch.Tensor, torch.Tensor, object]] = []
-    h = x.detach().to(torch.float64 if mode in ("f64", "bf16") else torch.float32)
-    if mode == "bf16":
+    h = x.detach().to(torch.float64 if mode in ("f64", "bf16", "bf16bwd") else torch.float32)
+    if mode in ("bf16", "bf16bwd"):
         h = _bf16r(h)
     for L in layers:
         aux = None
@@ -687,7 +703,7 @@ def subspace_heatmaps(proj_model: nn.Module, name_map: Dict[str, RuleSpec], K: i
     default; equal in exact arithmetic since every rule is linear in the relevance).  Default:
     "sum" for the product-order modes ("exact", "bf16"), "clone" otherwise."""
     if standard is None:
-        standard = "sum" if mode in ("exact", "bf16") else "clone"
+        standard = "sum" if mode in ("exact", "bf16", "bf16bwd") else "clone"
     rules = class_composite_rules(name_map, K)
     xr = x.repeat_interleave(K + 1, dim=0)
     if forced_inputs is not None:
