@@ -931,6 +931,30 @@ int drsa_amd_drsa_fused_step(const float* A, const float* C, int64_t N, int d, i
   return fused_step(A, C, N, (double)N_total, g, gs, gs_out, U, U_out, f_out, nullptr, ws, (hipStream_t)stream);
 }
 
+int drsa_amd_drsa_fused_step_counted(const float* A, const float* C, int64_t N, int d, int K, const float* gs,
+                                     int64_t N_total, const float* U, float* U_out, float* f_traj, int* counter,
+                                     float* gs_out, void* ws, size_t ws_size, void* stream) {
+  const Geom g = geom(d, K);
+  DRSA_REQUIRE(g.ok && fused_ok(g), "drsa_fused_step_counted: unsupported d=%d K=%d", d, K);
+  DRSA_REQUIRE(N > 0 && N_total >= N, "drsa_fused_step_counted: need 0 < N <= N_total");
+  DRSA_REQUIRE(A && C && gs && U && U_out && f_traj && counter && gs_out, "drsa_fused_step_counted: null pointer");
+  DRSA_REQUIRE(U != U_out, "drsa_fused_step_counted: U and U_out must not alias");
+  DRSA_REQUIRE(ws && ws_size >= ws_bytes(N, g), "drsa_fused_step_counted: workspace too small");
+  DRSA_REQUIRE(((uintptr_t)A % 16) == 0 && ((uintptr_t)C % 16) == 0, "drsa_fused_step_counted: A/C must be 16B aligned");
+  return fused_step(A, C, N, (double)N_total, g, gs, gs_out, U, U_out, f_traj, counter, ws, (hipStream_t)stream);
+}
+
+int drsa_amd_drsa_finish_counted(const float* gs, int64_t N_total, int d, int K, const float* U, float* U_out,
+                                 float* f_traj, int* counter, void* stream) {
+  const Geom g = geom(d, K);
+  DRSA_REQUIRE(g.ok, "drsa_finish_counted: unsupported d=%d K=%d", d, K);
+  DRSA_REQUIRE(N_total > 0, "drsa_finish_counted: N_total must be > 0");
+  DRSA_REQUIRE(gs && U && U_out && f_traj && counter, "drsa_finish_counted: null pointer");
+  DRSA_REQUIRE(U != U_out, "drsa_finish_counted: U and U_out must not alias");
+  return dispatch_finish(gs, (double)N_total, g, U, U_out, f_traj, counter, 1, 0, kPolarTol, kPolarMaxIter, nullptr,
+                         (hipStream_t)stream);
+}
+
 int drsa_amd_drsa_step(const float* A, const float* C, int64_t N, int d, int K, const float* U,
                        float* U_out, float* f_out, void* ws, size_t ws_size, void* stream) {
   const Geom g = geom(d, K);

@@ -12,7 +12,10 @@ polar step, so U stays replicated without a broadcast.  The step math is the ref
 (``drsa.py:84-106``); sharding is exact up to the fp32 summation order of the partials.
 
 The per-step kernels are pluggable (``backend``) so the orchestration is tested on CPU with
-gloo (tests/test_dist_cpu.py) using the oracle's closed form; the product backend is HIP.
+gloo (tests/test_dist_cpu.py) using the oracle's closed form; the product backend is HIP.  Over
+RCCL the step loop is captured once in a graph -- the all-reduce and the step kernels of two steps
+-- and replayed (the trajectory slot advances through a device counter), so no Python or launch
+work sits between steps; DRSA_AMD_SHARDED_GRAPH=0 runs it eagerly (same kernels, same bits).
 """
 from __future__ import annotations
 
@@ -67,10 +70,53 @@ class HipBackend:
                    gs.data_ptr(), int(N_total), U.data_ptr(), U_out.data_ptr(), f_out.data_ptr(), gs_out.data_ptr(),
                    self.ws.ptr, self.ws.nbytes, _capi.stream_ptr(U.device))
 
+    def fused_counted(self, gs: torch.Tensor, N_total: int, U: torch.Tensor, U_out: torch.Tensor,
+                      f_traj: torch.Tensor, counter: torch.Tensor, gs_out: torch.Tensor) -> None:
+        """fused() with f(U) -> f_traj[*counter], counter += 1 on the device (graph replays)."""
+        _capi.call("drsa_amd_drsa_fused_step_counted", self.A.data_ptr(), self.C.data_ptr(), self.A.size(0), self.d,
+                   self.K, gs.data_ptr(), int(N_total), U.data_ptr(), U_out.data_ptr(), f_traj.data_ptr(),
+                   counter.data_ptr(), gs_out.data_ptr(), self.ws.ptr, self.ws.nbytes, _capi.stream_ptr(U.device))
+
+    def finish_counted(self, gs: torch.Tensor, N_total: int, U: torch.Tensor, U_out: torch.Tensor,
+                       f_traj: torch.Tensor, counter: torch.Tensor) -> None:
+        _capi.call("drsa_amd_drsa_finish_counted", gs.data_ptr(), int(N_total), self.d, self.K, U.data_ptr(),
+                   U_out.data_ptr(), f_traj.data_ptr(), counter.data_ptr(), _capi.stream_ptr(U.device))
+
     def objective(self, gs: torch.Tensor, N_total: int, U: torch.Tensor) -> torch.Tensor:
         _capi.call("drsa_amd_drsa_finish", gs.data_ptr(), int(N_total), self.d, self.K, U.data_ptr(), None,
                    self.f.data_ptr(), 1, None, _capi.stream_ptr(U.device))
         return self.f.clone()
+
+
+# graph replays issued by the sharded loops in this process (tests check the graph path ran)
+STATS = {"graph_replays": 0, "capture_failures": 0}
+
+
+def _graph_ok(group, backends) -> bool:
+    """Capture the step loop (kernels + the RCCL all-reduce) in a graph: RCCL process group, HIP
+    backends, and DRSA_AMD_SHARDED_GRAPH not 0."""
+    if os.environ.get("DRSA_AMD_SHARDED_GRAPH", "1") == "0" or not dist.is_initialized():
+        return False
+    if not all(isinstance(b, HipBackend) for b in backends):
+        return False
+    try:
+        return dist.get_backend(group) == "nccl"
+    except Exception:
+        return False
+
+
+def _capture(body) -> Optional["torch.cuda.CUDAGraph"]:
+    """One captured replay of ``body`` (two steps: U ping-pongs back to its buffer), or None when
+    the capture is refused (then the loop runs eagerly, same kernels and the same bits)."""
+    g = torch.cuda.CUDAGraph()
+    try:
+        with torch.cuda.graph(g):
+            body()
+    except Exception:
+        torch.cuda.synchronize()
+        STATS["capture_failures"] += 1
+        return None
+    return g
 
 
 def sharded_run(A_local: torch.Tensor, C_local: torch.Tensor, U0: torch.Tensor, K: int, steps: int,
@@ -87,11 +133,25 @@ def sharded_run(A_local: torch.Tensor, C_local: torch.Tensor, U0: torch.Tensor, 
         # between two buffers and f lands in its trajectory slot (no per-step allocation)
         Ub = [U0.detach().clone().contiguous(), torch.empty_like(U0)]
         traj_t = torch.empty(steps + 1, device=U0.device, dtype=torch.float32)
+        counter = torch.zeros(1, device=U0.device, dtype=torch.int32)   # f(U_t) -> traj_t[counter++]
         gs = backend.partial(Ub[0])
-        for t in range(steps):
+
+        def step(t):
             if dist.is_initialized():
                 dist.all_reduce(gs, op=dist.ReduceOp.SUM, group=group)
-            backend.fused(gs, N_total, Ub[t % 2], Ub[(t + 1) % 2], traj_t[t:t + 1], gs)
+            backend.fused_counted(gs, N_total, Ub[t % 2], Ub[(t + 1) % 2], traj_t, counter, gs)
+
+        t0 = 0
+        if steps >= 4 and _graph_ok(group, [backend]):
+            # the whole step (all-reduce + fused launch) replayed from one graph, two steps per replay
+            graph = _capture(lambda: (step(0), step(1)))
+            if graph is not None:
+                for _ in range(steps // 2):
+                    graph.replay()
+                STATS["graph_replays"] += steps // 2
+                t0 = 2 * (steps // 2)
+        for t in range(t0, steps):
+            step(t)
         if dist.is_initialized():
             dist.all_reduce(gs, op=dist.ReduceOp.SUM, group=group)
         traj_t[steps:] = backend.objective(gs, N_total, Ub[steps % 2])
@@ -142,10 +202,35 @@ def sharded_run_joint(problems, steps: int, group=None, backends=None):
             if dist.is_initialized():
                 dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
 
-        for t in range(steps):
+        counters = [torch.zeros(1, device=dev, dtype=torch.int32) for _ in range(P)]
+        # the P finishes (single-workgroup polar each) run concurrently: problems 1.. on side streams
+        side = [torch.cuda.Stream(device=dev) for _ in range(P - 1)]
+
+        def step(t):
             reduce_all([Ub[p][t % 2] for p in range(P)])
+            cur = torch.cuda.current_stream(dev)
+            ev = torch.cuda.Event()
+            ev.record(cur)
             for p in range(P):
-                backends[p].finish_into(backends[p].gs, N_tot[p], Ub[p][t % 2], Ub[p][(t + 1) % 2], tr[p][t:t + 1])
+                st = cur if p == 0 else side[p - 1]
+                if p:
+                    st.wait_event(ev)
+                with torch.cuda.stream(st):
+                    backends[p].finish_counted(backends[p].gs, N_tot[p], Ub[p][t % 2], Ub[p][(t + 1) % 2], tr[p],
+                                               counters[p])
+            for st in side:
+                cur.wait_stream(st)
+
+        t0 = 0
+        if steps >= 4 and _graph_ok(group, backends):
+            graph = _capture(lambda: (step(0), step(1)))
+            if graph is not None:
+                for _ in range(steps // 2):
+                    graph.replay()
+                STATS["graph_replays"] += steps // 2
+                t0 = 2 * (steps // 2)
+        for t in range(t0, steps):
+            step(t)
         reduce_all([Ub[p][steps % 2] for p in range(P)])
         out = []
         for p in range(P):

@@ -72,6 +72,16 @@ int drsa_amd_drsa_fused_step(const float* A, const float* C, int64_t N, int d, i
                              int64_t N_total, const float* U, float* U_out, float* f_out, float* gs_out, void* ws,
                              size_t ws_size, void* stream);
 
+/* Counter-indexed forms for a step loop captured once in a graph and replayed (the sharded loop
+ * with its RCCL all-reduce, xai/drsa/distributed.py): f(U) goes to f_traj[*counter] and the device
+ * int *counter is incremented by the kernel, so every replay fills the next trajectory slot.
+ * Otherwise identical to drsa_amd_drsa_fused_step / drsa_amd_drsa_finish (objective_only = 0). */
+int drsa_amd_drsa_fused_step_counted(const float* A, const float* C, int64_t N, int d, int K, const float* gs,
+                                     int64_t N_total, const float* U, float* U_out, float* f_traj, int* counter,
+                                     float* gs_out, void* ws, size_t ws_size, void* stream);
+int drsa_amd_drsa_finish_counted(const float* gs, int64_t N_total, int d, int K, const float* U, float* U_out,
+                                 float* f_traj, int* counter, void* stream);
+
 /* One SubspaceOptimizer.run iteration (drsa.py:84-106): f_out[0] = f(U), U_out = new U. */
 int drsa_amd_drsa_step(const float* A, const float* C, int64_t N, int d, int K, const float* U,
                        float* U_out, float* f_out, void* workspace, size_t workspace_bytes, void* stream);

@@ -357,3 +357,57 @@ def test_bf16_joint_run_objective_within_loosened_tolerance(tdt):
         Un = U16.cpu().double().numpy()
         assert np.abs(Un.T @ Un - np.eye(128)).max() < 1e-5
     assert torch.equal(one16[1], j16[0][1])           # single-problem bf16 route = joint route
+
+
+def _rccl_graph_worker(port, A, C, U0, K, steps, q):
+    """One rank over RCCL (nccl backend, world size 1): the sharded loops with the step graph
+    (all-reduce captured) and eagerly, C4-shape fused and C5-shape joint."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    from drsa_audio_amd.xai.drsa import distributed as D
+    out = {}
+    Ag, Cg, Ug = (torch.from_numpy(v).to(dev) for v in (A, C, U0))
+    g = torch.Generator().manual_seed(3)
+    U5 = [torch.linalg.qr(torch.randn(128, 128, generator=g, dtype=torch.float64))[0].float().to(dev) for _ in range(2)]
+    probs = []
+    for p_ in range(2):
+        A5, C5 = drsa_inputs(3000, 128, 40 + p_)
+        probs.append((torch.from_numpy(A5).to(dev), torch.from_numpy(C5).to(dev), U5[p_], 16))
+    for mode in ("1", "0"):
+        os.environ["DRSA_AMD_SHARDED_GRAPH"] = mode
+        U, tr = D.sharded_run(Ag, Cg, Ug, K, steps)
+        joint = D.sharded_run_joint(probs, 7)
+        out[mode] = (U.cpu().numpy(), tr, [(u.cpu().numpy(), t) for u, t in joint])
+        if mode == "1":
+            out["stats"] = dict(D.STATS)
+    dist.destroy_process_group()
+    q.put(out)
+
+
+@pytest.mark.gpu
+def test_sharded_step_graph_over_rccl_equals_eager():
+    """The captured sharded step (RCCL all-reduce + fused step in one graph, replayed; odd step
+    counts finish eagerly) gives exactly the eager loop's U and trajectory, fused and joint."""
+    import socket
+    import torch.multiprocessing as mp
+    A, C = drsa_inputs(20000, 64, 12)
+    U0 = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "u64_seed42.npy"))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_graph_worker, args=(port, A, C, U0, 8, 11, q))
+    p.start()
+    out = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    g, e = out["1"], out["0"]
+    assert out["stats"]["graph_replays"] == 5 + 3 and out["stats"]["capture_failures"] == 0, out["stats"]
+    assert np.array_equal(g[0], e[0]) and np.array_equal(g[1], e[1])
+    assert len(g[1]) == 12 and np.all(np.isfinite(g[1]))
+    for (ug, tg), (ue, te) in zip(g[2], e[2]):
+        assert np.array_equal(ug, ue) and np.array_equal(tg, te)
