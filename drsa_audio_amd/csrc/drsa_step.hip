@@ -458,16 +458,36 @@ __global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_ker
 // (Measured against float4 / 64-group and slab-split variants in scripts/probe_reduce.hip: the
 // kernel boundary behind 4-17 MB of freshly written slabs dominates; this one is the fastest.)
 // ---------------------------------------------------------------------------
+// One chain per (element, p mod 4): sum over p = grp, grp + 4, ... in ascending order.  The slabs
+// were just written by every CU of the partial (L2 of other XCDs / HBM), so the chain's loads are
+// all issued before its adds (RB of them per batch): one memory round trip per batch instead of
+// one per 8 loads -- the same additions in the same order, so the same bits.
+#ifndef DRSA_REDUCE_BATCH
+#define DRSA_REDUCE_BATCH 64
+#endif
+constexpr int kReduceBatch = DRSA_REDUCE_BATCH;
+__device__ __forceinline__ float reduce_chain(const float* __restrict__ partials, int P, int ES, int e, int grp) {
+  float acc = 0.f;
+  for (int p0 = grp; p0 < P; p0 += 4 * kReduceBatch) {
+    float v[kReduceBatch];
+#pragma unroll
+    for (int j = 0; j < kReduceBatch; ++j) {
+      const int p = p0 + 4 * j;
+      v[j] = partials[(size_t)(p < P ? p : grp) * ES + e];
+    }
+#pragma unroll
+    for (int j = 0; j < kReduceBatch; ++j)
+      if (p0 + 4 * j < P) acc += v[j];
+  }
+  return acc;
+}
+
 __global__ __launch_bounds__(256) void drsa_reduce_kernel(const float* __restrict__ partials, int P, int E, int ES,
                                                           float* __restrict__ out) {
   __shared__ float part[4][64];
   const int l = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + l;
-  float acc = 0.f;
-  if (e < E) {
-#pragma unroll 8
-    for (int p = grp; p < P; p += 4) acc += partials[(size_t)p * ES + e];
-  }
+  const float acc = e < E ? reduce_chain(partials, P, ES, e, grp) : 0.f;
   part[grp][l] = acc;
   __syncthreads();
   if (grp == 0 && e < E) out[e] = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
@@ -606,11 +626,7 @@ __global__ __launch_bounds__(256) void drsa_reduce_batched_kernel(const BatchDes
   const int G = q.G;
   const int l = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + l;
-  float acc = 0.f;
-  if (e < E) {
-#pragma unroll 8
-    for (int p = grp; p < G; p += 4) acc += q.partials[(size_t)p * ES + e];
-  }
+  const float acc = e < E ? reduce_chain(q.partials, G, ES, e, grp) : 0.f;
   part[grp][l] = acc;
   __syncthreads();
   if (grp == 0 && e < E) q.gs[e] = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
