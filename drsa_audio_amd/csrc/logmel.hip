@@ -270,8 +270,9 @@ __global__ __launch_bounds__(LM_THREADS) void logmel_kernel(LogmelArgs a) {
 // -> 0.122-0.127 ms.  LDS-bound (PMC: LDS active ~55 % of the kernel, VALU ~40 %).
 // ===========================================================================
 typedef float v2f __attribute__((ext_vector_type(2)));
-// 12 waves (3 per SIMD): the kernel needs ~156 VGPRs; at 16 waves (128 VGPRs) it spilled and ran 4 %
-// slower
+// 12 waves (3 per SIMD; the LDS footprint holds one block per CU).  110 VGPRs since lanes 60-63
+// duplicate lanes 0-3 (with active-lane branches: ~156 VGPRs, 0.124 ms -> 0.119 ms without); at 16
+// waves the tables + mel tile exceed 160 KB of LDS
 constexpr int LF_M = 400, LF_R = 20, LF_FPW = 3, LF_WAVES = 12, LF_THREADS = LF_WAVES * 64;
 constexpr int LF_FPR = LF_WAVES * LF_FPW;   // frames per round
 constexpr int LF_RS = 21;          // transpose row stride: 21 * q distinct mod 32 for q < 20
@@ -388,17 +389,18 @@ __global__ __launch_bounds__(LF_THREADS) void logmel800_kernel(LogmelArgs a) {
   const int MW = a.width + 1;                         // padded mel-tile row (conflict-free column writes)
   __syncthreads();
 
-  const int fl = lane / LF_R, q = lane % LF_R;        // frame slot in the wave, n2 (pass A) / k1 (pass B)
-  const bool lact = lane < LF_FPW * LF_R;
-  const int partner = lact ? fl * LF_R + (q == 0 ? 0 : LF_R - q) : lane;
+  // frame slot in the wave and n2 (pass A) / k1 (pass B); lanes 60-63 duplicate lanes 0-3 (same
+  // loads, same values, same LDS addresses), so no stage needs an active-lane branch
+  const int fl = lane < LF_FPW * LF_R ? lane / LF_R : 0, q = lane < LF_FPW * LF_R ? lane % LF_R : lane - LF_FPW * LF_R;
+  const int partner = fl * LF_R + (q == 0 ? 0 : LF_R - q);
   // float2 sample loads when every frame start is 8-byte aligned (even hop and an aligned chunk)
   const bool vec_ok = (a.hop & 1) == 0 && ((((uintptr_t)x) & 7) == 0);
-  float* B = buf + w * LF_WB + (lact ? fl : 0) * LF_FS;
+  float* B = buf + w * LF_WB + fl * LF_FS;
   float pk = 0.f;
   for (int tb = 0; tb < a.width; tb += LF_FPR) {
     const int nfr = min(LF_FPR, a.width - tb);
     const int s = LF_FPW * w + fl;                    // frame slot in the round
-    const bool fok = lact && s < nfr;
+    const bool fok = s < nfr;
     cf y[20];
     // ---- pass A ----
     {
@@ -447,28 +449,17 @@ __global__ __launch_bounds__(LF_THREADS) void logmel800_kernel(LogmelArgs a) {
     }
     // ---- transpose (real parts, then imaginary parts) ----
     cf v[20];
-    if (lact) {
 #pragma unroll
-      for (int k1 = 0; k1 < LF_R; ++k1) B[k1 * LF_RS + q] = y[k1].x;
-    }
+    for (int k1 = 0; k1 < LF_R; ++k1) B[k1 * LF_RS + q] = y[k1].x;
     wave_lds_sync();
-    if (lact) {
 #pragma unroll
-      for (int n2 = 0; n2 < LF_R; ++n2) v[n2].x = B[q * LF_RS + n2];
-    }
+    for (int n2 = 0; n2 < LF_R; ++n2) v[n2].x = B[q * LF_RS + n2];
     wave_lds_sync();
-    if (lact) {
 #pragma unroll
-      for (int k1 = 0; k1 < LF_R; ++k1) B[k1 * LF_RS + q] = y[k1].y;
-    }
+    for (int k1 = 0; k1 < LF_R; ++k1) B[k1 * LF_RS + q] = y[k1].y;
     wave_lds_sync();
-    if (lact) {
 #pragma unroll
-      for (int n2 = 0; n2 < LF_R; ++n2) v[n2].y = B[q * LF_RS + n2];
-    } else {
-#pragma unroll
-      for (int n2 = 0; n2 < LF_R; ++n2) v[n2] = {0.f, 0.f};
-    }
+    for (int n2 = 0; n2 < LF_R; ++n2) v[n2].y = B[q * LF_RS + n2];
     // ---- pass B: Z[q + 20 k2] = v[k2] ----
     dft20(v);
     // ---- real-input split + |X| straight into the frame's slab (its transpose reads are done:
@@ -481,12 +472,12 @@ __global__ __launch_bounds__(LF_THREADS) void logmel800_kernel(LogmelArgs a) {
       const cf A = {zk.x + zr.x, zk.y - zr.y};
       const cf Bv = {zk.x - zr.x, zk.y + zr.y};
       const cf X2 = cadd(cmulv(Bv, vtw[q + LF_R * k2]), A);
-      if (lact) B[lf_moff(fl) + q + LF_R * k2] = 0.5f * sqrtf(X2.x * X2.x + X2.y * X2.y);
+      B[lf_moff(fl) + q + LF_R * k2] = 0.5f * sqrtf(X2.x * X2.x + X2.y * X2.y);
       // groups of 5 bins: the scheduler would otherwise hoist all 40 partner shuffles (and the V
       // reads) to the top and spill
       if (k2 % 5 == 4) __builtin_amdgcn_sched_barrier(0);
     }
-    if (lact && q == 0) B[lf_moff(fl) + LF_M] = fabsf(v[0].x - v[0].y);   // X[400] = Re Z0 - Im Z0
+    if (q == 0) B[lf_moff(fl) + LF_M] = fabsf(v[0].x - v[0].y);   // X[400] = Re Z0 - Im Z0
     wave_lds_sync();
     // ---- mel filters: lane pair p = (mel p / 3, frame p % 3), consecutive mels (similar band
     //      widths) in one pass ----
