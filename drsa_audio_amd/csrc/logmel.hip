@@ -273,6 +273,29 @@ typedef float v2f __attribute__((ext_vector_type(2)));
 // 12 waves (3 per SIMD; the LDS footprint holds one block per CU).  110 VGPRs since lanes 60-63
 // duplicate lanes 0-3 (with active-lane branches: ~156 VGPRs, 0.124 ms -> 0.119 ms without); at 16
 // waves the tables + mel tile exceed 160 KB of LDS
+#ifndef LF_SPLIT_GROUP
+#define LF_SPLIT_GROUP 5
+#endif
+#ifndef LF_MEL_UNROLL
+#define LF_MEL_UNROLL 4
+#endif
+#ifndef LF_WIN_GROUP
+#define LF_WIN_GROUP 4
+#endif
+// LF_PROFILE builds (scripts/logmel_phases.py only): per-wave clock cycles of each phase
+#ifdef LF_PROFILE
+__device__ unsigned long long lf_prof_buf[4096 * 12 * 8];
+#define LF_T(i)                                                    \
+  do {                                                             \
+    __builtin_amdgcn_sched_barrier(0);                             \
+    const unsigned long long t_ = __builtin_readcyclecounter();    \
+    lf_acc[i] += t_ - lf_t;                                        \
+    lf_t = t_;                                                     \
+    __builtin_amdgcn_sched_barrier(0);                             \
+  } while (0)
+#else
+#define LF_T(i) do {} while (0)
+#endif
 constexpr int LF_M = 400, LF_R = 20, LF_FPW = 3, LF_WAVES = 12, LF_THREADS = LF_WAVES * 64;
 constexpr int LF_FPR = LF_WAVES * LF_FPW;   // frames per round
 constexpr int LF_RS = 21;          // transpose row stride: 21 * q distinct mod 32 for q < 20
@@ -350,6 +373,9 @@ __global__ __launch_bounds__(LF_THREADS) void logmel800_kernel(LogmelArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
   const int chunk = blockIdx.x;
+#ifdef LF_PROFILE
+  unsigned long long lf_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, lf_t = __builtin_readcyclecounter();
+#endif
   const float* x = a.wav + (int64_t)(chunk / a.chunks_per_song) * a.song_stride +
                    (int64_t)(chunk % a.chunks_per_song) * a.chunk_hop;
   cf* tw = reinterpret_cast<cf*>(sm + a.o_tw);      // [k1][n2] = W_400^{n2 k1}
@@ -388,6 +414,7 @@ __global__ __launch_bounds__(LF_THREADS) void logmel800_kernel(LogmelArgs a) {
   }
   const int MW = a.width + 1;                         // padded mel-tile row (conflict-free column writes)
   __syncthreads();
+  LF_T(0);
 
   // frame slot in the wave and n2 (pass A) / k1 (pass B); lanes 60-63 duplicate lanes 0-3 (same
   // loads, same values, same LDS addresses), so no stage needs an active-lane branch
@@ -418,7 +445,7 @@ __global__ __launch_bounds__(LF_THREADS) void logmel800_kernel(LogmelArgs a) {
             pk = fmaxf(pk, fmaxf(fabsf(xv[n1].x), fabsf(xv[n1].y)));
             { const float2 wv = win2[LF_R * n1 + q]; y[n1] = {xv[n1].x * wv.x, xv[n1].y * wv.y}; }
             // window reads in groups of 4 (hoisting all 20 next to the 20 sample loads spills)
-            if (n1 % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+            if (n1 % LF_WIN_GROUP == LF_WIN_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
           }
         } else {
           const float* xp = x + base + 2 * q;
@@ -443,10 +470,12 @@ __global__ __launch_bounds__(LF_THREADS) void logmel800_kernel(LogmelArgs a) {
           { const float2 wv = win2[LF_R * n1 + q]; y[n1] = {x0 * wv.x, x1 * wv.y}; }
         }
       }
+      LF_T(1);
       dft20(y);
 #pragma unroll
       for (int k1 = 1; k1 < LF_R; ++k1) y[k1] = cmulv(y[k1], tw[k1 * LF_R + q]);
     }
+    LF_T(2);
     // ---- transpose (real parts, then imaginary parts) ----
     cf v[20];
 #pragma unroll
@@ -460,8 +489,10 @@ __global__ __launch_bounds__(LF_THREADS) void logmel800_kernel(LogmelArgs a) {
     wave_lds_sync();
 #pragma unroll
     for (int n2 = 0; n2 < LF_R; ++n2) v[n2].y = B[q * LF_RS + n2];
+    LF_T(3);
     // ---- pass B: Z[q + 20 k2] = v[k2] ----
     dft20(v);
+    LF_T(4);
     // ---- real-input split + |X| straight into the frame's slab (its transpose reads are done:
     //      LDS ops of one wave stay in order) ----
 #pragma unroll
@@ -472,13 +503,15 @@ __global__ __launch_bounds__(LF_THREADS) void logmel800_kernel(LogmelArgs a) {
       const cf A = {zk.x + zr.x, zk.y - zr.y};
       const cf Bv = {zk.x - zr.x, zk.y + zr.y};
       const cf X2 = cadd(cmulv(Bv, vtw[q + LF_R * k2]), A);
-      B[lf_moff(fl) + q + LF_R * k2] = 0.5f * sqrtf(X2.x * X2.x + X2.y * X2.y);
+      // v_sqrt_f32 (1 ulp; the correctly rounded sqrtf expands to ~10 instructions)
+      B[lf_moff(fl) + q + LF_R * k2] = 0.5f * __builtin_amdgcn_sqrtf(X2.x * X2.x + X2.y * X2.y);
       // groups of 5 bins: the scheduler would otherwise hoist all 40 partner shuffles (and the V
       // reads) to the top and spill
-      if (k2 % 5 == 4) __builtin_amdgcn_sched_barrier(0);
+      if (k2 % LF_SPLIT_GROUP == LF_SPLIT_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
     }
     if (q == 0) B[lf_moff(fl) + LF_M] = fabsf(v[0].x - v[0].y);   // X[400] = Re Z0 - Im Z0
     wave_lds_sync();
+    LF_T(5);
     // ---- mel filters: lane pair p = (mel p / 3, frame p % 3), consecutive mels (similar band
     //      widths) in one pass ----
     for (int p0 = 0; p0 < LF_FPW * a.n_mels; p0 += 64) {
@@ -491,11 +524,25 @@ __global__ __launch_bounds__(LF_THREADS) void logmel800_kernel(LogmelArgs a) {
       const float* wm = bw + boff[mc];
       const float* mp = buf + w * LF_WB + f * LF_FS + lf_moff(f) + lo;
       const float* wt = bwt + mc;
+      // the same sequential fma chain, its LDS reads issued LF_MEL_UNROLL at a time (past the
+      // band: weight 0 and magnitude 0, acc + 0 * 0 == acc for the non-negative sums here)
       float acc = 0.f;
-      for (int j = 0; j < nb; ++j) acc = fmaf(j < LF_NBT ? wt[j * (a.n_mels + 1)] : wm[j], mp[j], acc);
+      for (int j0 = 0; j0 < nb; j0 += LF_MEL_UNROLL) {
+        float wv[LF_MEL_UNROLL], mv[LF_MEL_UNROLL];
+#pragma unroll
+        for (int u = 0; u < LF_MEL_UNROLL; ++u) {
+          const int j = j0 + u;
+          const bool jok = j < nb;
+          wv[u] = jok ? (j < LF_NBT ? wt[j * (a.n_mels + 1)] : wm[j]) : 0.f;
+          mv[u] = jok ? mp[j] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < LF_MEL_UNROLL; ++u) acc = fmaf(wv[u], mv[u], acc);
+      }
       if (ok) mel[m * MW + t] = acc;
     }
     wave_lds_sync();                                   // magnitudes consumed before the next round's transposes
+    LF_T(6);
   }
   __syncthreads();
   {
@@ -509,14 +556,25 @@ __global__ __launch_bounds__(LF_THREADS) void logmel800_kernel(LogmelArgs a) {
   __syncthreads();
   float p = red[0];
   for (int i = 1; i < LF_WAVES; ++i) p = fmaxf(p, red[i]);
-  const float inv_scale = a.peak_norm ? p : 1.f;
+  // mel / peak as mel * (1 / peak) (a power-of-two input scaling still cancels exactly) and
+  // log10 as v_log_f32 * log10(2): 1-2 ulp instead of the ~40-instruction divide + log10f
+  const float rscale = a.peak_norm ? 1.f / p : 1.f;
   float* o = a.out + (size_t)chunk * a.n_mels * a.width;
   const int total = a.n_mels * a.width;
+  int m = tid / a.width, t = tid % a.width;
+  const int dm = LF_THREADS / a.width, dt = LF_THREADS % a.width;
   for (int i = tid; i < total; i += LF_THREADS) {
-    float vv = log10f(mel[(i / a.width) * MW + i % a.width] / inv_scale + a.log_eps);
+    float vv = __builtin_amdgcn_logf(fmaf(mel[m * MW + t], rscale, a.log_eps)) * 0.30102999566398120f;
     if (a.do_clamp) vv = (vv < a.clamp_min) ? a.clamp_min : vv;
     o[i] = vv;
+    m += dm;
+    t += dt;
+    if (t >= a.width) { t -= a.width; ++m; }
   }
+#ifdef LF_PROFILE
+  LF_T(7);
+  if (chunk < 4096) lf_prof_buf[((size_t)chunk * LF_WAVES + w) * 8 + (lane & 7)] = lf_acc[lane & 7];
+#endif
 }
 
 int factor_radices(int M, int* r) {
@@ -530,6 +588,11 @@ int factor_radices(int M, int* r) {
 
 }  // namespace
 
+#ifdef LF_PROFILE
+extern "C" int drsa_amd_logmel_prof(unsigned long long* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(lf_prof_buf), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -1;
+}
+#endif
 extern "C" int drsa_amd_logmel_smem_bytes(int n_fft, int hop, int n_mels, int width, int band_nnz) {
   const int M = n_fft / 2;
   int off = 0;
