@@ -296,7 +296,7 @@ __device__ unsigned long long lf_prof_buf[4096 * 12 * 8];
 #else
 #define LF_T(i) do {} while (0)
 #endif
-constexpr int LF_M = 400, LF_R = 20, LF_FPW = 3, LF_WAVES = 12, LF_THREADS = LF_WAVES * 64;
+constexpr int LF_M = 400, LF_R = 20, LF_FPW = 3, LF_WAVES = 8, LF_THREADS = LF_WAVES * 64;
 constexpr int LF_FPR = LF_WAVES * LF_FPW;   // frames per round
 constexpr int LF_RS = 21;          // transpose row stride: 21 * q distinct mod 32 for q < 20
 constexpr int LF_FS = 420;         // frame slab (== 4 mod 32: the three frames' pass-B reads are conflict-free)
@@ -369,7 +369,7 @@ __device__ __forceinline__ void dft20(cf (&vc)[20]) {
   }
 }
 
-__global__ __launch_bounds__(LF_THREADS) void logmel800_kernel(LogmelArgs a) {
+__global__ __launch_bounds__(LF_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void logmel800_kernel(LogmelArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
   const int chunk = blockIdx.x;
@@ -387,9 +387,9 @@ __global__ __launch_bounds__(LF_THREADS) void logmel800_kernel(LogmelArgs a) {
   float* bw = sm + a.o_bw;
   float* bwt = sm + a.o_bwt;                          // [j][m] at row stride n_mels + 1
   float* buf = sm + a.o_fft;                          // [16 waves][3 frames][420]: transposes, then |X|
-  float* mel = sm + a.o_mel;
   float* red = sm + a.o_red;
 
+  LF_T(7);
   for (int j = tid; j < LF_M; j += LF_THREADS) {
     double s, c;
     const int e = ((j / LF_R) * (j % LF_R)) % LF_M;
@@ -412,8 +412,8 @@ __global__ __launch_bounds__(LF_THREADS) void logmel800_kernel(LogmelArgs a) {
     const int j = i / a.n_mels, m = i % a.n_mels;
     bwt[j * (a.n_mels + 1) + m] = (j < a.band_n[m]) ? a.band_w[a.band_off[m] + j] : 0.f;
   }
-  const int MW = a.width + 1;                         // padded mel-tile row (conflict-free column writes)
   __syncthreads();
+  float* o = a.out + (size_t)chunk * a.n_mels * a.width;
   LF_T(0);
 
   // frame slot in the wave and n2 (pass A) / k1 (pass B); lanes 60-63 duplicate lanes 0-3 (same
@@ -539,40 +539,52 @@ __global__ __launch_bounds__(LF_THREADS) void logmel800_kernel(LogmelArgs a) {
 #pragma unroll
         for (int u = 0; u < LF_MEL_UNROLL; ++u) acc = fmaf(wv[u], mv[u], acc);
       }
-      if (ok) mel[m * MW + t] = acc;
+      if (ok) o[m * a.width + t] = acc;               // linear mel; log + peak scale below
     }
     wave_lds_sync();                                   // magnitudes consumed before the next round's transposes
     LF_T(6);
   }
-  __syncthreads();
   {
     const int c0 = max(0, a.frame0 * a.hop - 400);
     const int c1 = min(a.L, (a.frame0 + a.width - 1) * a.hop + 400);
     for (int i = tid; i < c0; i += LF_THREADS) pk = fmaxf(pk, fabsf(x[i]));
     for (int i = c1 + tid; i < a.L; i += LF_THREADS) pk = fmaxf(pk, fabsf(x[i]));
   }
-  for (int o = 32; o > 0; o >>= 1) pk = fmaxf(pk, shfl_xor(pk, o));
+  for (int off = 32; off > 0; off >>= 1) pk = fmaxf(pk, shfl_xor(pk, off));
   if (lane == 0) red[w] = pk;
-  __syncthreads();
-  float p = red[0];
-  for (int i = 1; i < LF_WAVES; ++i) p = fmaxf(p, red[i]);
-  // mel / peak as mel * (1 / peak) (a power-of-two input scaling still cancels exactly) and
-  // log10 as v_log_f32 * log10(2): 1-2 ulp instead of the ~40-instruction divide + log10f
-  const float rscale = a.peak_norm ? 1.f / p : 1.f;
-  float* o = a.out + (size_t)chunk * a.n_mels * a.width;
+  __syncthreads();   // the block's linear mel visible to all its waves (stores write through the CU's L1)
+  float peak = red[0];
+  for (int i = 1; i < LF_WAVES; ++i) peak = fmaxf(peak, red[i]);
+  LF_T(7);
+  // in place over the block's own output (just written, L2-resident): mel / peak as
+  // mel * (1 / peak) (a power-of-two input scaling still cancels exactly) and log10 as
+  // v_log_f32 * log10(2): 1-2 ulp instead of the ~40-instruction divide + log10f
+  const float rscale = a.peak_norm ? 1.f / peak : 1.f;
   const int total = a.n_mels * a.width;
-  int m = tid / a.width, t = tid % a.width;
-  const int dm = LF_THREADS / a.width, dt = LF_THREADS % a.width;
-  for (int i = tid; i < total; i += LF_THREADS) {
-    float vv = __builtin_amdgcn_logf(fmaf(mel[m * MW + t], rscale, a.log_eps)) * 0.30102999566398120f;
-    if (a.do_clamp) vv = (vv < a.clamp_min) ? a.clamp_min : vv;
-    o[i] = vv;
-    m += dm;
-    t += dt;
-    if (t >= a.width) { t -= a.width; ++m; }
+  auto fin = [&](float v) {
+    float vv = __builtin_amdgcn_logf(fmaf(v, rscale, a.log_eps)) * 0.30102999566398120f;
+    return a.do_clamp ? ((vv < a.clamp_min) ? a.clamp_min : vv) : vv;
+  };
+  if ((((uintptr_t)o) & 15) == 0 && (total & 3) == 0) {
+    float4* o4 = reinterpret_cast<float4*>(o);
+    constexpr int EU = 8;
+    for (int i0 = 0; i0 < total / 4; i0 += EU * LF_THREADS) {
+      float4 v[EU];
+#pragma unroll
+      for (int u = 0; u < EU; ++u) {
+        const int i = i0 + u * LF_THREADS + tid;
+        if (i < total / 4) v[u] = o4[i];
+      }
+#pragma unroll
+      for (int u = 0; u < EU; ++u) {
+        const int i = i0 + u * LF_THREADS + tid;
+        if (i < total / 4) o4[i] = make_float4(fin(v[u].x), fin(v[u].y), fin(v[u].z), fin(v[u].w));
+      }
+    }
+  } else {
+    for (int i = tid; i < total; i += LF_THREADS) o[i] = fin(o[i]);
   }
 #ifdef LF_PROFILE
-  LF_T(7);
   if (chunk < 4096) lf_prof_buf[((size_t)chunk * LF_WAVES + w) * 8 + (lane & 7)] = lf_acc[lane & 7];
 #endif
 }
@@ -666,7 +678,7 @@ extern "C" int drsa_amd_logmel(const float* wav, int64_t n_songs, int64_t song_s
     a.o_bw = take(band_nnz);
     a.o_samp = take(fast ? 0 : (LM_WAVES - 1) * hop + n_fft);
     a.o_fft = take(fast ? LF_WAVES * LF_WB : LM_WAVES * 4 * M);
-    a.o_mel = take(fast ? n_mels * (width + 1) : n_mels * width);
+    a.o_mel = take(fast ? 0 : n_mels * width);
     a.o_bwt = take(fast ? LF_NBT * (n_mels + 1) : 0);
     a.o_red = take(fast ? LF_WAVES : LM_WAVES);
     a.smem_floats = off;

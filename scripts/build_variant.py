@@ -15,7 +15,8 @@ def main(name, src, *defs):
     B.build(verbose=False)
     exp = os.path.join(B.LIBDIR, "exp")
     os.makedirs(exp, exist_ok=True)
-    srcp = os.path.join(B.CSRC, src)
+    srcp = src if os.path.isabs(src) else os.path.join(B.CSRC, src)   # an absolute path replaces its namesake
+    src = os.path.basename(src)
     obj = os.path.join(exp, f"{name}_{src.replace('.hip', '.o')}")
     subprocess.run([B._hipcc(), *B.CXXFLAGS, *defs, "-c", srcp, "-o", obj], check=True)
     objs = [os.path.join(B.OBJDIR, f.replace(".hip", ".o")) for f in sorted(os.listdir(B.CSRC)) if f.endswith(".hip")

@@ -22,11 +22,12 @@ for _ in range(3):
     ld.load_songs(songs)
 torch.cuda.synchronize()
 lib = _capi.load()
-n = 512 * 12 * 8
+WAVES = int(os.environ.get("LF_WAVES", "8"))
+n = 512 * WAVES * 8
 buf = np.zeros(n, dtype=np.uint64)
 assert lib.drsa_amd_logmel_prof(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(n)) == 0
-c = buf.reshape(512, 12, 8).astype(np.float64)
-names = ["init", "load+window", "dftA+twiddle", "transpose", "dftB", "split+|X|", "mel", "epilogue"]
+c = buf.reshape(512, WAVES, 8).astype(np.float64)
+names = ["init", "load+window", "dftA+twiddle", "transpose", "dftB", "split+|X|", "mel", "log pass"]
 tot = c.sum(axis=2).mean()
 print(json.dumps({"cycles_per_wave_mean": {k: float(v) for k, v in zip(names, c.mean(axis=(0, 1)))},
                   "total_cycles_per_block": float(tot)}, indent=1))
