@@ -300,7 +300,8 @@ constexpr int LF_M = 400, LF_R = 20, LF_FPW = 3, LF_WAVES = 8, LF_THREADS = LF_W
 constexpr int LF_FPR = LF_WAVES * LF_FPW;   // frames per round
 constexpr int LF_RS = 21;          // transpose row stride: 21 * q distinct mod 32 for q < 20
 constexpr int LF_FS = 420;         // frame slab (== 4 mod 32: the three frames' pass-B reads are conflict-free)
-constexpr int LF_WB = LF_FPW * LF_FS;
+// per-wave LDS: the 3 frames' slabs + a scratch slab for lanes 60-63 (LF_FPW + 1 slabs)
+constexpr int LF_WB = (LF_FPW + 1) * LF_FS;
 constexpr int LF_NBT = 16;         // band positions held transposed (wider bands read the rest from bw)
 // magnitude row of frame f at slab offset LF_MOFF(f) (0, 11, 5): with the transposed weights and the
 // padded mel tile, the mel stage's LDS accesses run at ~1.6 cycles per group instead of ~3
@@ -416,9 +417,11 @@ __global__ __launch_bounds__(LF_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
   float* o = a.out + (size_t)chunk * a.n_mels * a.width;
   LF_T(0);
 
-  // frame slot in the wave and n2 (pass A) / k1 (pass B); lanes 60-63 duplicate lanes 0-3 (same
-  // loads, same values, same LDS addresses), so no stage needs an active-lane branch
-  const int fl = lane < LF_FPW * LF_R ? lane / LF_R : 0, q = lane < LF_FPW * LF_R ? lane % LF_R : lane - LF_FPW * LF_R;
+  // frame slot in the wave and n2 (pass A) / k1 (pass B).
+  // lanes 60-63 run a 4th frame slot (q = 0-3) through their own scratch slab: no active-lane
+  // branches, and at slab offset 3 * 420 = 12 (mod 32) their transpose reads share no bank with
+  // frames 1 and 2 (as duplicates of lanes 0-3 they conflicted with lanes 32-35 on every read)
+  const int fl = lane / LF_R, q = lane % LF_R;
   const int partner = fl * LF_R + (q == 0 ? 0 : LF_R - q);
   // float2 sample loads when every frame start is 8-byte aligned (even hop and an aligned chunk)
   const bool vec_ok = (a.hop & 1) == 0 && ((((uintptr_t)x) & 7) == 0);
