@@ -117,3 +117,17 @@ def test_feeds_the_explainer_end_to_end():
     hg.generate_subspace_heatmaps(x)
     assert hg.info["subspace_heatmaps"].shape == (8, 4, 128, 128)
     assert np.isfinite(hg.info["subspace_relevances"]).all()
+
+
+@pytest.mark.parametrize("n_mels,width,hop", [(41, 61, 361), (20, 50, 360)])
+def test_n_fft_800_kernel_odd_shapes(n_mels, width, hop):
+    """The n_fft = 800 kernel off the GTZAN shape: an odd hop (scalar sample loads), a mel x width
+    tile that is not a multiple of 4 (scalar in-place log pass), a partial last round, and (20
+    mels) bands wider than the 16 transposed weight rows (the band-table tail)."""
+    ld = _loader(None, sample_rate=16000, n_fft=800, hop_length=hop, n_mels=n_mels, slice_length=0, width=width)
+    rng = np.random.default_rng(n_mels)
+    wav = rng.uniform(-1, 1, (3, 24000 + 7)).astype(np.float32)
+    out = ld.transform_wav(torch.from_numpy(wav).to(DEV), clamp=False).cpu().numpy()
+    mel = L.mel_spectrogram(wav.astype(np.float64), 800, hop, n_mels, 16000)
+    ref = np.log10(mel + 1e-7)[..., 1:width + 1].reshape(3, 1, n_mels, width)
+    assert np.abs(out - ref).max() <= TOL_LOG
