@@ -9,4 +9,4 @@ for r in 1 2; do
   timeout -k 10 100 python $S > $O/base_$r.json
   for n in "$@"; do DRSA_AMD_LIB=drsa_audio_amd/lib/exp/$n.so timeout -k 10 100 python $S > $O/${n}_$r.json; done
 done
-for f in $O/*.json; do echo "$f $(python -c "import json,sys; print(json.load(open('$f'))['ms_per_launch'])")"; done
+for f in $O/*.json; do echo "$f $(python -c "import json,sys; d=json.load(open('$f')); print(d.get('ms_per_launch', d.get('ms')))")"; done
