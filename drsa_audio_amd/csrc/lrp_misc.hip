@@ -262,18 +262,47 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
       for (int ks = 0; ks < DP / 4; ++ks) preg[jb * (DP / 4) + ks] = Pm[(ks * 4 + (lane >> 4)) * DP + jb * 16 + (lane & 15)];
   }
   static_assert(P / 16 == 4, "one 16-pixel block per wave");
-  for (int t = 0; t < PT; ++t) {
-    const int tile = blockIdx.x * PT + t;
-    if (tile >= (H / RPT) * xt) break;
+  // the a tile goes HBM -> registers one tile ahead (issued before the current tile's GEMMs),
+  // then registers -> LDS at the top of its own iteration
+  // (DP <= 64; at DP = 128 the 32 registers would cost a wave per SIMD)
+  constexpr bool PFT = DP <= 64;
+  constexpr int NPF = PFT ? DP * P / 256 : 1;
+  const int ntiles = (H / RPT) * xt;
+  float pf[NPF];
+  auto fetch_tile = [&](int tile) {
     const int y0 = (tile / xt) * RPT, x0 = (tile % xt) * TW;
-    __syncthreads();
-    for (int i = tid; i < DP * P; i += 256) {
-      const int c = i / P, p = i % P;
+#pragma unroll
+    for (int u = 0; u < (PFT ? NPF : 0); ++u) {
+      const int i = tid + 256 * u, c = i / P, p = i % P;
       const bool ok = c < d;
       const float v = a[((size_t)b * d + (ok ? c : 0)) * HW + (y0 + p / TW) * W + x0 + p % TW];
-      as[c * PL + p] = ok ? v : 0.f;
+      pf[u] = ok ? v : 0.f;
+    }
+  };
+  if constexpr (PFT)
+    if (blockIdx.x * PT < ntiles) fetch_tile(blockIdx.x * PT);
+  for (int t = 0; t < PT; ++t) {
+    const int tile = blockIdx.x * PT + t;
+    if (tile >= ntiles) break;
+    const int y0 = (tile / xt) * RPT, x0 = (tile % xt) * TW;
+    __syncthreads();
+    if constexpr (PFT) {
+#pragma unroll
+      for (int u = 0; u < NPF; ++u) {
+        const int i = tid + 256 * u;
+        as[(i / P) * PL + i % P] = pf[u];
+      }
+    } else {
+      for (int i = tid; i < DP * P; i += 256) {
+        const int c = i / P, p = i % P;
+        const bool ok = c < d;
+        const float v = a[((size_t)b * d + (ok ? c : 0)) * HW + (y0 + p / TW) * W + x0 + p % TW];
+        as[c * PL + p] = ok ? v : 0.f;
+      }
     }
     __syncthreads();
+    if constexpr (PFT)
+      if (t + 1 < PT && tile + 1 < ntiles) fetch_tile(tile + 1);
     // h[j][p] = sum_c U[c][j] a[c][p] and delta[c][p] = sum_k P[c][k] a[k][p]: wave w owns pixel
     // block w and runs the 2 NB output blocks as independent MFMA chains sharing the B operand read
     // (per element the single-chain k order); then a' = a + delta (= h U^T, residual form above)

@@ -6,4 +6,4 @@ O=gpurun_out/$1; shift
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_lrp_gpu.py tests/test_engine_gpu.py tests/test_logmel_gpu.py -x -q --timeout 120 --timeout-method thread > $O/t.log 2>&1 || { tail -30 $O/t.log; exit 1; }
 tail -2 $O/t.log
-bash scripts/ab_lib.sh $(basename $O)_ab scripts/bench_first_layer.py "$@"
+bash scripts/ab_lib.sh $(basename $O)_ab ${AB_SCRIPT:-scripts/bench_first_layer.py} "$@"
