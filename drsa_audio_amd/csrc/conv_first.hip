@@ -53,6 +53,12 @@ __global__ __launch_bounds__(kThreads) void first_conv_pool_kernel(ConvArgs a, i
   // blockIdx.y: channel slice (more waves in flight for the store stream)
   const int cper = (a.cout + gridDim.y - 1) / gridDim.y;
   const int c_lo = blockIdx.y * cper, c_hi = min(a.cout, c_lo + cper);
+#ifndef DRSA_FIRST_FWD_CUNROLL
+#define DRSA_FIRST_FWD_CUNROLL 4
+#endif
+  // unrolled over channels: the next channels' weight / bias scalar loads issue ahead of this
+  // channel's fma chains instead of one load latency per channel
+#pragma unroll DRSA_FIRST_FWD_CUNROLL
   for (int co = c_lo; co < c_hi; ++co) {
     float w[NG][9];
 #pragma unroll
