@@ -10,19 +10,18 @@
 // ---------------------------------------------------------------------------
 namespace drsa_conv {
 extern const Table kTableFwdA, kTableFwdB, kTableFwdC, kTableFwdD, kTableFwdE, kTableBwdA, kTableBwdB, kTableBwdC,
-    kTableBwdcA, kTableBwdcB, kTableFwdBfA, kTableFwdBfB, kTableFwdBfC, kTableFwdP4, kTableBwdBfA, kTableBwdBfB;
+    kTableFwdBfA, kTableFwdBfB, kTableFwdBfC, kTableFwdP4, kTableBwdBfA, kTableBwdBfB;
 }
 
 namespace {
 using drsa_conv::Entry;
 using namespace drsa_conv;
 
-const drsa_conv::Table* kTables[] = {&drsa_conv::kTableFwdA, &drsa_conv::kTableFwdB, &drsa_conv::kTableFwdC,
-                                     &drsa_conv::kTableFwdD, &drsa_conv::kTableFwdE, &drsa_conv::kTableBwdA,
-                                     &drsa_conv::kTableBwdB, &drsa_conv::kTableBwdC, &drsa_conv::kTableBwdcA,
-                                     &drsa_conv::kTableBwdcB, &drsa_conv::kTableFwdBfA, &drsa_conv::kTableFwdBfB,
-                                     &drsa_conv::kTableFwdBfC, &drsa_conv::kTableFwdP4, &drsa_conv::kTableBwdBfA,
-                                     &drsa_conv::kTableBwdBfB};
+const drsa_conv::Table* kTables[] = {&drsa_conv::kTableFwdA,  &drsa_conv::kTableFwdB,   &drsa_conv::kTableFwdC,
+                                     &drsa_conv::kTableFwdD,  &drsa_conv::kTableFwdE,   &drsa_conv::kTableBwdA,
+                                     &drsa_conv::kTableBwdB,  &drsa_conv::kTableBwdC,   &drsa_conv::kTableFwdBfA,
+                                     &drsa_conv::kTableFwdBfB, &drsa_conv::kTableFwdBfC, &drsa_conv::kTableFwdP4,
+                                     &drsa_conv::kTableBwdBfA, &drsa_conv::kTableBwdBfB};
 
 int pad32(int c) { return (c + 31) / 32 * 32; }
 
@@ -34,7 +33,7 @@ int env_int(const char* name, int dflt) {
 const Entry* find(int cin_p, int cout_p, int W, int ng, int amode, int epi, int et = 0, int pw = 2) {
   int th = 8, tw, mw;
   static const int th16 = env_int("DRSA_AMD_CONV_TH16", 0);
-  if (W >= 32) { tw = 32; mw = 8; th = (th16 && cout_p == 32 && ng <= 2 && epi != EPI_BWDC) ? 16 : 8; }
+  if (W >= 32) { tw = 32; mw = 8; th = (th16 && cout_p == 32 && ng <= 2) ? 16 : 8; }
   else if (W > 8) { tw = 16; mw = 8; }
   else { tw = 8; mw = 4; }
   for (const drsa_conv::Table* t : kTables)
@@ -142,15 +141,6 @@ int drsa_amd_conv_bwd(const float* g, const uint8_t* g_amax, const float* wts, c
   a.cin = cin; a.cout = cout; a.clones = clones; a.xmode = xmode; a.post = post; a.eps = eps;
   static const int dbg = env_int("DRSA_AMD_CONV_DBG", 0);
   a.dbg = dbg;
-  // DRSA_AMD_CONV_CLONES=1: one workgroup per (tile, sample) looping over the K+1 clones
-  // (lrp_conv_clones.h).  Bit-identical, reads x/den once per tile, but measured slower on the
-  // GTZAN features.3 shape (2.12 vs 1.92 ms: 2 waves/SIMD at its register footprint cannot hide
-  // the per-chunk staging latency), so the per-clone kernel is the default.  Read per call.
-  const int use_clones = env_int("DRSA_AMD_CONV_CLONES", 0);
-  if (clones > 1 && use_clones) {
-    const Entry* ec = find(cin_p, cout_p, W, ng, g_amax ? A_POOLSPARSE : A_DENSE, EPI_BWDC);
-    if (ec) return launch(ec, a, Bq / clones, (hipStream_t)stream);
-  }
   const Entry* e = find(cin_p, cout_p, W, ng, g_amax ? A_POOLSPARSE : A_DENSE, EPI_BWD);
   if (!e) {
     drsa::set_error("conv_bwd: no kernel for cin=%d cout=%d W=%d ng=%d sparse=%d", cin, cout, W, ng, g_amax != nullptr);

@@ -43,9 +43,6 @@
 #ifndef DRSA_CONV_PRE_N
 #define DRSA_CONV_PRE_N 64
 #endif
-#ifndef DRSA_CONV_BWDC_WPE
-#define DRSA_CONV_BWDC_WPE 2
-#endif
 #ifndef DRSA_CONV_BF_WPE
 #define DRSA_CONV_BF_WPE 2
 #endif
@@ -74,8 +71,7 @@ constexpr int halo_stride(int hx, int mw) {
 }
 
 enum AMode { A_DENSE = 0, A_POOLSPARSE = 1 };
-// EPI_BWDC: backward with all clones of a sample in one workgroup (lrp_conv_clones.h)
-enum Epi { EPI_FWD_POOL = 0, EPI_FWD_RELU = 1, EPI_BWD = 2, EPI_BWDC = 3 };
+enum Epi { EPI_FWD_POOL = 0, EPI_FWD_RELU = 1, EPI_BWD = 2 };
 
 // halo column c (pixel tx0 - 1 + c) lives at LDS column c + XO, so the tile interior starts
 // 16-byte aligned (float4 staging stores) and pool cells cover aligned float2 pairs.
@@ -107,9 +103,8 @@ struct ConvCfg {
   static constexpr int PLANE_RAW = HY * RS;
   static constexpr int PLANE = PLANE_RAW + ((PLANE_RAW % 32) == 0 ? 4 : 0);
   // M-tile = the 32 pixels of one MFMA B operand: window-major 2x2 pool windows (MTH = 16/MW rows
-  // x 2*MW), or for EPI_BWDC row-major MTH x MTW with MTW = min(TW, 32), so that register r of
-  // the accumulator holds 32 consecutive pixels of a row (epilogue straight to global memory)
-  static constexpr int MTW = EPI == EPI_BWDC ? (TW < 32 ? TW : 32) : 2 * MW;
+  // x 2*MW)
+  static constexpr int MTW = 2 * MW;
   static constexpr int MTH = 32 / MTW;
   static constexpr int MTX = TW / MTW;     // M-tiles per tile row
   static constexpr int MT = (TH / MTH) * MTX;
@@ -132,10 +127,10 @@ struct ConvCfg {
       BF ? bf_halo_floats + bf_w_floats : (size_t)CIC * PLANE + (size_t)NG * KCP * COUT;
   static constexpr size_t epi_floats = (size_t)TCH * TH * TWP;
   static constexpr size_t lds_floats =
-      (EPI == EPI_BWDC || staging_floats > epi_floats) ? staging_floats : epi_floats;
+      staging_floats > epi_floats ? staging_floats : epi_floats;
   // minimum waves per SIMD the register allocation must allow (1 block = 1 wave per SIMD)
   static constexpr int WPE = BF ? (COUT <= 64 ? DRSA_CONV_BF_WPE : 1)
-                             : EPI == EPI_BWDC ? DRSA_CONV_BWDC_WPE : (EPI == EPI_BWD && NG == 1) ? (SMALL_BWD ? 4 : DRSA_CONV_BWD_WPE)
+                             : (EPI == EPI_BWD && NG == 1) ? (SMALL_BWD ? 4 : DRSA_CONV_BWD_WPE)
                              : (EPI != EPI_BWD && CIC <= 8 && COUT <= 32 && NG <= 2 ? DRSA_CONV_FWD_WPE : 1);
   // operand prefetch distance of the MFMA loop (k-steps)
   static constexpr int PD = DRSA_CONV_PD_BWD > 0 && EPI >= EPI_BWD ? DRSA_CONV_PD_BWD : 1;

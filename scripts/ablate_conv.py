@@ -29,11 +29,10 @@ print(json.dumps({"ms": ms, "tflops": 2 * 37748736 * Bq / ms / 1e9}))
 if __name__ == "__main__":
     res = {}
     for th16 in os.environ.get("ABL_TH16", "0,1").split(","):
-      for cl in os.environ.get("ABL_CLONES", "1").split(","):
         for dbg in os.environ.get("ABL_DBG", "0,1,2,3,4,5,6,7").split(","):
-            env = dict(os.environ, DRSA_AMD_CONV_DBG=dbg, DRSA_AMD_CONV_TH16=th16, DRSA_AMD_CONV_CLONES=cl)
+            env = dict(os.environ, DRSA_AMD_CONV_DBG=dbg, DRSA_AMD_CONV_TH16=th16)
             r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
             line = [l for l in r.stdout.splitlines() if l.startswith("{")]
-            key = f"th16={th16} clones={cl} dbg={dbg}"
+            key = f"th16={th16} dbg={dbg}"
             res[key] = json.loads(line[0]) if line else r.stderr[-300:]
             print(key, res[key], flush=True)
