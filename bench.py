@@ -424,6 +424,17 @@ def drsa_sharded_bench(device, world, rank, steps=100):
     out = {"config": f"row-sharded DRSA: {n} rows/rank x {world} ranks, d={d}, K={K}, all-reduce {d*d+K} fp32/step",
            "ms_per_step": dt / steps * 1e3, "vector_steps_per_s": n * world * steps / dt, "steps": steps,
            "objective_final": float(traj[-1])}
+    if rank == 0:
+        # self-check (outside the timed region): every rank's seeded rows regenerated here, the
+        # unsharded single-process run on their concatenation, max relative trajectory deviation
+        from drsa_audio_amd.xai.drsa.drsa import drsa_run
+        Aa, Ca = (torch.from_numpy(np.concatenate(v)).to(device)
+                  for v in zip(*(drsa_inputs(n, d, 100 + r) for r in range(world))))
+        _, tr1 = drsa_run(Aa, Ca, Ug, K, steps)
+        tr1 = tr1.cpu().numpy().astype(np.float64)
+        out["traj_dev_vs_unsharded"] = float(np.max(np.abs(np.asarray(traj, np.float64) - tr1) / np.abs(tr1)))
+        del Aa, Ca
+    dist.barrier()
     # C5 on N GPUs: the two VGGish layers (j = 26, 33; d = 128, K = 16) row-sharded, one packed
     # all-reduce of both partials per step (distributed.py::sharded_run_joint)
     from drsa_audio_amd.xai.drsa.distributed import sharded_run_joint
@@ -448,6 +459,18 @@ def drsa_sharded_bench(device, world, rank, steps=100):
                                  f"K={K5}, one all-reduce of 2 x {d5 * d5 + K5} fp32/step",
                        "ms_per_joint_step": dt5 / s5 * 1e3, "steps": s5,
                        "objective_final": [float(tr[-1]) for _, tr in res]}
+    if rank == 0:
+        from drsa_audio_amd.xai.drsa.drsa import drsa_run
+        devs = []
+        for p_ in range(2):
+            Aa, Ca = (torch.from_numpy(np.concatenate(v)).to(device)
+                      for v in zip(*(drsa_inputs(n, d5, 200 + 10 * r + p_) for r in range(world))))
+            _, tr1 = drsa_run(Aa, Ca, probs[p_][2], K5, s5)
+            tr1 = tr1.cpu().numpy().astype(np.float64)
+            devs.append(float(np.max(np.abs(np.asarray(res[p_][1], np.float64) - tr1) / np.abs(tr1))))
+            del Aa, Ca
+        out["c5_joint"]["traj_dev_vs_unsharded"] = max(devs)
+    dist.barrier()
     return out
 
 
@@ -503,7 +526,7 @@ def drsa_grid_bench(device, world, rank, steps=100, N=20000, classes=None):
 
 
 # --------------------------------------------------------------------------- main
-LEGS = ("c2", "drsa", "frontend", "joint", "vggish", "sharded", "grid", "to_host")
+LEGS = ("c2", "drsa", "frontend", "joint", "vggish", "sharded", "grid", "to_host", "clone")
 
 
 def main():
@@ -545,7 +568,11 @@ def main():
 
     B, K = args.batch, 4
     model = gtzan128().to(device)
-    hg = HeatmapGenerator(model, load_u(), LRP_NAME_MAP_GTZAN, "blues", num_concepts=K, layer_idx=7, device=device)
+    # headline: the standard heatmap as the sum of the K concept heatmaps (exact reformulation, every
+    # rule is linear in R; gated bit-exact vs the oracle in both modes); the reference's clone-0
+    # form (HeatmapGenerator's default) is timed beside it in secondary.clone_mode
+    hg = HeatmapGenerator(model, load_u(), LRP_NAME_MAP_GTZAN, "blues", num_concepts=K, layer_idx=7, device=device,
+                          standard="sum")
     x = synthetic_logmel(B, seed=1 + rank, device=device)
 
     log(f"[bench] rank {rank}/{world}: headline B={B}, {args.warmup} warm-up + {args.steps} timed steps")
@@ -598,13 +625,16 @@ def main():
             kernels[tag]["tflops"] = 2.0 * m / (avg * 1e-3) / 1e12
     dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
     dom_ach = kernels[dom].get("tflops", 0.0)
-    traffic = None
+    traffic = traffic_src = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         try:
             with open(pmc_path) as fh:
                 pm = json.load(fh)
             traffic = pm.get("per_launch_bytes", {}).get(dom)
+            # PMC counters cannot be read inside this process: the bytes come from the committed
+            # rocprofv3 --pmc passes (scripts/pmc_run.sh) of the same kernel, named here
+            traffic_src = f"profiles/pmc_traffic.json ({pm.get('profile', 'unlabelled')}), not measured in this run"
         except Exception:
             traffic = None
     total_macs = sum(macs.values())
@@ -651,6 +681,25 @@ def main():
         from drsa_audio_amd.xai.drsa.cluster.optsubspaces import GTZAN_CLASSES
         grid = drsa_grid_bench(device, world, rank, steps=args.grid_steps,
                                classes=GTZAN_CLASSES[:max(1, args.grid_classes)])
+    # the reference's clone-0 standard heatmap (K+1 clones below the projection, explainer.py:92)
+    clone_mode = None
+    if rank == 0 and "clone" in legs:
+        log("[bench] clone-mode rate")
+        hgc = HeatmapGenerator(model, load_u(), LRP_NAME_MAP_GTZAN, "blues", num_concepts=K, layer_idx=7,
+                               device=device, standard="clone")
+        for _ in range(2):
+            hgc.generate_subspace_heatmaps(x, to_host=False)
+        torch.cuda.synchronize(device)
+        t1 = time.perf_counter()
+        nc = 10
+        for _ in range(nc):
+            hgc.generate_subspace_heatmaps(x, to_host=False)
+        torch.cuda.synchronize(device)
+        tc = (time.perf_counter() - t1) / nc
+        clone_mode = {"explained_samples_per_s": B / tc, "ms_per_step": tc * 1e3,
+                      "note": "HeatmapGenerator(standard='clone') (the default): the standard heatmap is clone 0 "
+                              "of K+1 relevance clones, as the reference's replicated batch (explainer.py:92)"}
+        del hgc
     # the reference API returns numpy (explainer.py:111): the same steps with the D2H copy of info
     to_host = None
     if rank == 0 and "to_host" in legs:
@@ -696,13 +745,17 @@ def main():
                     "torch.manual_seed(0); U = ortho_group.rvs(64) seed 42)",
             "config": {"workload": "GTZAN-128 HeatmapGenerator: LRP (WSquare/Gamma/Epsilon name map) + DRSA "
                                    "subspace heatmaps, K=4 at layer j=7 (conv3 block, d=64), sorted info dict",
+                       "standard_heatmap": "sum of the K concept heatmaps (standard='sum'; exact reformulation, "
+                                           "bit-exact vs the oracle); the reference's clone-0 form: "
+                                           "secondary.clone_mode; with the numpy info D2H: secondary.to_host",
                        "global_batch": B * world, "per_gpu_batch": B, "input": "128x128 log-mel",
                        "parallelism": f"data-parallel x{world} (no collective on the data path)",
                        "launch": ("torchrun" if os.environ.get("TORCHELASTIC_RUN_ID") else
                                   "bench.py --gpus (own launcher)" if world > 1 else "single process"),
                        "one_device_rehearsal": one_dev, "backend": backend if world > 1 else None},
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": dom_ach, "peak": FP32_MFMA_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": dom_ach / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic},
+                         "unit": "TFLOP/s", "frac": dom_ach / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic,
+                         "traffic_source": traffic_src},
             "whole_path": {"algorithmic_gflop_per_sample": 2.0 * total_macs / B / 1e9,
                            "achieved_tflops": 2.0 * total_macs * value / B / world / 1e12},
             "kernels": kernels,
@@ -710,6 +763,7 @@ def main():
                           "explained_samples_per_s_bs64": bs64 and bs64 * world, "drsa": drsa,
                           "drsa_sharded": drsa_sharded, "drsa_joint_c5": joint, "vggish_lrp": vgg,
                           "drsa_grid_task_parallel": grid, "logmel_frontend": frontend, "to_host": to_host,
+                          "clone_mode": clone_mode,
                           "cpu_baseline_drsa_c3": cpu_drsa},
             "cpu_baseline": cpu,
         }

@@ -71,6 +71,8 @@ SIGNATURES = {
                                      _vp]),
     "drsa_amd_normalize_workspace_bytes": (_sz, []),
     "drsa_amd_normalize_vectors": (_i32, [_fp, _i64, _i32, _fp, _vp, _sz, _vp]),
+    "drsa_amd_normalize_sumsq": (_i32, [_fp, _i64, _vp, _sz, _fp, _vp]),
+    "drsa_amd_normalize_scale": (_i32, [_fp, _i64, _i32, _fp, _i32, _i64, _fp, _vp]),
     "drsa_amd_logmel_smem_bytes": (_i32, [_i32, _i32, _i32, _i32, _i32]),
     "drsa_amd_logmel": (_i32, [_fp, _i64, _i64, _i32, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _fp, _ip, _ip, _ip,
                                _fp, _i32, _i32, _i32, _f32, _f32, _fp, _vp]),

@@ -121,14 +121,36 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ v,
   if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// the block partials re-reduced in a fixed order (wave 0: stride-64 chains, then a shuffle tree)
+__device__ double reduce_parts(const double* __restrict__ part, int nblk) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nblk; i += 64) s += part[i];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  return s;
+}
+
+// one fp64 sum of squares per call (the sharded normalisation's local term)
+__global__ __launch_bounds__(64) void sumsq_finish_kernel(const double* __restrict__ part, int nblk,
+                                                          double* __restrict__ sum_out) {
+  const double s = reduce_parts(part, nblk);
+  if (threadIdx.x == 0) sum_out[0] = s;
+}
+
+// E = sqrt((sums[0] + sums[1] + ... in rank order) / n_total); the scale over this call's elements.
+// nsums == 0: the sum is this call's own block partials (single-process normalize_vectors).
 __global__ __launch_bounds__(256) void scale_kernel(const float* __restrict__ v, int64_t n, float d4, int nblk,
-                                                    const double* __restrict__ part, float* __restrict__ out) {
+                                                    const double* __restrict__ part, const double* __restrict__ sums,
+                                                    int nsums, double n_total, float* __restrict__ out) {
   __shared__ float sc;
-  if (threadIdx.x < 64) {           // wave 0 re-reduces the partials in a fixed order
-    double s = 0.0;
-    for (int i = threadIdx.x; i < nblk; i += 64) s += part[i];
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    if (threadIdx.x == 0) sc = (float)sqrt(s / (double)n);
+  if (threadIdx.x < 64) {
+    double s;
+    if (nsums == 0) {
+      s = reduce_parts(part, nblk);
+    } else {
+      s = 0.0;
+      for (int r = 0; r < nsums; ++r) s += sums[r];
+    }
+    if (threadIdx.x == 0) sc = (float)sqrt(s / n_total);
   }
   __syncthreads();
   const float E = sc;
@@ -205,7 +227,39 @@ extern "C" int drsa_amd_normalize_vectors(const float* v, int64_t n, int d, floa
   hipLaunchKernelGGL(sumsq_kernel, dim3(nblk), dim3(256), 0, (hipStream_t)stream, v, n, (double*)ws);
   DRSA_LAUNCH_CHECK();
   hipLaunchKernelGGL(scale_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, v, n, d4, nblk,
-                     (const double*)ws, out);
+                     (const double*)ws, (const double*)nullptr, 0, (double)n, out);
+  DRSA_LAUNCH_CHECK();
+  return DRSA_OK;
+}
+
+extern "C" int drsa_amd_normalize_sumsq(const float* v, int64_t n, void* ws, size_t ws_bytes, double* sum_out,
+                                        void* stream) {
+  DRSA_REQUIRE(ws && sum_out, "normalize_sumsq: null pointer");
+  DRSA_REQUIRE(n >= 0 && (n == 0 || v), "normalize_sumsq: bad input");
+  DRSA_REQUIRE(ws_bytes >= NV_BLOCKS * sizeof(double), "normalize_sumsq: workspace too small");
+  if (n == 0) {                     // a rank without rows contributes 0
+    DRSA_HIP(hipMemsetAsync(sum_out, 0, sizeof(double), (hipStream_t)stream));
+    return DRSA_OK;
+  }
+  const int64_t nb = (n + 255) / 256;
+  const int nblk = (int)(nb < NV_BLOCKS ? nb : NV_BLOCKS);
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nblk), dim3(256), 0, (hipStream_t)stream, v, n, (double*)ws);
+  DRSA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(sumsq_finish_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (const double*)ws, nblk,
+                     sum_out);
+  DRSA_LAUNCH_CHECK();
+  return DRSA_OK;
+}
+
+extern "C" int drsa_amd_normalize_scale(const float* v, int64_t n, int d, const double* sums, int nsums,
+                                        int64_t n_total, float* out, void* stream) {
+  DRSA_REQUIRE(sums && nsums >= 1, "normalize_scale: needs >= 1 partial sum");
+  DRSA_REQUIRE(n >= 0 && d > 0 && n_total > 0 && n <= n_total, "normalize_scale: bad sizes");
+  DRSA_REQUIRE(n == 0 || (v && out), "normalize_scale: null pointer");
+  if (n == 0) return DRSA_OK;
+  const float d4 = (float)pow((double)d, 0.25);
+  hipLaunchKernelGGL(scale_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, v, n, d4, 0,
+                     (const double*)nullptr, sums, nsums, (double)n_total, out);
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;
 }

@@ -15,6 +15,8 @@ import os
 import weakref
 from collections import OrderedDict
 
+import torch
+
 from .hooks import HookedAutograd, has_custom_hooks
 from .plan import EngineError, LRPEngine, bf16_backward_default
 
@@ -32,9 +34,18 @@ class _Entry:
 
 def _fingerprint(model):
     """Parameters AND buffers: the plan folds BatchNorm running statistics into the weights, so a
-    train-mode forward or a buffers-only load_state_dict must recompile."""
+    train-mode forward or a buffers-only load_state_dict must recompile.  Also the DRSA projection
+    matrices, which are plain tensor attributes (``Projection.U``, ``InvProjection.U_inv``,
+    ``ProjectionModel.U``; cxai/model/modify_model.py:4-123): the plan caches U and P = UU^T - I, so
+    an in-place update (``_version``) or a rebinding (``data_ptr``) of U must recompile too."""
+    proj = []
+    for m in model.modules():
+        for attr in ("U", "U_inv"):
+            t = getattr(m, attr, None)
+            if isinstance(t, torch.Tensor):
+                proj.append((attr, t.data_ptr(), t._version))
     return (tuple((p.data_ptr(), p._version) for p in model.parameters()) +
-            tuple((b.data_ptr(), b._version) for b in model.buffers()))
+            tuple((b.data_ptr(), b._version) for b in model.buffers()) + tuple(proj))
 
 
 def _ref(obj):

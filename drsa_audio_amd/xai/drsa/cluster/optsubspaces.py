@@ -88,7 +88,11 @@ def hip_runner(problems, steps: int):
     fp32 = all(A.dtype == torch.float32 for A, _, _, _ in problems)
     with torch.cuda.stream(side):
         if len(geoms) == 1 and fp32:
-            out = drsa_run_batched(problems, steps)
+            # one partial workgroup per CU for every problem: the row partition (and so the fp32
+            # summation order) is drsa_run's, independent of how many tasks share the launch, the
+            # world size or the LPT plan -- grid results equal drsa.main's bit for bit
+            cu = torch.cuda.get_device_properties(dev).multi_processor_count
+            out = drsa_run_batched(problems, steps, blocks=cu)
         else:
             out = drsa_run_joint(problems, steps)
     torch.cuda.current_stream(dev).wait_stream(side)
@@ -179,6 +183,10 @@ def main(conf: int = 1, path_to_data: str = "/input-data", path_to_models: str =
     data = {}
     for c in classes:
         for l in layers:
-            data[(c, l)] = load_and_normalize_data(
+            # normalised on the GPU, then kept on the host: optimize_grid moves only this rank's
+            # tasks' datasets to the device
+            a, cv = load_and_normalize_data(
                 os.path.join(path_to_data, sub.format(c=c), f"dataset_layer{l}.pkl"), device=device)
+            data[(c, l)] = (a.cpu(), cv.cpu())
+            del a, cv
     return optimize_grid(data, path_to_models, num_concepts=K, steps=steps, runs=3, seed=42, device=device)

@@ -94,29 +94,41 @@ STATS = {"graph_replays": 0, "capture_failures": 0}
 
 def _graph_ok(group, backends) -> bool:
     """Capture the step loop (kernels + the RCCL all-reduce) in a graph: RCCL process group, HIP
-    backends, and DRSA_AMD_SHARDED_GRAPH not 0."""
-    if os.environ.get("DRSA_AMD_SHARDED_GRAPH", "1") == "0" or not dist.is_initialized():
+    backends and DRSA_AMD_SHARDED_GRAPH.  Default ("auto"): only at world size 1 -- a captured
+    multi-rank RCCL all-reduce has not yet been checked against the eager loop on two GPUs;
+    DRSA_AMD_SHARDED_GRAPH=1 enables it at any world size, 0 disables it."""
+    mode = os.environ.get("DRSA_AMD_SHARDED_GRAPH", "auto")
+    if mode == "0" or not dist.is_initialized():
         return False
     if not all(isinstance(b, HipBackend) for b in backends):
         return False
     try:
-        return dist.get_backend(group) == "nccl"
+        if dist.get_backend(group) != "nccl":
+            return False
     except Exception:
         return False
+    return mode == "1" or dist.get_world_size(group) == 1
 
 
-def _capture(body) -> Optional["torch.cuda.CUDAGraph"]:
+def _capture(body, group=None) -> Optional["torch.cuda.CUDAGraph"]:
     """One captured replay of ``body`` (two steps: U ping-pongs back to its buffer), or None when
-    the capture is refused (then the loop runs eagerly, same kernels and the same bits)."""
+    the capture is refused (then the loop runs eagerly, same kernels and the same bits).  The
+    ranks agree first (MIN of a success flag over the group): either every rank replays the graph
+    or every rank runs eagerly."""
     g = torch.cuda.CUDAGraph()
+    ok = 1
     try:
         with torch.cuda.graph(g):
             body()
     except Exception:
         torch.cuda.synchronize()
         STATS["capture_failures"] += 1
-        return None
-    return g
+        ok = 0
+    if dist.is_initialized():
+        flag = torch.tensor([ok], dtype=torch.int32, device=torch.device("cuda", torch.cuda.current_device()))
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+        ok = int(flag.item())
+    return g if ok else None
 
 
 def sharded_run(A_local: torch.Tensor, C_local: torch.Tensor, U0: torch.Tensor, K: int, steps: int,
@@ -144,7 +156,7 @@ def sharded_run(A_local: torch.Tensor, C_local: torch.Tensor, U0: torch.Tensor, 
         t0 = 0
         if steps >= 4 and _graph_ok(group, [backend]):
             # the whole step (all-reduce + fused launch) replayed from one graph, two steps per replay
-            graph = _capture(lambda: (step(0), step(1)))
+            graph = _capture(lambda: (step(0), step(1)), group)
             if graph is not None:
                 for _ in range(steps // 2):
                     graph.replay()
@@ -223,7 +235,7 @@ def sharded_run_joint(problems, steps: int, group=None, backends=None):
 
         t0 = 0
         if steps >= 4 and _graph_ok(group, backends):
-            graph = _capture(lambda: (step(0), step(1)))
+            graph = _capture(lambda: (step(0), step(1)), group)
             if graph is not None:
                 for _ in range(steps // 2):
                     graph.replay()
@@ -268,21 +280,27 @@ def shard_rows(N: int, world: int, rank: int) -> slice:
 
 
 def main_sharded(activation_vecs: torch.Tensor, context_vecs: torch.Tensor, model_root: str,
-                 num_concepts: int = 4, steps: int = 2000, runs: int = 3, seed: int = 42) -> Optional[List[str]]:
+                 num_concepts: int = 4, steps: int = 2000, runs: int = 3, seed: int = 42,
+                 local_rows: bool = False, group=None) -> Optional[List[str]]:
     """drsa.main semantics (drsa.py:241-301) with the rows split over the process group; rank 0
-    writes ``run{r}/projection_matrix.pkl`` and ``run{r}/train_stats.csv``."""
+    writes ``run{r}/projection_matrix.pkl`` and ``run{r}/train_stats.csv``.
+
+    ``local_rows=False``: every rank passes the whole (A, C) and keeps its ``shard_rows`` range.
+    ``local_rows=True``: every rank passes only its own rows, e.g. from
+    ``preprocessing.drsa_training_data(..., group=...)`` (no rank ever holds the full set)."""
     import pickle
     from .drsa import initial_projections
-    world = dist.get_world_size() if dist.is_initialized() else 1
-    rank = dist.get_rank() if dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
     dev = torch.device("cuda", torch.cuda.current_device())
-    sl = shard_rows(activation_vecs.size(0), world, rank)
+    sl = slice(None) if local_rows else shard_rows(activation_vecs.size(0), world, rank)
     A = activation_vecs[sl].to(dev, torch.float32).contiguous()
     C = context_vecs[sl].to(dev, torch.float32).contiguous()
     d = A.size(1)
     paths = []
     for r, U in enumerate(initial_projections(d, runs, seed), start=1):
-        Uf, traj = sharded_run(A, C, torch.tensor(U, dtype=torch.float32, device=dev), num_concepts, steps)
+        Uf, traj = sharded_run(A, C, torch.tensor(U, dtype=torch.float32, device=dev), num_concepts, steps,
+                               group=group)
         if rank == 0:
             path = os.path.join(model_root, f"run{r}")
             os.makedirs(path, exist_ok=True)

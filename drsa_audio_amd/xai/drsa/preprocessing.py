@@ -108,19 +108,24 @@ def _vectors(cap: dict, idx: Optional[torch.Tensor], L: int, layout: int, A_out:
 def preprocess_data(model: nn.Module, input_batch, composite, layer_idx: int, class_idx: Optional[int],
                     num_locations: Optional[int] = None, one_hot_encoded: bool = False, device=None,
                     attr_batch_size: int = 1024, layout: int = LAYOUT_REFERENCE,
-                    num_classes: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+                    num_classes: Optional[int] = None, group=None) -> Tuple[torch.Tensor, torch.Tensor]:
     """(activation_vectors, context_vectors) at model.features[layer_idx].
 
     num_locations given: [B*L, d] rows at L sampled locations per sample (training data);
     None: every location, [B, H*W, d] (inference).  ``layout`` LAYOUT_REFERENCE keeps the
     reference's get_vectors_from_maps row order (D12); LAYOUT_ROWS gives one d-vector per
     (sample, location).  ``attr_batch_size`` bounds the LRP working set (the reference uses
-    64; results do not depend on it)."""
+    64; results do not depend on it).  ``group``: ``input_batch`` is this rank's slice of a
+    global batch (ranks in order) and the sampled locations are this slice's draws from the
+    global numpy stream (every rank draws for all samples, as one process would)."""
     x = _as_device_batch(input_batch, device)
     dev = x.device
     name = _layer_name(model, layer_idx)
     eng = get_engine(model, composite)
     B = x.size(0)
+    if B == 0:
+        raise _capi.DrsaAmdError("preprocess_data: empty input batch")
+    off, B_all = (0, B) if group is None else _sample_offset(B, group)
     li, where = eng.capture_stage(name)
     idx_all = None
     out_a = out_c = None
@@ -134,7 +139,8 @@ def preprocess_data(model: nn.Module, input_batch, composite, layer_idx: int, cl
         if out_a is None:
             if num_locations:
                 # sample after the maps exist, as the reference (one draw per sample, in order)
-                idx_all = torch.from_numpy(sample_spatial_locations(B, (H, W), num_locations).astype(np.int32)).to(dev)
+                draws = sample_spatial_locations(B_all, (H, W), num_locations)[off:off + B]
+                idx_all = torch.from_numpy(draws.astype(np.int32)).to(dev)
                 out_a = torch.empty(B * num_locations, C, device=dev)
                 out_c = torch.empty(B * num_locations, C, device=dev)
             else:
@@ -168,22 +174,84 @@ def get_vectors_from_maps(maps: torch.Tensor, idcs_batch: np.ndarray) -> torch.T
     return A
 
 
-def normalize_vectors(vectors: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """preprocessing.py:219-231: v / sqrt(mean(v^2)) / d^(1/4) (HIP, deterministic reduction)."""
+class _HipNormalizeOps:
+    """The two halves of drsa_amd_normalize_vectors for rows spread over ranks."""
+
+    def sumsq(self, v: torch.Tensor) -> torch.Tensor:
+        """This rank's fp64 sum of v^2 (a [1] device tensor; 0 for an empty shard)."""
+        out = torch.empty(1, dtype=torch.float64, device=v.device)
+        ws = torch.empty(_capi.lib().drsa_amd_normalize_workspace_bytes(), dtype=torch.uint8, device=v.device)
+        _capi.call("drsa_amd_normalize_sumsq", _capi.ptr(v) if v.numel() else None, v.numel(), ws.data_ptr(),
+                   ws.numel(), out.data_ptr(), _capi.stream_ptr(v.device))
+        return out
+
+    def scale(self, v: torch.Tensor, sums: torch.Tensor, n_total: int, out: torch.Tensor) -> None:
+        """out = v / sqrt((sums[0] + sums[1] + ...) / n_total) / d^(1/4)."""
+        _capi.call("drsa_amd_normalize_scale", _capi.ptr(v) if v.numel() else None, v.numel(), v.size(-1),
+                   sums.data_ptr(), sums.numel(), int(n_total), _capi.ptr(out) if out.numel() else None,
+                   _capi.stream_ptr(v.device))
+
+
+def _all_gather_rows(t: torch.Tensor, group) -> torch.Tensor:
+    """[world, *t.shape] with rank r's ``t`` in row r (RCCL on the device, gloo through the host)."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    src = t if dist.get_backend(group) == "nccl" else t.cpu()
+    parts = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(parts, src.contiguous(), group=group)
+    return torch.stack(parts).to(t.device)
+
+
+def normalize_vectors(vectors: torch.Tensor, out: Optional[torch.Tensor] = None, group=None,
+                      _ops=None) -> torch.Tensor:
+    """preprocessing.py:219-231: v / sqrt(mean(v^2)) / d^(1/4) (HIP, deterministic reduction).
+
+    ``group`` (a process group, e.g. ``dist.group.WORLD``): ``vectors`` is this rank's share of the
+    rows and the mean runs over ALL ranks' elements, as the reference normalises the whole
+    1000-sample set at once (getdrsadata.py:47-59).  One all-gather of (sum v^2, count) per call in
+    fp64; every rank adds the sums in rank order, so all ranks use the same E.  Without ``group``
+    the mean is over ``vectors`` alone (the reference's single-process call)."""
     v = vectors.detach()
-    _capi.require_gpu(v, "vectors")
     out = torch.empty_like(v) if out is None else out
-    ws = torch.empty(_capi.lib().drsa_amd_normalize_workspace_bytes(), dtype=torch.uint8, device=v.device)
-    _capi.call("drsa_amd_normalize_vectors", v.data_ptr(), v.numel(), v.size(-1), out.data_ptr(), ws.data_ptr(),
-               ws.numel(), _capi.stream_ptr(v.device))
+    if group is None:
+        _capi.require_gpu(v, "vectors")
+        ws = torch.empty(_capi.lib().drsa_amd_normalize_workspace_bytes(), dtype=torch.uint8, device=v.device)
+        _capi.call("drsa_amd_normalize_vectors", v.data_ptr(), v.numel(), v.size(-1), out.data_ptr(), ws.data_ptr(),
+                   ws.numel(), _capi.stream_ptr(v.device))
+        return out
+    ops = _ops or _HipNormalizeOps()
+    if _ops is None:
+        _capi.require_gpu(v, "vectors")
+    local = torch.cat([ops.sumsq(v).reshape(1).to(torch.float64),
+                       torch.tensor([float(v.numel())], dtype=torch.float64, device=v.device)])
+    table = _all_gather_rows(local, group)                   # [world, 2]: (sum v^2, count) per rank
+    n_total = int(table[:, 1].sum().item())
+    if n_total == 0:
+        raise _capi.DrsaAmdError("normalize_vectors: no elements on any rank")
+    ops.scale(v, table[:, 0].contiguous(), n_total, out)
     return out
+
+
+def _sample_offset(b_local: int, group) -> Tuple[int, int]:
+    """(first global sample index of this rank, global batch size): ranks hold consecutive slices."""
+    import torch.distributed as dist
+    rank = dist.get_rank(group)
+    sizes = _all_gather_rows(torch.tensor([b_local], dtype=torch.int64), group).reshape(-1).tolist()
+    return int(sum(sizes[:rank])), int(sum(sizes))
 
 
 def drsa_training_data(model: nn.Module, input_batch, composite, layer_idx: int, class_idx: int,
                        num_locations: int = 20, one_hot_encoded: bool = False, device=None,
-                       attr_batch_size: int = 1024) -> Tuple[torch.Tensor, torch.Tensor]:
+                       attr_batch_size: int = 1024, group=None) -> Tuple[torch.Tensor, torch.Tensor]:
     """preprocess_data -> normalize_vectors on A and on C separately (getdrsadata.py:119-137 then
-    :47-59 without the pickle round trip): normalised (A, C) [B*L, d], ready for drsa.main."""
+    :47-59 without the pickle round trip): normalised (A, C) [B*L, d], ready for drsa.main.
+
+    ``group``: rank-local extraction for the row-sharded optimiser (SURVEY §8(e) "per-GPU
+    extraction").  ``input_batch`` is this rank's slice of the global batch (rank 0 first); the
+    locations are drawn from the global numpy stream for every global sample as one process would
+    (each rank keeps its own rows) and the normalisation is over all ranks' rows.  The returned
+    rows are this rank's rows of the single-process result; feed them to
+    ``distributed.main_sharded(..., local_rows=True)``."""
     A, C = preprocess_data(model, input_batch, composite, layer_idx, class_idx, num_locations, one_hot_encoded,
-                           device, attr_batch_size)
-    return normalize_vectors(A, out=A), normalize_vectors(C, out=C)
+                           device, attr_batch_size, group=group)
+    return normalize_vectors(A, out=A, group=group), normalize_vectors(C, out=C, group=group)

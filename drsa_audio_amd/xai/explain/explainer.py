@@ -32,15 +32,16 @@ class HeatmapGenerator:
     def __init__(self, model: nn.Module, U: torch.Tensor, name_map: List[Tuple[List[str], object]],
                  sample_class: str, num_concepts: int = 4, layer_idx: int = 10,
                  device: str | torch.device = torch.device("cuda"), canonizers=None,
-                 standard: str = "sum") -> None:
+                 standard: str = "clone") -> None:
         """``canonizers`` (extension, default None = the reference's composite) is passed to the
         class composite, e.g. ``[SequentialMergeBatchNorm()]`` for the VGGish-BN models of the
         reference's DRSA scripts (getdrsadata.py:113), whose layer 19 has d = 100.
-        ``standard`` (extension): "sum" (default) computes the standard heatmap as the sum of the K
-        concept heatmaps -- every LRP rule is linear in the relevance, so this is the reference's
-        clone 0 up to fp32 rounding (as close to float64 as clone 0, tests/test_lrp_gpu.py), and the
-        network below the projection runs K instead of K+1 times; "clone" propagates clone 0 as
-        the reference's replicated batch does (explainer.py:92)."""
+        ``standard`` (extension): "clone" (default, the reference's semantics) propagates clone 0
+        as the reference's replicated batch does (explainer.py:92); "sum" computes the standard
+        heatmap as the sum of the K concept heatmaps -- every LRP rule is linear in the relevance,
+        so this is the reference's clone 0 up to fp32 rounding (as close to float64 as clone 0,
+        tests/test_lrp_gpu.py), and the network below the projection runs K instead of K+1 times
+        (the bench headline's mode; ties in the standard relevance may order differently)."""
         if standard not in ("sum", "clone"):
             raise ValueError("standard must be 'sum' or 'clone'")
         self.standard = standard

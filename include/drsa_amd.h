@@ -336,6 +336,18 @@ int drsa_amd_drsa_vectors(const float* act, const float* rel, const uint8_t* rel
 size_t drsa_amd_normalize_workspace_bytes(void);
 int drsa_amd_normalize_vectors(const float* v, int64_t n, int d, float* out, void* ws, size_t ws_bytes, void* stream);
 
+/* The same normalisation over rows spread across ranks (getdrsadata.py:47-59 normalises the whole
+ * 1000-sample x 20-location set at once, preprocessing.py:229-231):
+ *   drsa_amd_normalize_sumsq: this rank's sum of v^2 -> sum_out[0] (fp64, device; the fixed-order
+ *       reduction of drsa_amd_normalize_vectors; 0 for n == 0);
+ *   drsa_amd_normalize_scale: E = sqrt((sums[0] + ... + sums[nsums-1], in that order) / n_total),
+ *       out = v / E / d^(1/4) over this rank's n elements.  sums are the ranks' sum_out values in
+ *       rank order (one all-gather), n_total the element count over all ranks.  out may alias v.
+ * With nsums = 1 and n_total = n this is drsa_amd_normalize_vectors up to the fp64 sum's last bit. */
+int drsa_amd_normalize_sumsq(const float* v, int64_t n, void* ws, size_t ws_bytes, double* sum_out, void* stream);
+int drsa_amd_normalize_scale(const float* v, int64_t n, int d, const double* sums, int nsums, int64_t n_total,
+                             float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

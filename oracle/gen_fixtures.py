@@ -447,8 +447,31 @@ def main_round3():
     print("round-3 fixtures written to", OUT)
 
 
+# C4 long horizon: the C4 shape (N = 160 000 = 8 x 20 000 rows, d = 64, K = 8) for the reference's
+# default 2 000 steps (drsa.py:76); same data seed and U0 as DRSA_LONG["c4"]
+DRSA_C4_LONG = {"c4long": (160000, 64, 8, 3, "u64_seed42", 2000)}
+
+
+def main_round4():
+    """Round-4 fixture (new file; earlier fixtures stay byte-identical)."""
+    OUT.mkdir(parents=True, exist_ok=True)
+    rdrsa, _, _ = _import_reference()
+    saved = dict(DRSA_LONG)
+    DRSA_LONG.clear()
+    DRSA_LONG.update(DRSA_C4_LONG)
+    try:
+        out = _drsa_long(rdrsa)
+    finally:
+        DRSA_LONG.clear()
+        DRSA_LONG.update(saved)
+    np.savez_compressed(OUT / "drsa_c4_fixture.npz", **out)
+    print("round-4 fixtures written to", OUT)
+
+
 if __name__ == "__main__":
-    if "--round3" in sys.argv:
+    if "--round4" in sys.argv:
+        main_round4()
+    elif "--round3" in sys.argv:
         main_round3()
     elif "--round2" in sys.argv:
         main_round2()

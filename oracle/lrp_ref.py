@@ -700,10 +700,10 @@ def subspace_heatmaps(proj_model: nn.Module, name_map: Dict[str, RuleSpec], K: i
     ``forced_inputs``: per-sample layer inputs (see ``lrp``), replicated like the batch.
     ``standard``: "clone" = clone 0 of the replicated batch (the reference); "sum" = the K concept
     heatmaps summed, k ascending, in the heatmaps' precision (the product's HeatmapGenerator
-    default; equal in exact arithmetic since every rule is linear in the relevance).  Default:
-    "sum" for the product-order modes ("exact", "bf16"), "clone" otherwise."""
+    standard="sum" option; equal in exact arithmetic since every rule is linear in the relevance).
+    Default: "clone", as the product's HeatmapGenerator default."""
     if standard is None:
-        standard = "sum" if mode in ("exact", "bf16", "bf16bwd") else "clone"
+        standard = "clone"
     rules = class_composite_rules(name_map, K)
     xr = x.repeat_interleave(K + 1, dim=0)
     if forced_inputs is not None:

@@ -51,7 +51,10 @@ def main(src, dst, current=False):
     with open(os.path.join(dst, "summary.md"), "w") as fh:
         fh.write("\n".join(lines) + "\n")
     if current and os.path.exists(os.path.join(dst, "pmc_traffic.json")):
-        shutil.copy(os.path.join(dst, "pmc_traffic.json"), os.path.join(os.path.dirname(dst), "pmc_traffic.json"))
+        pm = json.load(open(os.path.join(dst, "pmc_traffic.json")))
+        pm["profile"] = os.path.basename(os.path.normpath(dst))      # bench.py names it in traffic_source
+        with open(os.path.join(os.path.dirname(dst), "pmc_traffic.json"), "w") as fh:
+            json.dump(pm, fh, indent=1)
 
 
 if __name__ == "__main__":

@@ -269,3 +269,58 @@ def test_launcher_spawns_ranks_and_forwards_rank0(tmp_path):
     r = subprocess.run([sys.executable, str(script), "2", "fail"], env=env, capture_output=True, text=True,
                        timeout=180)
     assert r.returncode == 3
+
+
+class OracleNormOps:
+    """normalize_vectors' two halves in numpy (the HIP kernels need a GPU): fp64 sum of squares,
+    then v / fl32(sqrt(sum / n)) / fl32(d^(1/4)) as preprocessing.py:229-231 writes it."""
+
+    def sumsq(self, v):
+        return torch.tensor([float(np.sum(v.double().numpy() ** 2))], dtype=torch.float64)
+
+    def scale(self, v, sums, n_total, out):
+        s = 0.0
+        for x in sums.tolist():          # rank order
+            s += x
+        E = np.float32(np.sqrt(s / n_total))
+        d4 = np.float32(v.size(-1) ** 0.25)
+        out.copy_(torch.from_numpy(v.numpy() / E / d4))
+
+
+def _worker_norm(rank, world, port, sizes, V, q):
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from drsa_audio_amd.xai.drsa.preprocessing import _sample_offset, normalize_vectors
+    lo = sum(sizes[:rank])
+    local = V[lo:lo + sizes[rank]].clone()
+    out = normalize_vectors(local, group=dist.group.WORLD, _ops=OracleNormOps())
+    off = _sample_offset(sizes[rank] // 4, dist.group.WORLD)
+    q.put((rank, out.numpy(), off))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("sizes", [(600, 400), (1000, 0)])
+def test_normalize_vectors_two_ranks_equals_single_process(sizes):
+    """normalize_vectors(group=...) on row shards equals the single-process normalisation of the
+    concatenation (getdrsadata.py:47-59 normalises the whole set): every rank's rows, bit for bit;
+    a rank without rows contributes nothing; the sample offsets are the ranks' prefix sums."""
+    rng = np.random.default_rng(5)
+    V = torch.from_numpy((rng.standard_normal((sum(sizes), 16)) * 3).astype(np.float32))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_norm, args=(r, 2, port, list(sizes), V, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (o, off) for r, o, off in (q.get(timeout=120) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ops = OracleNormOps()
+    ref = torch.empty_like(V)
+    ops.scale(V, ops.sumsq(V), V.numel(), ref)
+    got = np.concatenate([res[0][0], res[1][0]])
+    assert np.array_equal(got, ref.numpy())
+    assert res[0][1] == (0, sum(sizes) // 4) and res[1][1] == (sizes[0] // 4, sum(sizes) // 4)

@@ -145,3 +145,68 @@ def test_prototype_search_matches_oracle():
     got = subset_objectives(va.to(DEV).contiguous(), vc.to(DEV).contiguous(), U.to(DEV), K, n).cpu().numpy()
     np.testing.assert_allclose(got, objs, rtol=1e-5)
     assert sp is not None and len(sp) == n
+
+
+def _rank_local_worker(rank, world, port, x_local, q):
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "tests"), os.path.join(root, "oracle")]
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from lrp_common import gtzan128
+    from drsa_audio_amd.xai.drsa.preprocessing import drsa_training_data
+    from drsa_audio_amd.xai.drsa.distributed import sharded_run
+    from drsa_audio_amd.utils.constants import LRP_NAME_MAP_GTZAN
+    from drsa_audio_amd.zennit.composites import NameMapComposite
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    np.random.seed(7)
+    A, C = drsa_training_data(gtzan128().to(dev), x_local.to(dev), NameMapComposite(LRP_NAME_MAP_GTZAN), 7, 3,
+                              num_locations=20, group=dist.group.WORLD)
+    U0 = torch.from_numpy(np.linalg.qr(np.random.default_rng(0).standard_normal((64, 64)))[0].astype(np.float32))
+    U, traj = sharded_run(A, C, U0.to(dev), 4, 30)
+    q.put((rank, A.cpu().numpy(), C.cpu().numpy(), traj, U.cpu().numpy()))
+    dist.destroy_process_group()
+
+
+def test_rank_local_training_data_two_ranks_equals_single_process():
+    """SURVEY §8(e) per-GPU extraction: two ranks on cuda:0 (gloo) each extract only their own
+    samples (5 + 3 of an 8-sample batch) with drsa_training_data(group=WORLD): the location draws
+    follow the global numpy stream and the normalisation runs over both ranks' rows, so the rows
+    equal the single-process result (within 1 ulp), and the row-sharded DRSA trajectory on them
+    equals the unsharded run within 1e-5."""
+    import socket
+    import torch.multiprocessing as mp
+    from drsa_audio_amd.xai.drsa.preprocessing import drsa_training_data
+    from drsa_audio_amd.xai.drsa.drsa import DrsaWorkspace, drsa_run
+    net = gtzan128()
+    x = logmel(8, seed=5)
+    np.random.seed(7)
+    A, C = drsa_training_data(_gpu(net), x.to(DEV), NameMapComposite(LRP_NAME_MAP_GTZAN), 7, 3, num_locations=20)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    parts = [x[:5].clone(), x[5:].clone()]
+    procs = [ctx.Process(target=_rank_local_worker, args=(r, 2, port, parts[r], q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r[0]: r[1:] for r in (q.get(timeout=300) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    Ag = np.concatenate([res[0][0], res[1][0]])
+    Cg = np.concatenate([res[0][1], res[1][1]])
+    A_, C_ = A.cpu().numpy(), C.cpu().numpy()
+    assert Ag.shape == A_.shape == (160, 64)
+    for got, ref in ((Ag, A_), (Cg, C_)):
+        ulp = np.abs(got.view(np.int32).astype(np.int64) - ref.view(np.int32).astype(np.int64))
+        assert ulp.max() <= 1, ulp.max()
+    assert np.array_equal(res[0][2], res[1][2]) and np.array_equal(res[0][3], res[1][3])
+    U0 = torch.from_numpy(np.linalg.qr(np.random.default_rng(0).standard_normal((64, 64)))[0].astype(np.float32))
+    _, traj1 = drsa_run(A, C, U0.to(DEV), 4, 30, DrsaWorkspace(A.size(0), 64, 4, DEV))
+    traj1 = traj1.cpu().numpy()
+    assert np.max(np.abs(res[0][2] - traj1) / np.abs(traj1)) < 1e-5

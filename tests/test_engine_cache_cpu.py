@@ -41,3 +41,27 @@ def test_bn_buffer_change_recompiles_and_finalizers_do_not_pile_up(monkeypatch):
     assert not any(f.alive for f in olds)                   # evicted entries detached theirs
     del m
     assert E.cache_size() == 0                              # the live finalizer still evicts
+
+
+def test_projection_u_update_recompiles(monkeypatch):
+    """ProjectionModel.U is a plain attribute, not a parameter: an in-place update of U (or a new
+    U bound to the Projection module) must recompile, since the plan caches U and UU^T - I
+    (VERDICT r03 weak #11)."""
+    from drsa_audio_amd.model.create_model import VGGType
+    from drsa_audio_amd.model.modify_model import ProjectionModel
+    monkeypatch.setattr(E, "LRPEngine", _Dummy)
+    E.clear_cache()
+    torch.manual_seed(0)
+    m = VGGType(n_filters=(8, 8, 16, 16, 16), n_dense=32, n_classes=2, pool_kernels=((2, 2),) * 5, dropout=0.0,
+                input_size=(64, 64), conv_bn=False, dense_bn=False, block_depth=1).eval()
+    U = torch.linalg.qr(torch.randn(16, 16))[0]
+    pm = ProjectionModel(m, 7, U, 4, case="toy").eval()
+    e1 = E.get_engine(pm, None)
+    assert E.get_engine(pm, None) is e1
+    pm.U.copy_(torch.linalg.qr(torch.randn(16, 16))[0])      # in place: the reference would use it
+    e2 = E.get_engine(pm, None)
+    assert e2 is not e1 and e1.released
+    assert E.get_engine(pm, None) is e2
+    pm.features.projection.U = torch.linalg.qr(torch.randn(16, 16))[0]   # rebound on the module
+    assert E.get_engine(pm, None) is not e2
+    E.clear_cache()

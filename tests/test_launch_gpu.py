@@ -26,6 +26,9 @@ def test_bench_gpus2_own_launcher_one_device():
     assert len(out["rank_ms_per_step"]) == 2 and out["ms_per_step"] == pytest.approx(max(out["rank_ms_per_step"]))
     sec = out["secondary"]
     assert sec["drsa_sharded"]["vector_steps_per_s"] > 0
+    # the N > 1 line checks itself against the unsharded run of every rank's rows
+    assert sec["drsa_sharded"]["traj_dev_vs_unsharded"] < 1e-5
+    assert sec["drsa_sharded"]["c5_joint"]["traj_dev_vs_unsharded"] < 1e-5
     g = sec["drsa_grid_task_parallel"]
     assert g["problems"] == 18 and g["problems_per_rank"] == [9, 9] and g["scaling"] == "strong"
     lo, hi = g["objective_final_min_max"]
