@@ -443,7 +443,7 @@ def drsa_sharded_bench(device, world, rank, steps=100):
     probs = []
     for p_ in range(2):
         A5, C5 = drsa_inputs(n, d5, 200 + 10 * rank + p_)
-        U5 = torch.linalg.qr(torch.randn(d5, d5, generator=g, dtype=torch.float64))[0].float()
+        U5 = torch.linalg.qr(torch.randn(d5, d5, generator=g, dtype=torch.float64))[0].float().contiguous()
         probs.append((torch.from_numpy(A5).to(device), torch.from_numpy(C5).to(device), U5.to(device), K5))
     sharded_run_joint(probs, 3)
     torch.cuda.synchronize(device)

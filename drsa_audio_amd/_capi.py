@@ -52,6 +52,9 @@ SIGNATURES = {
                                  _i32, _f32, _vp]),
     "drsa_amd_conv_bwd_bf16": (_i32, [_fp, _vp, _vp, _fp, _fp, _fp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
                                       _i32, _f32, _vp]),
+    "drsa_amd_conv_fwd_den_ring": (_i32, [_fp, _fp, _fp, _fp, _fp, _vp, _fp, _i32, _i32, _i32, _i32, _i32, _vp]),
+    "drsa_amd_conv_bwd_den_ring": (_i32, [_fp, _vp, _vp, _i32, _fp, _fp, _fp, _fp, _i32, _i32, _i32, _i32, _i32, _i32,
+                                          _i32, _i32, _f32, _vp]),
     "drsa_amd_conv_bwd_has_kernel_bf16": (_i32, [_i32, _i32, _i32, _i32, _i32]),
     "drsa_amd_linear_fwd": (_i32, [_fp, _fp, _fp, _fp, _fp, _i32, _i32, _i32, _vp]),
     "drsa_amd_linear_bwd": (_i32, [_fp, _ip, _i32, _fp, _i32, _i32, _f32, _fp, _fp, _i32, _fp, _i32, _f32, _fp,
@@ -85,7 +88,7 @@ class DrsaProblem(C.Structure):
 
 
 XM_NONE, XM_MUL, XM_SPLIT = 0, 1, 2
-POST_NONE, POST_DIV, POST_MASK = 0, 1, 2
+POST_NONE, POST_DIV, POST_MASK, POST_DIV_RING = 0, 1, 2, 3
 
 
 class DrsaAmdError(RuntimeError):

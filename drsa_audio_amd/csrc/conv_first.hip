@@ -49,6 +49,14 @@ __global__ __launch_bounds__(kThreads) void first_conv_pool_kernel(ConvArgs a, i
 
   const size_t plane2 = (size_t)H2 * W2;
   const size_t obase = ((size_t)b * a.cout) * plane2 + (size_t)qy * W2 + 4 * g4;
+  // den_ring_only (map den): the backward needs the per-sample copy only on the border ring of
+  // float4 groups (POST_DIV_RING; the map is one value per channel elsewhere), stored compactly:
+  // per plane [row 0 | row H2-1 | rows 1..H2-2 x (first 4, last 4 columns)], coalesced float4s
+  const bool den_ring = DEN == 1 && a.den_ring_only;
+  const bool on_ring = qy == 0 || qy == H2 - 1 || g4 == 0 || 4 * g4 + 4 >= W2;
+  const int ring_n = 2 * W2 + 8 * (H2 - 2);
+  const int ring_i = qy == 0 ? 4 * g4 : qy == H2 - 1 ? W2 + 4 * g4 : 2 * W2 + (qy - 1) * 8 + (g4 == 0 ? 0 : 4);
+  const size_t rbase = (size_t)b * a.cout * ring_n + ring_i;
 
   // blockIdx.y: channel slice (more waves in flight for the store stream)
   const int cper = (a.cout + gridDim.y - 1) / gridDim.y;
@@ -93,8 +101,11 @@ __global__ __launch_bounds__(kThreads) void first_conv_pool_kernel(ConvArgs a, i
       ym[j] = m;
       amw |= (uint32_t)am << (8 * j);
       if constexpr (DEN == 1) {
+        // off the ring (den_ring) nothing is stored: those lanes read one address (an L1
+        // broadcast) instead of their scattered map pixel
         const int py = am >> 1, px = am & 1;
-        dn[j] = a.den_map[((size_t)co * H + 2 * qy + py) * W + 8 * g4 + 2 * j + px];
+        const size_t mi = ((size_t)co * H + 2 * qy + py) * W + 8 * g4 + 2 * j + px;
+        dn[j] = a.den_map[(den_ring && !on_ring) ? 0 : mi];
       } else if constexpr (DEN == 2) {
         // the rule's denominator at the argmax pixel only (every chain is per pixel)
         float xs[9];
@@ -132,7 +143,12 @@ __global__ __launch_bounds__(kThreads) void first_conv_pool_kernel(ConvArgs a, i
     const size_t o = obase + (size_t)co * plane2;
     *reinterpret_cast<float4*>(a.out + o) = make_float4(ym[0], ym[1], ym[2], ym[3]);
     *reinterpret_cast<uint32_t*>(a.out_amax + o) = amw;
-    if constexpr (DEN != 0) *reinterpret_cast<float4*>(a.out_den + o) = make_float4(dn[0], dn[1], dn[2], dn[3]);
+    if constexpr (DEN != 0) {
+      if (!den_ring)
+        *reinterpret_cast<float4*>(a.out_den + o) = make_float4(dn[0], dn[1], dn[2], dn[3]);
+      else if (on_ring)
+        *reinterpret_cast<float4*>(a.out_den + rbase + (size_t)co * ring_n) = make_float4(dn[0], dn[1], dn[2], dn[3]);
+    }
   }
 }
 

@@ -3,7 +3,10 @@
 #include <stdint.h>
 
 enum XMode { XM_NONE = 0, XM_MUL = 1, XM_SPLIT = 2 };
-enum PostMode { POST_NONE = 0, POST_DIV = 1, POST_MASK = 2 };
+// POST_DIV_RING: POST_DIV where the next layer's denominator is a WSquare / Flat map under a 2x2
+// pool: one value per channel (den_const4[c][0..3]) off the border ring of float4 groups, and the
+// per-sample copy at the argmax (den) only on that ring (the forward writes nothing else)
+enum PostMode { POST_NONE = 0, POST_DIV = 1, POST_MASK = 2, POST_DIV_RING = 3 };
 
 struct ConvArgs {
   const float* in;          // A source: NCHW input (dense) or g at pool resolution (sparse)
@@ -11,6 +14,7 @@ struct ConvArgs {
   const float* wts;         // [NG][9 * cin_p][cout_p], k = ci * 9 + ky * 3 + kx
   const float* bias;        // forward: [3][cout_p] = (b, b+, b-)
   const float* den_map;     // forward, WSquare/Flat: [cout][H][W] input-independent denominator
+  const float* den_const4;  // backward POST_DIV_RING: [cout][4] the map's value off the ring
   const float* x;           // backward: activation at output resolution (per sample)
   const float* den;         // backward POST_DIV: next layer's denominator at output resolution
   float* out;
@@ -21,6 +25,7 @@ struct ConvArgs {
   int clones;               // batch index / clones = sample index
   int xmode, post;
   float eps;
+  int den_ring_only;        // forward (first layer, map den): write out_den on the ring groups only
   int dbg;                  // ablation only (DRSA_AMD_CONV_DBG): 1 no staging loads, 2 no epilogue I/O, 4 no MFMA
 };
 

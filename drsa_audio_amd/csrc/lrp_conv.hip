@@ -175,4 +175,42 @@ int drsa_amd_conv_bwd_bf16(const float* g, const uint8_t* g_amax, const uint16_t
   return launch(e, a, Bq, (hipStream_t)stream);
 }
 
+int drsa_amd_conv_fwd_den_ring(const float* in, const float* wts, const float* bias, const float* den_map, float* out,
+                               uint8_t* out_amax, float* den_ring, int B, int cout, int H, int W, int ng,
+                               void* stream) {
+  DRSA_REQUIRE(in && wts && den_map && out && out_amax && den_ring, "conv_fwd_den_ring: null pointer");
+  DRSA_REQUIRE(B > 0 && H >= 4 && W > 0 && H % 2 == 0 && W % 16 == 0,
+               "conv_fwd_den_ring: needs H >= 4 even and W %% 16 == 0 (got %dx%d)", H, W);
+  DRSA_REQUIRE(ng >= 1 && ng <= 3, "conv_fwd_den_ring: ng must be 1..3");
+  ConvArgs a{};
+  a.in = in; a.wts = wts; a.bias = bias; a.den_map = den_map; a.out = out; a.out_amax = out_amax;
+  a.out_den = den_ring; a.H = H; a.W = W; a.cin = 1; a.cout = cout; a.clones = 1; a.den_ring_only = 1;
+  return drsa_first_conv_pool(a, pad32(cout), ng, B, (hipStream_t)stream);
+}
+
+int drsa_amd_conv_bwd_den_ring(const float* g, const uint8_t* g_amax, const void* wts, int wts_bf16, const float* x,
+                               const float* den_ring, const float* den_const4, float* out, int Bq, int clones, int cin,
+                               int cout, int H, int W, int ng, int xmode, float eps, void* stream) {
+  DRSA_REQUIRE(Bq > 0 && clones > 0 && Bq % clones == 0, "conv_bwd_den_ring: bad batch/clones");
+  DRSA_REQUIRE(x && den_ring && den_const4, "conv_bwd_den_ring: needs x, den_ring and den_const4");
+  DRSA_REQUIRE(H % 2 == 0 && W % 4 == 0, "conv_bwd_den_ring: H must be even and W %% 4 == 0 (got %dx%d)", H, W);
+  DRSA_REQUIRE(xmode == XM_NONE || xmode == XM_MUL || xmode == XM_SPLIT, "conv_bwd_den_ring: bad xmode");
+  DRSA_REQUIRE(((uintptr_t)den_const4 & 15) == 0, "conv_bwd_den_ring: den_const4 must be 16-byte aligned");
+  const int et = wts_bf16 ? 1 : 0;
+  DRSA_REQUIRE(!et || (ng == 1 && cin >= 16 && ((uintptr_t)wts & 15) == 0),
+               "conv_bwd_den_ring: bf16 weights need ng == 1, cin >= 16 and 16-byte alignment");
+  DRSA_REQUIRE(et || (ng >= 1 && ng <= 2), "conv_bwd_den_ring: ng must be 1..2");
+  const Entry* e = find(pad32(cin), pad32(cout), W, ng, g_amax ? A_POOLSPARSE : A_DENSE, EPI_BWD, et);
+  if (!e) {
+    drsa::set_error("conv_bwd_den_ring: no kernel for cin=%d cout=%d W=%d ng=%d sparse=%d bf16=%d", cin, cout, W, ng,
+                    g_amax != nullptr, et);
+    return DRSA_EUNSUPPORTED;
+  }
+  ConvArgs a{};
+  a.in = g; a.in_amax = g_amax; a.wts = reinterpret_cast<const float*>(wts); a.x = x; a.den = den_ring;
+  a.den_const4 = den_const4; a.out = out; a.H = H; a.W = W; a.cin = cin; a.cout = cout;
+  a.clones = clones; a.xmode = xmode; a.post = POST_DIV_RING; a.eps = eps;
+  return launch(e, a, Bq, (hipStream_t)stream);
+}
+
 }  // extern "C"

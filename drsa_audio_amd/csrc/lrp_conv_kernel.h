@@ -647,10 +647,22 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
   // its own basic block, one full memory round trip after another)
   const bool need_x = (a.xmode != XM_NONE || a.post != POST_NONE) && !(a.dbg & 2);
   const bool mul_x = a.xmode != XM_NONE && !(a.dbg & 2), split_x = a.xmode == XM_SPLIT && !(a.dbg & 2);
-  const bool post_div = a.post == POST_DIV, post_any = a.post != POST_NONE;
+  // POST_DIV_RING: float4 groups off the image's border ring read the map's per-channel value
+  // (den_const4, one 16-byte line per channel: an L1 broadcast) instead of the per-sample copy,
+  // which the forward writes on the ring only; the pointer is a per-lane select, no branch
+  const bool ring = a.post == POST_DIV_RING && a.den_const4;
+  const bool post_div = a.post == POST_DIV || ring, post_any = a.post != POST_NONE;
   const float* xsrc = xs ? xs : oqp;
-  const float* dsrc = (ds && post_div) ? ds : xsrc;
+  const float* dsrc = (ds && post_div && !ring) ? ds : xsrc;
   const float eps = a.eps;
+  const bool on_ring = !pix_ok || ty0 + py == 0 || ty0 + py == H - 1 || tx0 + px == 0 || tx0 + px + 4 >= W;
+  const bool use_c4 = ring && !on_ring;
+  // the compact ring of plane (sample, channel): [row 0 | row H-1 | rows 1..H-2 x (4 + 4 columns)]
+  const int ring_n = 2 * W + 8 * (H - 2);
+  const int Y = ty0 + py, X = tx0 + px;
+  const int ring_i = !pix_ok ? 0 : Y == 0 ? X : Y == H - 1 ? W + X : 2 * W + (Y - 1) * 8 + (X == 0 ? 0 : 4);
+  const float* rsrc = ring ? a.den + (size_t)bs * a.cout * ring_n + ring_i : dsrc;
+  const size_t dstride = ring ? (size_t)ring_n : (size_t)HW;
   // epilogue x/den loads of (n-tile v, pass sub); (0, 0) is issued before the last chunk's MFMAs
   auto epi_loads = [&](int v, int sub, float4 (&xk)[V4T], float4 (&dk)[V4T], bool lx = true, bool ld = true,
                        int i0 = 0, int i1 = -1) {
@@ -662,7 +674,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
       const bool ok = cl < TCH && co < a.cout;
       const int coc = ok ? co : 0;
       if (lx) xk[it] = *reinterpret_cast<const float4*>(xsrc + (size_t)coc * HW);
-      if (ld) dk[it] = *reinterpret_cast<const float4*>(dsrc + (size_t)coc * HW);
+      if (ld) dk[it] = *reinterpret_cast<const float4*>(use_c4 ? a.den_const4 + (size_t)coc * 4 : rsrc + coc * dstride);
     }
   };
   // x groups prefetched before the last chunk's MFMAs (all of them spill a few registers)
@@ -675,6 +687,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
     stg.store(halo, wl, tid);
     __syncthreads();
     epi_loads(0, 0, pre_x, pre_d, true, DRSA_CONV_PRE_D, 0, kPreN);
+
     if (active && !(a.dbg & 4)) {
       if constexpr (Cfg::BF)
         mfma_chunk_bf<Cfg>(reinterpret_cast<const uint4*>(halo), reinterpret_cast<const uint4*>(wl), pix_off, lane, wn,

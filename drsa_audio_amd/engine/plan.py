@@ -42,13 +42,17 @@ import torch
 import torch.nn as nn
 
 from .. import _capi
-from .._capi import POST_DIV, POST_MASK, POST_NONE, XM_MUL, XM_NONE, XM_SPLIT
+from .._capi import POST_DIV, POST_DIV_RING, POST_MASK, POST_NONE, XM_MUL, XM_NONE, XM_SPLIT
 from ..zennit import rules as R
 from ..zennit.canonizers import SequentialMergeBatchNorm
 
 # store h and a' in HBM for projection_bwd instead of recomputing them there (A/B comparisons
 # only; both paths are bit-identical)
 _PROJ_STORE = os.environ.get("DRSA_AMD_PROJ_STORE", "0") == "1"
+# A/B switch: 1 = the WSquare/Flat layer's forward stores its per-sample denominator at the argmax
+# everywhere and the next backward reads it there (POST_DIV) instead of the ring form (POST_DIV_RING:
+# the copy on the image's border ring only, the map's per-channel interior value elsewhere)
+_DEN_COPY = os.environ.get("DRSA_AMD_DEN_COPY", "0") == "1"
 
 
 def _pad32(c: int) -> int:
@@ -72,6 +76,7 @@ def _eps_of(rule) -> float:
 
 
 @dataclass
+
 class ProjGroup:
     U: torch.Tensor
     K: int
@@ -451,6 +456,15 @@ class LRPEngine:
             st.den_maps[key] = den
         return st.den_maps[key]
 
+    def _den_const4(self, st: ConvStage, H: int, W: int) -> torch.Tensor:
+        """[cout][4]: the map's interior value per channel (drsa_amd_first_layer_den computes every
+        interior pixel with the same 9-tap chain, so map[c][1][1] is all of them), 4 copies."""
+        key = ("c4", H, W)
+        if key not in st.den_maps:
+            m = self._den_map(st, H, W)
+            st.den_maps[key] = m[:, 1, 1].reshape(-1, 1).expand(-1, 4).contiguous()
+        return st.den_maps[key]
+
     def _conv_fwd(self, tag, st: ConvStage, neg: bool, cur, den_map, out, amax, den, B, h, w, ng, pool, s):
         """One conv forward launch: the bf16 kernel in a bf16 plan (Cin > 1), else fp32."""
         bias3 = st.bias3_n if neg else st.bias3
@@ -515,12 +529,25 @@ class LRPEngine:
                 cur, h, w = out, h // ph, w // pw
             elif st.proj is None and st.pool:
                 ph, pw = st.pool_k
+                # WSquare / Flat first layer under a 2x2 pool: its map is one value per channel off the
+                # image's border ring, so the forward stores the per-sample denominator copy only on the
+                # ring, compactly (drsa_amd_conv_fwd_den_ring), and the next conv's backward reads the
+                # map's interior value elsewhere (drsa_amd_conv_bwd_den_ring; bit-identical)
+                ring = (st.den_kind == "map" and st.pool_k == (2, 2) and st.cin == 1 and w % 16 == 0 and h >= 4
+                        and li + 1 < len(self.stages) and self.stages[li + 1].den_kind != "ab" and not _DEN_COPY)
                 out = self._buf((li, "y"), (B, st.cout, h // ph, w // pw))
                 amax = self._buf((li, "amax"), (B, st.cout, h // ph, w // pw), torch.uint8)
-                den = self._buf((li, "den"), (B, st.cout, h // ph, w // pw)) if need_den else None
-                self._conv_fwd(f"conv_fwd:{st.name}", st, False, cur, den_map, out, amax, den, B, h, w, st.ng_fwd,
-                               fused_pool, s)
-                rec.update(y=out, amax=amax, den=den, Hout=h // ph, Wout=w // pw)
+                if ring:
+                    den = self._buf((li, "den_ring"), (B, st.cout, 2 * (w // 2) + 8 * (h // 2 - 2)))
+                    self._call(f"conv_fwd:{st.name}", "drsa_amd_conv_fwd_den_ring", cur.data_ptr(),
+                               st.wts_fwd.data_ptr(), st.bias3.data_ptr(), den_map.data_ptr(), out.data_ptr(),
+                               amax.data_ptr(), den.data_ptr(), B, st.cout, h, w, st.ng_fwd, s)
+                else:
+                    den = self._buf((li, "den"), (B, st.cout, h // ph, w // pw)) if need_den else None
+                    self._conv_fwd(f"conv_fwd:{st.name}", st, False, cur, den_map, out, amax, den, B, h, w, st.ng_fwd,
+                                   fused_pool, s)
+                rec.update(y=out, amax=amax, den=den, Hout=h // ph, Wout=w // pw,
+                           den_const4=self._den_const4(st, h, w) if ring else None)
                 if st.den_kind == "ab":   # second pass: den_n (y and argmax rewritten with the same values)
                     den_n = self._buf((li, "den_n"), (B, st.cout, h // ph, w // pw))
                     self._conv_fwd(f"conv_fwd_n:{st.name}", st, True, cur, None, out, amax, den_n, B, h, w, 2,
@@ -588,6 +615,8 @@ class LRPEngine:
             return POST_NONE, None, 0.0
         if st.den_kind is None or st.den_kind == "ab":
             return POST_MASK, None, 0.0
+        if rec.get("den_const4") is not None:
+            return POST_DIV_RING, rec, st.eps        # den = rec["den"] on the ring, rec["den_const4"] elsewhere
         return POST_DIV, rec["den"], st.eps
 
     @torch.no_grad()
@@ -696,6 +725,14 @@ class LRPEngine:
                 self._call(f"ab_combine:{st.name}", "drsa_amd_ab_combine", pos.data_ptr(), neg.data_ptr(), st.alpha,
                            st.beta, x_in.data_ptr() if post != POST_NONE else None, _capi.ptr(den), out.data_ptr(), Bq,
                            clones, st.cin * h * w, post, float(eps), s)
+            elif post == POST_DIV_RING:
+                out = self._buf((li, "R"), (Bq, st.cin, h, w))
+                bf = st.wts_bwd_bf is not None and _capi.lib().drsa_amd_conv_bwd_has_kernel_bf16(
+                    st.cout, st.cin, w, 1, int(amax_in is not None))
+                self._call(f"conv_bwd:{st.name}", "drsa_amd_conv_bwd_den_ring", g.data_ptr(), _capi.ptr(amax_in),
+                           (st.wts_bwd_bf if bf else st.wts_bwd).data_ptr(), 1 if bf else 0, x_in.data_ptr(),
+                           den["den"].data_ptr(), den["den_const4"].data_ptr(), out.data_ptr(), Bq, clones, st.cout,
+                           st.cin, h, w, st.ng_bwd, st.xmode_bwd, float(eps), s)
             else:
                 out = self._buf((li, "R"), (Bq, st.cin, h, w))
                 bf = st.wts_bwd_bf is not None and _capi.lib().drsa_amd_conv_bwd_has_kernel_bf16(

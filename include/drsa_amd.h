@@ -172,6 +172,30 @@ int drsa_amd_conv_bwd(const float* g, const uint8_t* g_amax, const float* wts, c
 int drsa_amd_conv_bwd_bf16(const float* g, const uint8_t* g_amax, const uint16_t* wts, const float* x, const float* den,
                            float* out, int Bq, int clones, int cin, int cout, int H, int W, int ng, int xmode,
                            int post, float eps, void* stream);
+
+/* WSquare / Flat first layer under a 2x2 max-pool, with its denominator map split for the next
+ * backward (zennit WSquare/Flat: den = conv(1; W^2, b^2); constants.py:29 puts
+ * WSquare on the first layer).  Such a map holds one value per channel on every pixel off its
+ * 1-pixel border ring (each interior pixel sums all 9 taps in the same order), so the denominator
+ * at the pool argmax is that value everywhere except near the image border.
+ *   drsa_amd_conv_fwd_den_ring: drsa_amd_conv_fwd for cin = 1, pool = 1 and the map den, except
+ *       that the per-sample copy of the denominator at the argmax goes only to den_ring, the border
+ *       ring of float4 groups stored compactly: per (sample, channel) plane R = 2 W/2 + 8 (H/2 - 2)
+ *       floats = [pooled row 0 | pooled row H/2-1 | rows 1..H/2-2 x (columns 0..3, W/2-4..W/2-1)]
+ *       (H >= 4, W % 16 == 0).
+ *   drsa_amd_conv_bwd_den_ring: drsa_amd_conv_bwd (wts_bf16 = 0) or _bf16 (wts_bf16 = 1) with
+ *       post = POST_DIV whose denominator is den_ring (the compact ring above) on the ring and den_const4[c][0..3] (the
+ *       map's interior value of channel c, 4 copies, 16-byte aligned) elsewhere.  Here H, W are the
+ *       pooled resolution.
+ * Together they give bit for bit what drsa_amd_conv_fwd (with out_den) + drsa_amd_conv_bwd(POST_DIV)
+ * give, while only ~1/16 of the per-sample denominator copy is ever stored and read, in full
+ * coalesced float4s (replace the same rule passes, attribute.py:98-107). */
+int drsa_amd_conv_fwd_den_ring(const float* in, const float* wts, const float* bias, const float* den_map, float* out,
+                               uint8_t* out_amax, float* den_ring, int B, int cout, int H, int W, int ng,
+                               void* stream);
+int drsa_amd_conv_bwd_den_ring(const float* g, const uint8_t* g_amax, const void* wts, int wts_bf16, const float* x,
+                               const float* den_ring, const float* den_const4, float* out, int Bq, int clones, int cin,
+                               int cout, int H, int W, int ng, int xmode, float eps, void* stream);
 /* 1 if drsa_amd_conv_bwd_bf16 has a kernel for this shape (sparse: g at 2x2-pool resolution). */
 int drsa_amd_conv_bwd_has_kernel_bf16(int cin, int cout, int W, int ng, int sparse);
 

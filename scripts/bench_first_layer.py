@@ -1,5 +1,5 @@
 """Micro-benchmark of drsa_amd_first_layer_bwd (pooled) at the bench shape: GTZAN-128 features.0,
-B=512 x (K+1)=5 clones, 32 channels, 128x128."""
+B=512 x K=4 clones, 32 channels, 128x128."""
 import json
 import os
 import sys
@@ -9,7 +9,7 @@ import torch
 from drsa_audio_amd import _capi
 
 dev = torch.device("cuda")
-Bs, clones, C, H, W = 512, 5, 32, 128, 128
+Bs, clones, C, H, W = 512, int(os.environ.get("FL_CLONES", "4")), 32, 128, 128
 Bq = Bs * clones
 g = torch.randn(Bq, C, H // 2, W // 2, device=dev)
 amax = torch.randint(0, 4, (Bs, C, H // 2, W // 2), device=dev, dtype=torch.uint8)

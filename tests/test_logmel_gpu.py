@@ -1,11 +1,13 @@
 """Log-mel HIP front end (csrc/logmel.hip) vs the CPU oracle (GPU).
 
-Tolerance (written here, floating point): |log-mel(GPU) - log-mel(oracle f64)| <= 1e-3 in
-log10 units (0.23 % in mel energy; the worst bins are the quiet ones, where any fp32 FFT's
-rounding noise relative to the frame's energy shows), and the linear-mel error relative to
-each chunk's maximum <= 2e-5.  torch.stft's own float32 restatement sits at the same distance
-from the f64 oracle (measured: 7.9e-5 vs ours 7.2e-5 on test 1; 2.1e-4 vs 3.7e-4 worst seen).
-Parity vs torchaudio itself is unpinned (not installed; no reference fixture).
+Tolerance (written here, floating point), anchored per test on the reference's own precision:
+the oracle's "torch32" restatement (torch.stft / the mel matmul / log10 in float32, the way the
+reference's torchaudio transform computes, dataloading.py:138-176) is run on the same input, and
+the HIP result's distance from the float64 oracle must be at most 2x torch32's distance, in the
+maximum AND in the RMS over all finite bins (``anchored``).  A regression of the kernel's
+arithmetic by 2x or more fails.  The worst bins are the quiet ones, where any fp32 FFT's rounding
+noise relative to the frame's energy shows.  The linear-mel error relative to each chunk's maximum
+stays <= 2e-5.  Parity vs torchaudio itself is unpinned (not installed; no reference fixture).
 """
 import numpy as np
 import pytest
@@ -15,7 +17,23 @@ import logmel_ref as L
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
-TOL_LOG = 1e-3
+RATIO = 2.0
+
+
+def anchored(out, ref, t32, ratio=RATIO):
+    """max and RMS of |out - ref| <= ratio x those of |t32 - ref| over the bins finite in all
+    three (clamped bins compare exactly).  Returns (max, max32, rms, rms32)."""
+    out, ref, t32 = (np.asarray(v, dtype=np.float64) for v in (out, ref, t32))
+    ok = np.isfinite(out) & np.isfinite(ref) & np.isfinite(t32)
+    assert np.array_equal(np.isfinite(out), np.isfinite(ref))
+    e, e32 = np.abs(out - ref)[ok], np.abs(t32 - ref)[ok]
+    m, m32 = e.max(), e32.max()
+    r, r32 = np.sqrt(np.mean(e * e)), np.sqrt(np.mean(e32 * e32))
+    print(f"\n  |d log-mel| vs f64: HIP max {m:.2e} rms {r:.2e}; torch32 max {m32:.2e} rms {r32:.2e}")
+    floor = 1e-7      # both exact (e.g. every bin clamped): nothing to anchor on
+    assert m <= ratio * m32 + floor, (m, m32)
+    assert r <= ratio * r32 + floor, (r, r32)
+    return m, m32, r, r32
 
 
 def _loader(case="gtzan", **kw):
@@ -28,10 +46,7 @@ def test_gtzan_songs_fused_slice_peak_logmel():
     ref = L.load_songs(songs, "gtzan", mode="f64")
     out = _loader().load_songs(torch.from_numpy(songs).to(DEV)).cpu().numpy()
     assert out.shape == ref.shape == (24, 1, 128, 128)
-    err = np.abs(out - ref).max()
-    t32 = L.load_songs(songs, "gtzan", mode="torch32")
-    print("max |dlogmel| gpu vs f64:", err, " torch32 vs f64:", np.abs(t32 - ref).max())
-    assert err <= TOL_LOG
+    anchored(out, ref, L.load_songs(songs, "gtzan", mode="torch32"))
 
 
 def test_transform_wav_toy_matches_oracle():
@@ -40,7 +55,7 @@ def test_transform_wav_toy_matches_oracle():
     ref = L.transform_wav(wav.astype(np.float64), "toy", mode="f64")
     out = _loader("toy").transform_wav(torch.from_numpy(wav).to(DEV)).cpu().numpy()
     assert out.shape == (5, 1, 64, 64)
-    assert np.abs(out - ref).max() <= TOL_LOG
+    anchored(out, ref, L.transform_wav(wav, "toy", mode="torch32"))
 
 
 def test_linear_mel_error_relative_to_chunk_max():
@@ -63,7 +78,9 @@ def test_right_reflect_edge_and_all_frames():
     out = ld.transform_wav(torch.from_numpy(wav).to(DEV), clamp=False).cpu().numpy()
     mel = L.mel_spectrogram(wav.astype(np.float64), 480, 240, 64, 16000)
     ref = np.log10(mel + 1e-7)[..., 1:67].reshape(2, 1, 64, 66)
-    assert np.abs(out - ref).max() <= TOL_LOG
+    m32 = L.mel_spectrogram(wav, 480, 240, 64, 16000, mode="torch32")
+    t32 = np.log10(m32 + np.float32(1e-7))[..., 1:67].reshape(2, 1, 64, 66)
+    anchored(out, ref, t32)
 
 
 def test_clamp_and_quiet_input():
@@ -73,8 +90,7 @@ def test_clamp_and_quiet_input():
     out = ld.transform_wav(torch.from_numpy(wav).to(DEV)).cpu().numpy()
     ref = L.transform_wav(wav.astype(np.float64), "gtzan", mode="f64")
     assert (ref == -4).mean() > 0.2                  # the clamp is exercised
-    assert np.array_equal(out == -4, ref == -4) or np.abs(out - ref).max() <= TOL_LOG
-    assert np.abs(out - ref).max() <= TOL_LOG
+    anchored(out, ref, L.transform_wav(wav, "gtzan", mode="torch32"))
 
 
 def test_silent_chunk_is_nan_like_reference():
@@ -99,7 +115,7 @@ def test_batch_independence_large_batch():
         one = ld.load_songs(torch.from_numpy(songs[i:i + 1]).to(DEV))
         assert torch.equal(big[8 * i:8 * i + 8], one)
     ref = L.load_songs(songs[[5]], "gtzan", mode="f64")
-    assert np.abs(big[40:48].cpu().numpy() - ref).max() <= TOL_LOG
+    anchored(big[40:48].cpu().numpy(), ref, L.load_songs(songs[[5]], "gtzan", mode="torch32"))
 
 
 def test_feeds_the_explainer_end_to_end():
@@ -130,4 +146,6 @@ def test_n_fft_800_kernel_odd_shapes(n_mels, width, hop):
     out = ld.transform_wav(torch.from_numpy(wav).to(DEV), clamp=False).cpu().numpy()
     mel = L.mel_spectrogram(wav.astype(np.float64), 800, hop, n_mels, 16000)
     ref = np.log10(mel + 1e-7)[..., 1:width + 1].reshape(3, 1, n_mels, width)
-    assert np.abs(out - ref).max() <= TOL_LOG
+    m32 = L.mel_spectrogram(wav, 800, hop, n_mels, 16000, mode="torch32")
+    t32 = np.log10(m32 + np.float32(1e-7))[..., 1:width + 1].reshape(3, 1, n_mels, width)
+    anchored(out, ref, t32)

@@ -58,7 +58,7 @@ def test_lrp_stage_ops_equal_engine_buffers(ops):
     from drsa_audio_amd.utils.constants import LRP_NAME_MAP_GTZAN
     from drsa_audio_amd.xai.explain.explainer import HeatmapGenerator
     net = gtzan128().to(DEV)
-    hg = HeatmapGenerator(net, u64(), LRP_NAME_MAP_GTZAN, "blues", num_concepts=4, layer_idx=7)
+    hg = HeatmapGenerator(net, u64(), LRP_NAME_MAP_GTZAN, "blues", num_concepts=4, layer_idx=7, standard="sum")
     x = logmel(3, seed=7).to(DEV)
     hg.generate_subspace_heatmaps(x, to_host=False)
     eng = get_engine(hg.projectionmodel, hg.composite)
