@@ -69,9 +69,36 @@ def build(verbose: bool = True, jobs: int | None = None) -> str:
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
         os.replace(LIB + ".tmp", LIB)
+    build_torch_ops(hipcc)
     if verbose:
-        print(f"[drsa_amd] built {LIB} from {len(srcs)} sources")
+        print(f"[drsa_amd] built {LIB} from {len(srcs)} sources (+ {os.path.basename(TORCH_LIB)})")
     return LIB
+
+
+TORCH_SRC = os.path.join(HERE, "csrc_torch", "ops_torch.cpp")
+TORCH_LIB = os.path.join(LIBDIR, "libdrsa_amd_torch.so")
+
+
+def build_torch_ops(hipcc: str) -> str:
+    """The C++ TORCH_LIBRARY(drsa_amd) registration (csrc_torch/ops_torch.cpp): host code compiled
+    against the installed torch and linked to libdrsa_amd.so (rpath $ORIGIN)."""
+    deps = [TORCH_SRC, LIB, os.path.join(ROOT, "include", "drsa_amd.h")]
+    if os.path.exists(TORCH_LIB) and os.path.getmtime(TORCH_LIB) >= max(os.path.getmtime(d) for d in deps):
+        return TORCH_LIB
+    import torch
+    tdir = os.path.dirname(torch.__file__)
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    cmd = [hipcc, "-O2", "-std=c++17", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+           f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-I", os.path.join(tdir, "include"),
+           "-I", os.path.join(tdir, "include", "torch", "csrc", "api", "include"), "-I", os.path.join(ROOT, "include"),
+           "-Wno-deprecated-declarations", TORCH_SRC, "-o", TORCH_LIB + ".tmp", "-L", LIBDIR, "-ldrsa_amd",
+           "-L", os.path.join(tdir, "lib"), "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+           "-Wl,-rpath,$ORIGIN"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"torch op library build failed:\n{r.stderr[-6000:]}")
+    os.replace(TORCH_LIB + ".tmp", TORCH_LIB)
+    return TORCH_LIB
 
 
 if __name__ == "__main__":

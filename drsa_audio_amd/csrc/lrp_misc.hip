@@ -480,7 +480,10 @@ __global__ __launch_bounds__(256) void projection_bwd_kernel(
       }
     }
     __syncthreads();
-    for (int qi = 0; qi < nq; ++qi) {
+#ifndef DRSA_PROJ_DBG
+#define DRSA_PROJ_DBG 0
+#endif
+    for (int qi = 0; qi < ((DRSA_PROJ_DBG & 2) ? 0 : nq); ++qi) {   // ablation bit 2: no clone stage
       const int q = fanout == 1 ? qi : fanout == 2 ? qi + 1 : b % (K + 1);
       const int j0 = q == 0 ? 0 : (q - 1) * dk, j1 = q == 0 ? d : q * dk;
       const size_t orow = fanout ? (size_t)b * nq + qi : (size_t)b;
@@ -512,7 +515,11 @@ __global__ __launch_bounds__(256) void projection_bwd_kernel(
           } else {
             gq = (ax > 0.f) ? Rv : 0.f;
           }
+#if DRSA_PROJ_DBG & 1
+          if (cok && gq == 12345.f) G[(orow * d + c) * HW + pixl] = gq;   // ablation: no G stores
+#else
           if (cok) G[(orow * d + c) * HW + pixl] = gq;
+#endif
         }
       }
     }
@@ -661,7 +668,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
         }
     }
     __builtin_amdgcn_wave_barrier();
-    for (int qi = 0; qi < nq; ++qi) {
+#ifndef DRSA_PROJ_DBG
+#define DRSA_PROJ_DBG 0
+#endif
+    for (int qi = 0; qi < ((DRSA_PROJ_DBG & 2) ? 0 : nq); ++qi) {   // ablation bit 2: no clone stage
       const int q = fanout == 1 ? qi : fanout == 2 ? qi + 1 : b % (K + 1);
       const int j0 = q == 0 ? 0 : (q - 1) * dk, j1 = q == 0 ? d : q * dk;
       const size_t orow = fanout ? (size_t)b * nq + qi : (size_t)b;
@@ -694,7 +704,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
           } else {
             gq = (ax > 0.f) ? Rv : 0.f;
           }
+#if DRSA_PROJ_DBG & 1
+          if (cok && gq == 12345.f) G[(orow * d + c) * HW + pixl] = gq;   // ablation: no G stores
+#else
           if (cok) G[(orow * d + c) * HW + pixl] = gq;
+#endif
         }
     }
   }

@@ -23,12 +23,13 @@ _capi.call("drsa_amd_projection_residual", U.data_ptr(), D, P.data_ptr(), s)
 
 
 RC = os.environ.get("RC", "1") == "1"   # recompute h and a' (engine default) vs stored buffers
+FAN = int(os.environ.get("FAN", "2"))   # 2: K concept clones (the engine default since round 3); 1: K+1
 
 
 def run():
     _capi.call("drsa_amd_projection_bwd", g.data_ptr(), amax.data_ptr(), None if RC else ap.data_ptr(),
                None if RC else h.data_ptr(), a.data_ptr(),
-               den.data_ptr(), U.data_ptr(), P.data_ptr(), G.data_ptr(), B, D, H, W, K, 1e-6, 1e-7, 1, s)
+               den.data_ptr(), U.data_ptr(), P.data_ptr(), G.data_ptr(), B, D, H, W, K, 1e-6, 1e-7, FAN, s)
 
 
 for _ in range(3):

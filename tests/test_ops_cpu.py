@@ -35,7 +35,27 @@ def test_meta_shapes():
 
 
 def test_cpu_tensors_refused():
-    with pytest.raises(_capi.DrsaAmdError):
+    # no CPU kernel is registered: the dispatcher refuses (NotImplementedError is a RuntimeError)
+    with pytest.raises(RuntimeError):
         torch.ops.drsa_amd.drsa_step(torch.rand(10, 64), torch.rand(10, 64), torch.eye(64), 4)
-    with pytest.raises(_capi.DrsaAmdError):
+    with pytest.raises(RuntimeError):
         torch.ops.drsa_amd.polar(torch.eye(8))
+
+
+def test_ops_are_registered_from_cpp():
+    """The stage ops come from the C++ TORCH_LIBRARY(drsa_amd) of libdrsa_amd_torch.so (visible to
+    TorchScript / C++ callers), with a CUDA (HIP) kernel and no CPU kernel."""
+    for name in dops.__all__:
+        if name == "logmel":
+            continue
+        dump = torch._C._dispatch_dump(f"drsa_amd::{name}")
+        assert "ops_torch.cpp" in dump, (name, dump)
+        assert torch._C._dispatch_has_kernel_for_dispatch_key(f"drsa_amd::{name}", "CUDA"), name
+        assert not torch._C._dispatch_has_kernel_for_dispatch_key(f"drsa_amd::{name}", "CPU"), name
+
+
+def test_torchscript_sees_the_ops():
+    @torch.jit.script
+    def f(V: torch.Tensor) -> torch.Tensor:
+        return torch.ops.drsa_amd.polar(V)
+    assert "drsa_amd::polar" in str(f.graph)
