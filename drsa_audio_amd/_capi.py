@@ -55,6 +55,9 @@ SIGNATURES = {
     "drsa_amd_conv_fwd_den_ring": (_i32, [_fp, _fp, _fp, _fp, _fp, _vp, _fp, _i32, _i32, _i32, _i32, _i32, _vp]),
     "drsa_amd_conv_bwd_den_ring": (_i32, [_fp, _vp, _vp, _i32, _fp, _fp, _fp, _fp, _i32, _i32, _i32, _i32, _i32, _i32,
                                           _i32, _i32, _f32, _vp]),
+    "drsa_amd_conv_bwd_has_kernel_bf16_pw": (_i32, [_i32, _i32, _i32, _i32]),
+    "drsa_amd_conv_bwd_bf16_pw": (_i32, [_fp, _vp, _i32, _vp, _fp, _fp, _fp, _i32, _i32, _i32, _i32, _i32, _i32,
+                                         _i32, _i32, _f32, _vp]),
     "drsa_amd_conv_bwd_has_kernel_bf16": (_i32, [_i32, _i32, _i32, _i32, _i32]),
     "drsa_amd_linear_fwd": (_i32, [_fp, _fp, _fp, _fp, _fp, _i32, _i32, _i32, _vp]),
     "drsa_amd_linear_bwd": (_i32, [_fp, _ip, _i32, _fp, _i32, _i32, _f32, _fp, _fp, _i32, _fp, _i32, _f32, _fp,

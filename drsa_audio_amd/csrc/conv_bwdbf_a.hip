@@ -8,6 +8,7 @@ static const Entry kTableBwdBfA_e[] = {
     BWD_SET_BF(32, 32),
     BWD_SET_BF(64, 32),
     BWD_SET_BF(64, 64),
+    BWD_SET_BF_P4(64, 64),
 };
 extern const Table kTableBwdBfA = {kTableBwdBfA_e, (int)(sizeof(kTableBwdBfA_e) / sizeof(kTableBwdBfA_e[0]))};
 }  // namespace drsa_conv

@@ -157,6 +157,32 @@ int drsa_amd_conv_bwd_has_kernel_bf16(int cin, int cout, int W, int ng, int spar
   return find(pad32(cin), pad32(cout), W, ng, sparse ? A_POOLSPARSE : A_DENSE, EPI_BWD, 1) != nullptr;
 }
 
+int drsa_amd_conv_bwd_has_kernel_bf16_pw(int cin, int cout, int W, int pool_w) {
+  if (cin < 16 || (pool_w != 2 && pool_w != 4)) return 0;
+  return find(pad32(cin), pad32(cout), W, 1, A_POOLSPARSE, EPI_BWD, 1, pool_w) != nullptr;
+}
+
+int drsa_amd_conv_bwd_bf16_pw(const float* g, const uint8_t* g_amax, int pool_w, const uint16_t* wts, const float* x,
+                              const float* den, float* out, int Bq, int clones, int cin, int cout, int H, int W,
+                              int xmode, int post, float eps, void* stream) {
+  DRSA_REQUIRE(g_amax && (pool_w == 2 || pool_w == 4), "conv_bwd_bf16_pw: needs g_amax and pool_w 2 or 4");
+  DRSA_REQUIRE(Bq > 0 && clones > 0 && Bq % clones == 0, "conv_bwd_bf16_pw: bad batch/clones");
+  DRSA_REQUIRE(cin >= 16, "conv_bwd_bf16_pw: cin >= 16 (16-channel bf16 chunks)");
+  DRSA_REQUIRE(H % 2 == 0 && W % pool_w == 0 && W % 4 == 0, "conv_bwd_bf16_pw: H even, W %% pool_w == 0, W %% 4 == 0");
+  DRSA_REQUIRE(xmode == XM_NONE || x, "conv_bwd_bf16_pw: xmode needs x");
+  DRSA_REQUIRE(post == POST_NONE || (x && (den || post == POST_MASK)), "conv_bwd_bf16_pw: POST_DIV needs x and den");
+  DRSA_REQUIRE(((uintptr_t)wts & 15) == 0, "conv_bwd_bf16_pw: weights must be 16-byte aligned");
+  const Entry* e = find(pad32(cin), pad32(cout), W, 1, A_POOLSPARSE, EPI_BWD, 1, pool_w);
+  if (!e) {
+    drsa::set_error("conv_bwd_bf16_pw: no kernel for cin=%d cout=%d W=%d pool 2x%d", cin, cout, W, pool_w);
+    return DRSA_EUNSUPPORTED;
+  }
+  ConvArgs a{};
+  a.in = g; a.in_amax = g_amax; a.wts = reinterpret_cast<const float*>(wts); a.x = x; a.den = den; a.out = out;
+  a.H = H; a.W = W; a.cin = cin; a.cout = cout; a.clones = clones; a.xmode = xmode; a.post = post; a.eps = eps;
+  return launch(e, a, Bq, (hipStream_t)stream);
+}
+
 int drsa_amd_conv_bwd_bf16(const float* g, const uint8_t* g_amax, const uint16_t* wts, const float* x, const float* den,
                            float* out, int Bq, int clones, int cin, int cout, int H, int W, int ng, int xmode,
                            int post, float eps, void* stream) {

@@ -140,7 +140,9 @@ struct ConvCfg {
   static_assert(MT % WM == 0 && NT % WN == 0 && WM * WN <= 4, "wave split");
   static_assert(!BF || (CIC == 16 && (EPI < EPI_BWD ? AMODE == A_DENSE : EPI == EPI_BWD)),
                 "bf16: 16-channel chunks; dense forward, or the per-clone backward (dense or pool-sparse g)");
-  static_assert(PW == 2 || (PW == 4 && EPI == EPI_FWD_POOL), "2x4 pool windows: forward pool epilogue only");
+  static_assert(PW == 2 || (PW == 4 && (EPI == EPI_FWD_POOL || (EPI == EPI_BWD && ET == 1 && AMODE == A_POOLSPARSE))),
+                "2x4 pool windows: the forward pool epilogue, or the bf16 backward's pool-sparse staging");
+  static constexpr int PW_ = PW;
 };
 
 // ---- staging of one input-channel chunk: registers <- global (load), LDS <- registers
@@ -407,16 +409,50 @@ struct StagerBF {
   static constexpr int HXB = Cfg::HXB, NCH = CIN / 16;
   static constexpr int NITEM = 2 * HY * HX, IT = (NITEM + NT_ - 1) / NT_;
   static constexpr int NWQ = NG * 18 * COUT, WIT = (NWQ + NT_ - 1) / NT_;
-  float st_f[IT][8];
+  // (2,4) pool-sparse staging: one item per (channel half, halo row, pool cell): the cell's 8
+  // channel values and argmax bytes are loaded once and expanded to its 4 pixels at store time
+  // (the generic per-pixel item would load each cell 4 times)
+  static constexpr bool P4 = Cfg::AMODE_ == A_POOLSPARSE && Cfg::PW_ == 4;
+  static constexpr int NCR = Cfg::TW_ / 4 + 2;                 // cells per halo row (2 partial)
+  static constexpr int NITEM4 = 2 * HY * NCR, IT4 = (NITEM4 + NT_ - 1) / NT_;
+  static constexpr int ITX = P4 ? IT4 : IT;
+  float st_f[ITX][8];
+  uint32_t st_a[P4 ? IT4 : 1][2];
   uint4 st_w[WIT];
 
   __device__ __forceinline__ void load(const ConvArgs& a, int c0, int tid, int ty0, int tx0, int bq, int bs) {
     const int H = a.H, W = a.W;
     const size_t HW = (size_t)H * W;
-    if constexpr (Cfg::AMODE_ == A_POOLSPARSE) {
-      // backward input at 2x2-pool resolution + argmax byte (the pool backward): halo pixel
-      // (gy, gx) holds g[cell] where the cell's argmax is this pixel, else 0
-      const int H2 = H >> 1, W2 = W >> 1;
+    if constexpr (P4) {
+      const int H2 = H >> 1, W2 = W >> 2;
+      const size_t HW2 = (size_t)H2 * W2;
+#pragma unroll
+      for (int it = 0; it < IT4; ++it) {
+        const int i = tid + it * NT_;
+        const int cs = i % NCR, r = i / NCR, hy = r % HY, half = r / HY;
+        const int gy = ty0 - 1 + hy, cx = (tx0 >> 2) - 1 + cs, cb = c0 + 8 * half;
+        const bool ok = i < NITEM4 && gy >= 0 && gy < H && cx >= 0 && cx < W2;
+        const size_t cell = ok ? (size_t)(gy >> 1) * W2 + cx : 0;
+        const size_t base = ok ? ((size_t)bq * a.cin + cb) * HW2 + cell : 0;
+        const size_t abase = ok ? ((size_t)bs * a.cin + cb) * HW2 + cell : 0;
+        uint32_t ab[2] = {0u, 0u};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const bool okc = ok && cb + j < a.cin;
+          const float v = a.in[okc ? base + j * HW2 : 0];
+          const uint32_t am = a.in_amax[okc ? abase + j * HW2 : 0];
+          st_f[it][j] = okc ? v : 0.f;
+          ab[j >> 2] |= (okc ? am : 0xffu) << (8 * (j & 3));   // 0xff matches no pixel
+        }
+        st_a[it][0] = ab[0];
+        st_a[it][1] = ab[1];
+      }
+    } else if constexpr (Cfg::AMODE_ == A_POOLSPARSE) {
+      // backward input at 2 x PW pool resolution + argmax byte (the pool backward; PW = 4: the
+      // VGGish (2,4) pool, create_model.py:61): halo pixel (gy, gx) holds g[cell] where the cell's
+      // argmax (row-major window position) is this pixel, else 0
+      constexpr int PWB = Cfg::PW_;
+      const int H2 = H >> 1, W2 = W / PWB;
       const size_t HW2 = (size_t)H2 * W2;
 #pragma unroll
       for (int it = 0; it < IT; ++it) {
@@ -424,10 +460,10 @@ struct StagerBF {
         const int hx = i % HX, r = i / HX, hy = r % HY, half = r / HY;
         const int gy = ty0 - 1 + hy, gx = tx0 - 1 + hx, cb = c0 + 8 * half;
         const bool ok = i < NITEM && gy >= 0 && gy < H && gx >= 0 && gx < W;
-        const size_t cell = ok ? (size_t)(gy >> 1) * W2 + (gx >> 1) : 0;
+        const size_t cell = ok ? (size_t)(gy >> 1) * W2 + (gx / PWB) : 0;
         const size_t base = ok ? ((size_t)bq * a.cin + cb) * HW2 + cell : 0;
         const size_t abase = ok ? ((size_t)bs * a.cin + cb) * HW2 + cell : 0;
-        const uint32_t sub = (uint32_t)(((gy & 1) << 1) | (gx & 1));
+        const uint32_t sub = (uint32_t)((gy & 1) * PWB + (gx % PWB));
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const bool okc = ok && cb + j < a.cin;
@@ -463,8 +499,37 @@ struct StagerBF {
     }
   }
 
-  __device__ __forceinline__ void store(float* halo, float* wl, int tid) const {
+  __device__ __forceinline__ void store(float* halo, float* wl, int tid, int ty0 = 0, int tx0 = 0) const {
     uint4* hb = reinterpret_cast<uint4*>(halo);
+    if constexpr (P4) {
+#pragma unroll
+      for (int it = 0; it < IT4; ++it) {
+        const int i = tid + it * NT_;
+        if (i < NITEM4) {
+          const int cs = i % NCR, r = i / NCR, hy = r % HY;
+          const uint32_t rowsub = (uint32_t)(((ty0 - 1 + hy) & 1) * 4);
+          // cell cs covers halo columns 4 cs - 3 .. 4 cs (halo column hx = pixel tx0 - 1 + hx)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int hx = 4 * cs - 3 + e;
+            if (hx >= 0 && hx < HX) {
+              float v8[8];
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const uint32_t am = (st_a[it][j >> 2] >> (8 * (j & 3))) & 0xffu;
+                v8[j] = am == rowsub + (uint32_t)e ? st_f[it][j] : 0.f;
+              }
+              uint4 q;
+              q.x = pack_bf16x2(v8[0], v8[1]);
+              q.y = pack_bf16x2(v8[2], v8[3]);
+              q.z = pack_bf16x2(v8[4], v8[5]);
+              q.w = pack_bf16x2(v8[6], v8[7]);
+              hb[r * HXB + hx] = q;
+            }
+          }
+        }
+      }
+    } else {
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
       const int i = tid + it * NT_;
@@ -477,6 +542,7 @@ struct StagerBF {
         q.w = pack_bf16x2(st_f[it][6], st_f[it][7]);
         hb[r * HXB + hx] = q;   // r = half * HY + hy
       }
+    }
     }
     uint4* wb = reinterpret_cast<uint4*>(wl);
 #pragma unroll
@@ -622,7 +688,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
   // addressing is set up, so that none of it is live across the loop)
   for (int chunk = 0; chunk + (EPI == EPI_BWD ? 1 : 0) < Cfg::NCHUNK; ++chunk) {
     __syncthreads();
-    stg.store(halo, wl, tid);
+    if constexpr (Cfg::BF) stg.store(halo, wl, tid, ty0, tx0);
+    else stg.store(halo, wl, tid);
     __syncthreads();
     if (chunk + 1 < Cfg::NCHUNK) stg.load(a, (chunk + 1) * CIC, tid, ty0, tx0, bq, bs);
     if (!active || (a.dbg & 4)) continue;
@@ -684,7 +751,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
     // last chunk, peeled: the staging registers are free, so the epilogue's first x loads go
     // out here and their latency hides under the MFMAs (den too would spill: measured slower)
     __syncthreads();
-    stg.store(halo, wl, tid);
+    if constexpr (Cfg::BF) stg.store(halo, wl, tid, ty0, tx0);
+    else stg.store(halo, wl, tid);
     __syncthreads();
     epi_loads(0, 0, pre_x, pre_d, true, DRSA_CONV_PRE_D, 0, kPreN);
 
@@ -1039,6 +1107,16 @@ struct Entry {
   CONV_ENTRY_BFA(CIN, COUT, 8, 32, 8, 1, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD),           \
   CONV_ENTRY_BFA(CIN, COUT, 8, 16, 8, 1, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD),           \
   CONV_ENTRY_BFA(CIN, COUT, 8, 8, 4, 1, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD)
+
+// bf16-operand per-clone backward with g at (2,4)-pool resolution (VGGish block 1)
+#define CONV_ENTRY_BFA_P4(CIN, COUT, TH, TW, MW)                                                           \
+  drsa_conv::Entry{CIN, COUT, TH, TW, MW, 16, 1, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD,              \
+                   drsa_conv::conv3x3_kernel<CIN, COUT, TH, TW, MW, 16, 1, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD, 1, 4>, \
+                   drsa_conv::ConvCfg<CIN, COUT, TH, TW, MW, 16, 1, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD, 1, 4>::lds_floats * sizeof(float), 1, 4}
+#define BWD_SET_BF_P4(CIN, COUT)                       \
+  CONV_ENTRY_BFA_P4(CIN, COUT, 8, 32, 8),              \
+  CONV_ENTRY_BFA_P4(CIN, COUT, 8, 16, 8),              \
+  CONV_ENTRY_BFA_P4(CIN, COUT, 8, 8, 4)
 
 #define CONV_ENTRY_BF(CIN, COUT, TH, TW, MW, NG, EP)                                                     \
   drsa_conv::Entry{CIN, COUT, TH, TW, MW, 16, NG, drsa_conv::A_DENSE, EP,                                 \

@@ -53,6 +53,9 @@ _PROJ_STORE = os.environ.get("DRSA_AMD_PROJ_STORE", "0") == "1"
 # everywhere and the next backward reads it there (POST_DIV) instead of the ring form (POST_DIV_RING:
 # the copy on the image's border ring only, the map's per-channel interior value elsewhere)
 _DEN_COPY = os.environ.get("DRSA_AMD_DEN_COPY", "0") == "1"
+# A/B switch: 0 = the (2,4) pool backward as a separate unpool (maxpool_bwd) before a dense-g bf16
+# backward conv, instead of folded into its pool-sparse staging (drsa_amd_conv_bwd_bf16_pw)
+_POOL24_SPARSE = os.environ.get("DRSA_AMD_BF16_POOL24_SPARSE", "1") == "1"
 
 
 def _pad32(c: int) -> int:
@@ -672,6 +675,7 @@ class LRPEngine:
             st, rec = self.stages[li], st0["stages"][li]
             h, w = rec["H"], rec["W"]
             amax_in = None
+            pool_w = 2          # pool width of a pool-sparse g (4: VGGish (2,4), bf16 backward)
             if st.proj is not None:
                 P = st.proj
                 K = P.K if P.mask else P.K
@@ -690,6 +694,12 @@ class LRPEngine:
                 g, clones, Bq = G, nq, B * nq
             elif st.pool and st.pool_k == (2, 2):
                 amax_in = rec["amax"]
+            elif (_POOL24_SPARSE and st.pool and st.pool_k == (2, 4) and st.wts_bwd_bf is not None
+                  and st.den_kind != "ab" and li > 0
+                  and self._post_for(li - 1)[0] != POST_DIV_RING
+                  and _capi.lib().drsa_amd_conv_bwd_has_kernel_bf16_pw(st.cout, st.cin, w, 4)):
+                # the (2,4) pool backward folded into the bf16 backward's staging (no unpooled g)
+                amax_in, pool_w = rec["amax"], 4
             elif st.pool:
                 ph, pw = st.pool_k
                 gf = self._buf((li, "g_unpool"), (Bq, st.cout, h, w))
@@ -733,6 +743,13 @@ class LRPEngine:
                            (st.wts_bwd_bf if bf else st.wts_bwd).data_ptr(), 1 if bf else 0, x_in.data_ptr(),
                            den["den"].data_ptr(), den["den_const4"].data_ptr(), out.data_ptr(), Bq, clones, st.cout,
                            st.cin, h, w, st.ng_bwd, st.xmode_bwd, float(eps), s)
+            elif pool_w == 4:
+                out = self._buf((li, "R"), (Bq, st.cin, h, w))
+                self._call(f"conv_bwd:{st.name}", "drsa_amd_conv_bwd_bf16_pw", g.data_ptr(), amax_in.data_ptr(), 4,
+                           st.wts_bwd_bf.data_ptr(),
+                           x_in.data_ptr() if (st.xmode_bwd != XM_NONE or post != POST_NONE) else None,
+                           _capi.ptr(den), out.data_ptr(), Bq, clones, st.cout, st.cin, h, w, st.xmode_bwd, post,
+                           float(eps), s)
             else:
                 out = self._buf((li, "R"), (Bq, st.cin, h, w))
                 bf = st.wts_bwd_bf is not None and _capi.lib().drsa_amd_conv_bwd_has_kernel_bf16(

@@ -173,6 +173,15 @@ int drsa_amd_conv_bwd_bf16(const float* g, const uint8_t* g_amax, const uint16_t
                            float* out, int Bq, int clones, int cin, int cout, int H, int W, int ng, int xmode,
                            int post, float eps, void* stream);
 
+/* drsa_amd_conv_bwd_bf16 with g at 2 x pool_w max-pool resolution (pool_w = 4: the VGGish (2,4)
+ * pool of block 1, create_model.py:61; pool_w = 2 is drsa_amd_conv_bwd_bf16 with g_amax): the pool
+ * backward is folded into the staging (each halo pixel takes its cell's g where the cell's argmax
+ * byte, row * pool_w + col, names it), so no unpooled g is written or read.  ng = 1. */
+int drsa_amd_conv_bwd_has_kernel_bf16_pw(int cin, int cout, int W, int pool_w);
+int drsa_amd_conv_bwd_bf16_pw(const float* g, const uint8_t* g_amax, int pool_w, const uint16_t* wts, const float* x,
+                              const float* den, float* out, int Bq, int clones, int cin, int cout, int H, int W,
+                              int xmode, int post, float eps, void* stream);
+
 /* WSquare / Flat first layer under a 2x2 max-pool, with its denominator map split for the next
  * backward (zennit WSquare/Flat: den = conv(1; W^2, b^2); constants.py:29 puts
  * WSquare on the first layer).  Such a map holds one value per channel on every pixel off its

@@ -97,6 +97,56 @@ def test_conv_bwd_bf16_kernel(cin, cout, sparse, W):
             assert torch.all((o - ref).abs() <= b2), (cin, cout, sparse, W)
 
 
+@pytest.mark.parametrize("cin,cout,W", [(64, 64, 256), (64, 64, 32), (64, 64, 16), (64, 64, 8)])
+def test_conv_bwd_bf16_pool24_sparse_equals_unpooled_dense(cin, cout, W):
+    """The (2,4) pool backward folded into the staging (drsa_amd_conv_bwd_bf16_pw, pool_w = 4) gives
+    exactly the dense kernel on the unpooled g (drsa_amd_relevance_unpool): the same bf16 operands
+    reach the same MFMA chain."""
+    lib = _capi.lib()
+    assert lib.drsa_amd_conv_bwd_has_kernel_bf16_pw(cin, cout, W, 4) == 1
+    gen = torch.Generator().manual_seed(cin + W)
+    B, clones, H = 2, 3, 16
+    Bq = B * clones
+    Wc = torch.randn(cout, cin, 3, 3, generator=gen) / (9 * cin) ** 0.5
+    wb = _bf16_layout(_layout(_r(Wc), _pad32(cin), _pad32(cout))[None], _pad32(cin), _pad32(cout)).to(DEV)
+    gp = torch.randn(Bq, cin, H // 2, W // 4, generator=gen).to(DEV)
+    am = torch.randint(0, 8, (B, cin, H // 2, W // 4), generator=gen, dtype=torch.uint8).to(DEV)
+    x = torch.randn(B, cout, H, W, generator=gen).clamp(min=0).to(DEV)
+    den = torch.randn(B, cout, H, W, generator=gen).to(DEV)
+    gd = torch.empty(Bq, cin, H, W, device=DEV)
+    s = _capi.stream_ptr()
+    _capi.call("drsa_amd_relevance_unpool", gp.data_ptr(), am.data_ptr(), Bq, clones, cin, H, W, 2, 4, gd.data_ptr(), s)
+    for xm, post in ((XM_NONE, POST_NONE), (XM_MUL, POST_DIV)):
+        o_ref = torch.full((Bq, cout, H, W), -9.0, device=DEV)
+        o_sp = torch.full_like(o_ref, -7.0)
+        _capi.call("drsa_amd_conv_bwd_bf16", gd.data_ptr(), None, wb.data_ptr(), x.data_ptr() if xm else None,
+                   den.data_ptr() if post else None, o_ref.data_ptr(), Bq, clones, cin, cout, H, W, 1, xm, post, 1e-6, s)
+        _capi.call("drsa_amd_conv_bwd_bf16_pw", gp.data_ptr(), am.data_ptr(), 4, wb.data_ptr(),
+                   x.data_ptr() if xm else None, den.data_ptr() if post else None, o_sp.data_ptr(), Bq, clones, cin,
+                   cout, H, W, xm, post, 1e-6, s)
+        torch.cuda.synchronize()
+        assert torch.equal(o_sp, o_ref), (xm, post)
+
+
+def test_vggish_bf16_backward_pool24_fold_equals_unpool(monkeypatch):
+    """Plan level: VGGish-BN standard LRP on the bf16-backward plan with the (2,4) pool backward
+    folded into conv_bwd:features.3 equals the plan with the separate unpool, bit for bit."""
+    import drsa_audio_amd.engine.plan as plan
+    from drsa_audio_amd.engine import clear_cache
+    from drsa_audio_amd.xai.explain.attribute import compute_relevances
+    monkeypatch.setenv("DRSA_AMD_BF16_BACKWARD", "1")
+    net = vggish().bfloat16().to(DEV)
+    x = logmel(2, 128, 256, seed=4).bfloat16().to(DEV)
+    comp = NameMapComposite(LRP_NAME_MAP_VGGISH, canonizers=[SequentialMergeBatchNorm()])
+    outs = []
+    for fold in (True, False):
+        monkeypatch.setattr(plan, "_POOL24_SPARSE", fold)
+        clear_cache()
+        outs.append(compute_relevances(net, x, comp, class_idx=3).cpu())
+    clear_cache()
+    assert torch.equal(outs[0], outs[1])
+
+
 def _rel(R, Rref):
     return [float((R[b].double() - Rref[b]).norm() / Rref[b].norm()) for b in range(R.size(0))]
 
