@@ -55,6 +55,8 @@ SIGNATURES = {
     "drsa_amd_conv_fwd_den_ring": (_i32, [_fp, _fp, _fp, _fp, _fp, _vp, _fp, _i32, _i32, _i32, _i32, _i32, _vp]),
     "drsa_amd_conv_bwd_den_ring": (_i32, [_fp, _vp, _vp, _i32, _fp, _fp, _fp, _fp, _i32, _i32, _i32, _i32, _i32, _i32,
                                           _i32, _i32, _f32, _vp]),
+    "drsa_amd_conv_bwd_den_map": (_i32, [_fp, _vp, _i32, _vp, _i32, _fp, _fp, _fp, _i32, _i32, _i32, _i32, _i32, _i32,
+                                         _i32, _i32, _f32, _vp]),
     "drsa_amd_conv_bwd_has_kernel_bf16_pw": (_i32, [_i32, _i32, _i32, _i32]),
     "drsa_amd_conv_bwd_bf16_pw": (_i32, [_fp, _vp, _i32, _vp, _fp, _fp, _fp, _i32, _i32, _i32, _i32, _i32, _i32,
                                          _i32, _i32, _f32, _vp]),
@@ -92,6 +94,7 @@ class DrsaProblem(C.Structure):
 
 XM_NONE, XM_MUL, XM_SPLIT = 0, 1, 2
 POST_NONE, POST_DIV, POST_MASK, POST_DIV_RING = 0, 1, 2, 3
+POST_DIV_MAP = 4   # host-side plan tag only: POST_DIV on an input-independent map (drsa_amd_conv_bwd_den_map)
 
 
 class DrsaAmdError(RuntimeError):

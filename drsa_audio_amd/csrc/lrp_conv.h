@@ -26,6 +26,7 @@ struct ConvArgs {
   int xmode, post;
   float eps;
   int den_ring_only;        // forward (first layer, map den): write out_den on the ring groups only
+  int den_shared;           // backward POST_DIV: den is one [cout][H][W] plane for every sample
   int dbg;                  // ablation only (DRSA_AMD_CONV_DBG): 1 no staging loads, 2 no epilogue I/O, 4 no MFMA
 };
 

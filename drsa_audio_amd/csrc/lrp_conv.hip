@@ -183,6 +183,33 @@ int drsa_amd_conv_bwd_bf16_pw(const float* g, const uint8_t* g_amax, int pool_w,
   return launch(e, a, Bq, (hipStream_t)stream);
 }
 
+int drsa_amd_conv_bwd_den_map(const float* g, const uint8_t* g_amax, int pool_w, const void* wts, int wts_bf16,
+                              const float* x, const float* den_map, float* out, int Bq, int clones, int cin, int cout,
+                              int H, int W, int ng, int xmode, float eps, void* stream) {
+  DRSA_REQUIRE(Bq > 0 && clones > 0 && Bq % clones == 0, "conv_bwd_den_map: bad batch/clones");
+  DRSA_REQUIRE(x && den_map, "conv_bwd_den_map: needs x and den_map");
+  DRSA_REQUIRE(!g_amax || pool_w == 2 || pool_w == 4, "conv_bwd_den_map: pool_w must be 2 or 4");
+  DRSA_REQUIRE(H % 2 == 0 && W % 4 == 0, "conv_bwd_den_map: H must be even and W %% 4 == 0 (got %dx%d)", H, W);
+  DRSA_REQUIRE(xmode == XM_NONE || xmode == XM_MUL || xmode == XM_SPLIT, "conv_bwd_den_map: bad xmode");
+  const int et = wts_bf16 ? 1 : 0;
+  DRSA_REQUIRE(!et || (ng == 1 && cin >= 16 && ((uintptr_t)wts & 15) == 0),
+               "conv_bwd_den_map: bf16 weights need ng == 1, cin >= 16 and 16-byte alignment");
+  DRSA_REQUIRE(et || (ng >= 1 && ng <= 2 && (!g_amax || pool_w == 2)),
+               "conv_bwd_den_map: fp32 weights need ng 1..2 and a 2x2 pool");
+  const int pw = g_amax ? pool_w : 2;
+  const Entry* e = find(pad32(cin), pad32(cout), W, ng, g_amax ? A_POOLSPARSE : A_DENSE, EPI_BWD, et, pw);
+  if (!e) {
+    drsa::set_error("conv_bwd_den_map: no kernel for cin=%d cout=%d W=%d ng=%d sparse=%d bf16=%d pool_w=%d", cin, cout,
+                    W, ng, g_amax != nullptr, et, pw);
+    return DRSA_EUNSUPPORTED;
+  }
+  ConvArgs a{};
+  a.in = g; a.in_amax = g_amax; a.wts = reinterpret_cast<const float*>(wts); a.x = x; a.den = den_map;
+  a.den_shared = 1; a.out = out; a.H = H; a.W = W; a.cin = cin; a.cout = cout; a.clones = clones; a.xmode = xmode;
+  a.post = POST_DIV; a.eps = eps;
+  return launch(e, a, Bq, (hipStream_t)stream);
+}
+
 int drsa_amd_conv_bwd_bf16(const float* g, const uint8_t* g_amax, const uint16_t* wts, const float* x, const float* den,
                            float* out, int Bq, int clones, int cin, int cout, int H, int W, int ng, int xmode,
                            int post, float eps, void* stream) {

@@ -706,7 +706,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
   const int HW = H * W;
   const size_t pix = pix_ok ? (size_t)(ty0 + py) * W + tx0 + px : 0;
   const float* xs = a.x ? a.x + (size_t)bs * a.cout * HW + pix : nullptr;
-  const float* ds = a.den ? a.den + (size_t)bs * a.cout * HW + pix : nullptr;
+  // den_shared: the next layer's denominator is an input-independent map [cout][H][W] (WSquare /
+  // Flat without a pool between): every sample reads the same plane (L2-resident), nothing per sample
+  const float* ds = a.den ? a.den + (a.den_shared ? (size_t)0 : (size_t)bs * a.cout * HW) + pix : nullptr;
   float* oqp = a.out + (size_t)bq * a.cout * HW + pix;
   // x and den come from clamped, always valid addresses (den falls back to x or out when the
   // mode does not use it) and are ALL issued before any arithmetic; the rule / post modes are

@@ -573,18 +573,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
     const int pl = w * 16 + pc;
     const int py = y0 + pl / TW, px = x0 + pl % TW;
     const size_t pixl = (size_t)py * W + px;
-    // a (and den) at rows c = i*16 + 4 rg + r: the output layout of every GEMM below
-    float av[NB * 4], dv[PF ? NB * 4 : 1];
+    // a at rows c = i*16 + 4 rg + r: the output layout of every GEMM below; the relevance R at a'
+    // (pool backward folded in) is loaded here too, so its latency hides under the h GEMM (it is
+    // first needed after the a' GEMM); den follows after the a' GEMM (needed by the clones only)
+    float av[NB * 4], dv[PF ? NB * 4 : 1], Rv0[NB * 4];
 #pragma unroll
     for (int i = 0; i < NB; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int c = i * 16 + rg * 4 + r;
         const bool ok = c < d;
-        const size_t os = ((size_t)b * d + (ok ? c : 0)) * HW + pixl;
+        const int cc = ok ? c : 0;
+        const size_t os = ((size_t)b * d + cc) * HW + pixl;
         const float aa = a[os];
         av[i * 4 + r] = ok ? aa : 0.f;
-        if constexpr (PF) dv[i * 4 + r] = has_den ? den[os] : 1.f;
+        if (sparse) {
+          const size_t q = ((size_t)b * d + cc) * H2 * W2 + (py >> 1) * W2 + (px >> 1);
+          const float gv = gp[q];   // unconditional load, then the argmax select
+          Rv0[i * 4 + r] = (amax[q] == (((py & 1) << 1) | (px & 1))) ? gv : 0.f;
+        } else {
+          Rv0[i * 4 + r] = gp[os];
+        }
       }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -631,18 +640,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
         for (int r = 0; r < 4; ++r) {
           const int c = cb * 16 + rg * 4 + r;
           const bool ok = c < d;
-          const int cc = ok ? c : 0;
-          float R;
-          if (sparse) {
-            const size_t q = ((size_t)b * d + cc) * H2 * W2 + (py >> 1) * W2 + (px >> 1);
-            const float gv = gp[q];   // unconditional load, then the argmax select
-            R = (amax[q] == (((py & 1) << 1) | (px & 1))) ? gv : 0.f;
-          } else {
-            R = gp[((size_t)b * d + cc) * HW + pixl];
-          }
+          const float R = Rv0[cb * 4 + r];
           const float apv = av[cb * 4 + r] + acc[cb][r];
           const float v = R / stab(apv, eps_proj);
           RA[c * PW + pc] = ok ? v : 0.f;
+        }
+    }
+    if constexpr (PF) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = i * 16 + rg * 4 + r;
+          const size_t os = ((size_t)b * d + (c < d ? c : 0)) * HW + pixl;
+          dv[i * 4 + r] = has_den ? den[os] : 1.f;
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -720,55 +731,105 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
 //   G from pool-sparse (gp, argmax) or dense; 16 x 64 output tile, 4 pixels per thread
 // ===========================================================================
 constexpr int FL_TH = 16, FL_TW = 64, FL_CC = 8;
+constexpr int FL_HY = FL_TH + 2, FL_RS = FL_TW + 8;           // LDS row: halo col 3, interior 4..67, halo 68
+constexpr int FL_ROWS = FL_CC * FL_HY;                        // staged rows per channel group
+constexpr int FL_NV4 = FL_ROWS * (FL_TW / 4);                 // interior float4 per group
+constexpr int FL_IV = (FL_NV4 + 255) / 256, FL_IH = (FL_ROWS * 2 + 255) / 256;
 
-__global__ __launch_bounds__(256) void first_layer_bwd_kernel(const float* __restrict__ g, const uint8_t* __restrict__ amax,
-                                                              const float* __restrict__ w2, float* __restrict__ out,
-                                                              int C, int H, int W, int clones) {
-  constexpr int HY = FL_TH + 2, HX = FL_TW + 2, RS = FL_TW + 4;
-  __shared__ float hal[FL_CC][HY][RS];
-  __shared__ float wsh[FL_CC][9];
+// Each thread owns 4 adjacent output pixels of one row.  A channel group's g tile (+1 halo) is
+// loaded as coalesced float4 rows (all of a thread's loads issued back to back into registers, the
+// next group's while the current one is consumed), then written to LDS; the chain per output pixel
+// is (channel, dy, dx), the order of oracle/lrp_exact.c and of the pooled kernel below.
+template <bool VEC>
+__global__ __launch_bounds__(256) void first_layer_bwd_kernel(const float* __restrict__ g, const float* __restrict__ w2,
+                                                              float* __restrict__ out, int C, int H, int W) {
+  __shared__ __attribute__((aligned(16))) float hal[FL_CC][FL_HY][FL_RS];
   const int tid = threadIdx.x;
   const int tiles_x = (W + FL_TW - 1) / FL_TW;
   const int ty0 = (blockIdx.x / tiles_x) * FL_TH, tx0 = (blockIdx.x % tiles_x) * FL_TW;
-  const int bq = blockIdx.y, bs = bq / clones;
+  const int bq = blockIdx.y;
   const int ly = tid / 16, lx = (tid % 16) * 4;   // 16 rows x 16 threads, 4 px each
+  const size_t plane = (size_t)H * W;
+  const float* gb = g + (size_t)bq * C * plane;
+  float4 rv[FL_IV];
+  float rh[FL_IH];
+  // loads from clamped (always valid) addresses, masked afterwards
+  auto fetch = [&](int c0) {
+#pragma unroll
+    for (int it = 0; it < FL_IV; ++it) {
+      const int i = tid + it * 256;
+      const int row = i / (FL_TW / 4), q = i % (FL_TW / 4);
+      const int ci = row / FL_HY, hy = row % FL_HY;
+      const int gy = ty0 - 1 + hy, gx = tx0 + 4 * q, c = c0 + ci;
+      const bool rok = i < FL_NV4 && c < C && gy >= 0 && gy < H;
+      if constexpr (VEC) {
+        const bool ok = rok && gx < W;
+        const float4 v = *reinterpret_cast<const float4*>(gb + (ok ? c * plane + (size_t)gy * W + gx : 0));
+        rv[it] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        float e[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const bool ok = rok && gx + k < W;
+          const float v = gb[ok ? c * plane + (size_t)gy * W + gx + k : 0];
+          e[k] = ok ? v : 0.f;
+        }
+        rv[it] = make_float4(e[0], e[1], e[2], e[3]);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < FL_IH; ++it) {
+      const int i = tid + it * 256;
+      const int row = i >> 1, side = i & 1;
+      const int ci = row / FL_HY, hy = row % FL_HY;
+      const int gy = ty0 - 1 + hy, gx = side ? tx0 + FL_TW : tx0 - 1, c = c0 + ci;
+      const bool ok = i < FL_ROWS * 2 && c < C && gy >= 0 && gy < H && gx >= 0 && gx < W;
+      const float v = gb[ok ? c * plane + (size_t)gy * W + gx : 0];
+      rh[it] = ok ? v : 0.f;
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int it = 0; it < FL_IV; ++it) {
+      const int i = tid + it * 256;
+      if (i < FL_NV4) {
+        const int row = i / (FL_TW / 4), q = i % (FL_TW / 4);
+        *reinterpret_cast<float4*>(&hal[row / FL_HY][row % FL_HY][4 + 4 * q]) = rv[it];
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < FL_IH; ++it) {
+      const int i = tid + it * 256;
+      if (i < FL_ROWS * 2) {
+        const int row = i >> 1, side = i & 1;
+        hal[row / FL_HY][row % FL_HY][side ? 4 + FL_TW : 3] = rh[it];
+      }
+    }
+  };
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  const int H2 = H / 2, W2 = W / 2;
+  fetch(0);
   for (int c0 = 0; c0 < C; c0 += FL_CC) {
     __syncthreads();
-    for (int idx = tid; idx < FL_CC * HY * HX; idx += 256) {
-      const int ci = idx / (HY * HX), rem = idx % (HY * HX);
-      const int hy = rem / HX, hx = rem % HX;
-      const int gy = ty0 - 1 + hy, gx = tx0 - 1 + hx, c = c0 + ci;
-      float v = 0.f;
-      if (c < C && gy >= 0 && gy < H && gx >= 0 && gx < W) {
-        if (amax) {
-          const size_t q = (((size_t)bq * C + c) * H2 + (gy >> 1)) * W2 + (gx >> 1);
-          const size_t qa = (((size_t)bs * C + c) * H2 + (gy >> 1)) * W2 + (gx >> 1);
-          v = (amax[qa] == (((gy & 1) << 1) | (gx & 1))) ? g[q] : 0.f;
-        } else {
-          v = g[(((size_t)bq * C + c) * H + gy) * W + gx];
-        }
-      }
-      hal[ci][hy][hx] = v;
-    }
-    for (int idx = tid; idx < FL_CC * 9; idx += 256) {
-      const int ci = idx / 9, t = idx % 9;
-      wsh[ci][t] = (c0 + ci < C) ? w2[(c0 + ci) * 9 + t] : 0.f;
-    }
+    stage();
     __syncthreads();
-#pragma unroll
+    if (c0 + FL_CC < C) fetch(c0 + FL_CC);
+#pragma unroll 2
     for (int ci = 0; ci < FL_CC; ++ci) {
+      // channels past C were staged as zeros: fma(0, w, acc) == acc, so any finite weight will do
+      const int c = min(c0 + ci, C - 1);
+      float wv[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) wv[t] = w2[c * 9 + t];
 #pragma unroll
       for (int dy = -1; dy <= 1; ++dy) {
-        float row[6];
-#pragma unroll
-        for (int e = 0; e < 6; ++e) row[e] = hal[ci][ly + 1 + dy][lx + e];
+        const float* r = &hal[ci][ly + 1 + dy][3 + lx];      // pixel tx0 + lx - 1 ..
+        const float4 m = *reinterpret_cast<const float4*>(r + 1);
+        const float row[6] = {r[0], m.x, m.y, m.z, m.w, r[5]};
 #pragma unroll
         for (int dx = -1; dx <= 1; ++dx) {
-          const float wv = wsh[ci][(1 - dy) * 3 + (1 - dx)];
+          const float wt = wv[(1 - dy) * 3 + (1 - dx)];
 #pragma unroll
-          for (int p = 0; p < 4; ++p) acc[p] = fmaf(row[p + 1 + dx], wv, acc[p]);
+          for (int p = 0; p < 4; ++p) acc[p] = fmaf(row[p + 1 + dx], wt, acc[p]);
         }
       }
     }
@@ -1270,6 +1331,7 @@ int proj_p_lds_env() {
   return v;
 }
 bool proj_p_lds_fwd() { return proj_p_lds_env() == 1; }
+
 bool proj_p_lds_bwd() { return proj_p_lds_env() == 1; }
 
 }  // namespace
@@ -1418,8 +1480,10 @@ int drsa_amd_first_layer_bwd(const float* g, const uint8_t* amax, const float* w
                        C, H, W, clones);
   } else {
     const dim3 grid(((H + FL_TH - 1) / FL_TH) * ((W + FL_TW - 1) / FL_TW), Bq);
-    hipLaunchKernelGGL(first_layer_bwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, g, amax, w2f, out, C, H, W,
-                       clones);
+    if (W % 4 == 0)
+      hipLaunchKernelGGL(first_layer_bwd_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, g, w2f, out, C, H, W);
+    else
+      hipLaunchKernelGGL(first_layer_bwd_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, g, w2f, out, C, H, W);
   }
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;

@@ -61,6 +61,8 @@ constexpr size_t ns_scratch_floats() {
   return ns_ks<DP>() == 1 ? 0 : (size_t)(DP / 32) * (DP / 32) * ns_ks<DP>() * 1024;
 }
 
+// (So the caller's tol does not bound the returned U after such a last update; the bound below does,
+// and the tests gate the result's orthogonality directly.)
 // Stop after the update once DP * err (a bound on the spectral error e = |1 - sigma^2|; loose by
 // ~sqrt(DP) for the spread-out errors of V = U + G) is below this: the update then leaves at most
 // 0.75 e^2 (1 + e/3) < 7.6e-5.  1e-2 instead of 1e-4 saves one Newton-Schulz iteration per step

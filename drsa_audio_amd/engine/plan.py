@@ -42,7 +42,7 @@ import torch
 import torch.nn as nn
 
 from .. import _capi
-from .._capi import POST_DIV, POST_DIV_RING, POST_MASK, POST_NONE, XM_MUL, XM_NONE, XM_SPLIT
+from .._capi import POST_DIV, POST_DIV_MAP, POST_DIV_RING, POST_MASK, POST_NONE, XM_MUL, XM_NONE, XM_SPLIT
 from ..zennit import rules as R
 from ..zennit.canonizers import SequentialMergeBatchNorm
 
@@ -559,9 +559,14 @@ class LRPEngine:
                 cur, h, w = out, h // ph, w // pw
             else:
                 a = self._buf((li, "a"), (B, st.cout, h, w))
-                den = self._buf((li, "den"), (B, st.cout, h, w)) if need_den else None
+                # WSquare / Flat without a pool after it (VGGish conv0 -> conv3): the per-sample
+                # denominator IS the input-independent map; the next backward reads the map itself
+                # (drsa_amd_conv_bwd_den_map), no per-sample copy is written
+                shared = (st.den_kind == "map" and st.proj is None and li + 1 < len(self.stages)
+                          and self.stages[li + 1].den_kind != "ab" and not _DEN_COPY)
+                den = self._buf((li, "den"), (B, st.cout, h, w)) if need_den and not shared else None
                 self._conv_fwd(f"conv_fwd:{st.name}", st, False, cur, den_map, a, None, den, B, h, w, st.ng_fwd, 0, s)
-                rec.update(a=a, den=den)
+                rec.update(a=a, den=den, den_map_shared=den_map if shared else None)
                 if st.den_kind == "ab":
                     den_n = self._buf((li, "den_n"), (B, st.cout, h, w))
                     self._conv_fwd(f"conv_fwd_n:{st.name}", st, True, cur, None, a, None, den_n, B, h, w, 2, 0, s)
@@ -618,6 +623,8 @@ class LRPEngine:
             return POST_NONE, None, 0.0
         if st.den_kind is None or st.den_kind == "ab":
             return POST_MASK, None, 0.0
+        if rec.get("den_map_shared") is not None:
+            return POST_DIV_MAP, rec["den_map_shared"], st.eps
         if rec.get("den_const4") is not None:
             return POST_DIV_RING, rec, st.eps        # den = rec["den"] on the ring, rec["den_const4"] elsewhere
         return POST_DIV, rec["den"], st.eps
@@ -743,6 +750,15 @@ class LRPEngine:
                            (st.wts_bwd_bf if bf else st.wts_bwd).data_ptr(), 1 if bf else 0, x_in.data_ptr(),
                            den["den"].data_ptr(), den["den_const4"].data_ptr(), out.data_ptr(), Bq, clones, st.cout,
                            st.cin, h, w, st.ng_bwd, st.xmode_bwd, float(eps), s)
+            elif post == POST_DIV_MAP:
+                out = self._buf((li, "R"), (Bq, st.cin, h, w))
+                bf = st.wts_bwd_bf is not None and (
+                    _capi.lib().drsa_amd_conv_bwd_has_kernel_bf16_pw(st.cout, st.cin, w, pool_w) if amax_in is not None
+                    else _capi.lib().drsa_amd_conv_bwd_has_kernel_bf16(st.cout, st.cin, w, 1, 0))
+                self._call(f"conv_bwd:{st.name}", "drsa_amd_conv_bwd_den_map", g.data_ptr(), _capi.ptr(amax_in), pool_w,
+                           (st.wts_bwd_bf if bf else st.wts_bwd).data_ptr(), 1 if bf else 0, x_in.data_ptr(),
+                           den.data_ptr(), out.data_ptr(), Bq, clones, st.cout, st.cin, h, w, st.ng_bwd,
+                           st.xmode_bwd, float(eps), s)
             elif pool_w == 4:
                 out = self._buf((li, "R"), (Bq, st.cin, h, w))
                 self._call(f"conv_bwd:{st.name}", "drsa_amd_conv_bwd_bf16_pw", g.data_ptr(), amax_in.data_ptr(), 4,

@@ -99,7 +99,14 @@ int drsa_amd_drsa_run(const float* A, const float* C, int64_t N, int d, int K, f
                       int steps, float* f_traj, int* counter, void* workspace, size_t workspace_bytes,
                       int use_graph, void* stream);
 
-/* orthogonalize (drsa.py:201-221): U_out = V (V^T V)^{-1/2}, Newton-Schulz on device, d <= 128. */
+/* orthogonalize (drsa.py:201-221): U_out = V (V^T V)^{-1/2}, Newton-Schulz on device, d <= 128.
+ * Stop rule (polar_ns.h): iterate X <- X (3I - X^T X)/2 from the scaled V until max|X^T X - I| is
+ * below the internal tolerance (4e-7), or stop after the update that starts from d * max|X^T X - I|
+ * < 1e-2 (that update provably leaves a spectral error below 0.75 e^2 (1 + e/3) < 7.6e-5, e <= d *
+ * max|.|; the typical spread-out error of V = U + G is ~sqrt(d) smaller), or when fp32 rounding is
+ * the floor.  So the tolerance is advisory for that last update: orthogonality of the result is the
+ * bound above, gated in tests/test_drsa_gpu.py at |U^T U - I| < 2e-6 (step) and 5e-6 (d = 128
+ * orthogonalize) and by the DRSA trajectories against the reference's fp64 eigh at 1e-4. */
 int drsa_amd_polar(const float* V, int d, float* U_out, int* iters_out, void* stream);
 
 /* compute_subspace_relevances (explainer.py:206-242): out[b][k] = sum_n sum_{j in block k}
@@ -181,6 +188,17 @@ int drsa_amd_conv_bwd_has_kernel_bf16_pw(int cin, int cout, int W, int pool_w);
 int drsa_amd_conv_bwd_bf16_pw(const float* g, const uint8_t* g_amax, int pool_w, const uint16_t* wts, const float* x,
                               const float* den, float* out, int Bq, int clones, int cin, int cout, int H, int W,
                               int xmode, int post, float eps, void* stream);
+
+/* The backward conv (fp32 weights: wts_bf16 = 0, ng 1..2, g dense or 2x2-pool-sparse; bf16 weights:
+ * wts_bf16 = 1, ng = 1, g dense or 2 x pool_w pool-sparse) with post = POST_DIV whose denominator is
+ * the next layer's input-independent WSquare / Flat map den_map [cout][H][W] itself, the same plane
+ * for every sample: the layer below is a WSquare / Flat conv NOT followed by a pool (VGGish block 1,
+ * block_depth 2: conv0 -> conv3), so its per-sample denominator is the map and no per-sample copy
+ * is written or read.  Bit-identical to drsa_amd_conv_bwd{,_bf16,_bf16_pw}(post = POST_DIV) on the
+ * copy (replaces the same rule backward, attribute.py:98-107). */
+int drsa_amd_conv_bwd_den_map(const float* g, const uint8_t* g_amax, int pool_w, const void* wts, int wts_bf16,
+                              const float* x, const float* den_map, float* out, int Bq, int clones, int cin, int cout,
+                              int H, int W, int ng, int xmode, float eps, void* stream);
 
 /* WSquare / Flat first layer under a 2x2 max-pool, with its denominator map split for the next
  * backward (zennit WSquare/Flat: den = conv(1; W^2, b^2); constants.py:29 puts

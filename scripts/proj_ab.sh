@@ -1,8 +1,8 @@
 set -eo pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/$1
-for v in base pdbg1 pdbg2 base pdbg1 pdbg2; do
+for v in base old base old; do
   L=drsa_audio_amd/lib/libdrsa_amd.so; [ $v != base ] && L=drsa_audio_amd/lib/exp/$v.so
-  echo -n "$v " >> gpurun_out/$1/proj.txt
+  echo -n "$v proj " >> gpurun_out/$1/proj.txt
   DRSA_AMD_LIB=$L timeout -k 10 120 python scripts/bench_projection_bwd.py >> gpurun_out/$1/proj.txt
 done

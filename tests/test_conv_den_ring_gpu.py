@@ -154,3 +154,73 @@ def test_plan_ring_equals_den_copy(monkeypatch, hg):
     clear_cache()
     for k in outs[0]:
         assert np.array_equal(outs[0][k], outs[1][k]), k
+
+
+@pytest.mark.parametrize("cin,H,W,sparse,bf16,pool_w", [(64, 16, 256, False, False, 2), (64, 16, 32, True, False, 2),
+                                                        (64, 16, 256, True, True, 4), (64, 16, 64, False, True, 2),
+                                                        (32, 8, 16, True, True, 2)])
+def test_conv_bwd_den_map_equals_post_div_on_copy(cin, H, W, sparse, bf16, pool_w):
+    """drsa_amd_conv_bwd_den_map (the next layer's denominator = its map, one plane for every
+    sample: a WSquare layer without a pool, VGGish conv0 -> conv3) equals POST_DIV on the
+    per-sample copy, bit for bit."""
+    lib = _capi.lib()
+    cout, S, clones = 64, 3, 2
+    Bq = S * clones
+    g = torch.Generator().manual_seed(cin + W + pool_w)
+    if sparse:
+        gin = torch.randn(Bq, cin, H // 2, W // pool_w, generator=g).to(DEV)
+        gam = torch.randint(0, 2 * pool_w, (S, cin, H // 2, W // pool_w), generator=g, dtype=torch.uint8).to(DEV)
+    else:
+        gin = torch.randn(Bq, cin, H, W, generator=g).to(DEV)
+        gam = None
+    x = (torch.randn(S, cout, H, W, generator=g).abs() * (torch.rand(S, cout, H, W, generator=g) > 0.3)).to(DEV)
+    dmap = torch.randn(cout, H, W, generator=g).to(DEV)
+    dcopy = dmap.unsqueeze(0).expand(S, -1, -1, -1).contiguous()
+    if bf16:
+        n = lib.drsa_amd_conv_weight_bf16_elems(cin, cout, 1)
+        wts = (torch.randn(n, generator=g) * 0.1).to(torch.bfloat16).view(torch.int16).to(DEV)
+    else:
+        n = lib.drsa_amd_conv_weight_floats(cin, cout, 1)
+        wts = (torch.randn(n, generator=g) * 0.1).to(DEV)
+    o_ref = torch.full((Bq, cout, H, W), -9.0, device=DEV)
+    o_m = torch.full_like(o_ref, -7.0)
+    s = _capi.stream_ptr(DEV)
+    if bf16 and sparse and pool_w == 4:
+        _capi.call("drsa_amd_conv_bwd_bf16_pw", gin.data_ptr(), gam.data_ptr(), 4, wts.data_ptr(), x.data_ptr(),
+                   dcopy.data_ptr(), o_ref.data_ptr(), Bq, clones, cin, cout, H, W, _capi.XM_MUL, _capi.POST_DIV, 1e-7, s)
+    else:
+        fn = "drsa_amd_conv_bwd_bf16" if bf16 else "drsa_amd_conv_bwd"
+        _capi.call(fn, gin.data_ptr(), _capi.ptr(gam), wts.data_ptr(), x.data_ptr(), dcopy.data_ptr(), o_ref.data_ptr(),
+                   Bq, clones, cin, cout, H, W, 1, _capi.XM_MUL, _capi.POST_DIV, 1e-7, s)
+    _capi.call("drsa_amd_conv_bwd_den_map", gin.data_ptr(), _capi.ptr(gam), pool_w, wts.data_ptr(), int(bf16),
+               x.data_ptr(), dmap.data_ptr(), o_m.data_ptr(), Bq, clones, cin, cout, H, W, 1, _capi.XM_MUL, 1e-7, s)
+    torch.cuda.synchronize()
+    assert torch.equal(o_m, o_ref)
+
+
+@pytest.mark.parametrize("bf16_bwd", [False, True])
+def test_vggish_plan_den_map_equals_den_copy(monkeypatch, bf16_bwd):
+    """VGGish-BN (WSquare conv0 -> conv3, no pool between): the plan reading the map itself equals
+    the plan with the per-sample copy (DRSA_AMD_DEN_COPY=1), fp32 and bf16-backward plans."""
+    import drsa_audio_amd.engine.plan as plan
+    from drsa_audio_amd.engine import clear_cache
+    from drsa_audio_amd.utils.constants import LRP_NAME_MAP_VGGISH
+    from drsa_audio_amd.xai.explain.attribute import compute_relevances
+    from drsa_audio_amd.zennit.canonizers import SequentialMergeBatchNorm
+    from drsa_audio_amd.zennit.composites import NameMapComposite
+    from lrp_common import logmel, vggish
+    if bf16_bwd:
+        monkeypatch.setenv("DRSA_AMD_BF16_BACKWARD", "1")
+    net = vggish()
+    if bf16_bwd:
+        net = net.bfloat16()
+    net = net.to(DEV)
+    x = logmel(2, 128, 256, seed=9).to(DEV)
+    comp = NameMapComposite(LRP_NAME_MAP_VGGISH, canonizers=[SequentialMergeBatchNorm()])
+    outs = []
+    for copy_den in (False, True):
+        monkeypatch.setattr(plan, "_DEN_COPY", copy_den)
+        clear_cache()
+        outs.append(compute_relevances(net, x, comp, class_idx=2).cpu())
+    clear_cache()
+    assert torch.equal(outs[0], outs[1])
