@@ -81,6 +81,10 @@ def kernel_macs(eng, B, K, standard="sum"):
         macs[f"conv_fwd:{st.name}"] = B * h * w * st.cout * st.cin * 9 * st.ng_fwd
         tag = f"first_layer_bwd:{st.name}" if (li == 0 and st.w2_first is not None) else f"conv_bwd:{st.name}"
         macs[tag] = B * nq * h * w * st.cout * st.cin * 9 * st.ng_bwd
+        if li == 0 and st.w2_first is not None and len(eng.stages) > 1:
+            # drsa_amd_conv_bwd_first_fused: the second layer's backward + the first layer's contraction
+            s1 = eng.stages[1]
+            macs[f"conv_bwd_first:{s1.name}"] = macs[f"conv_bwd:{s1.name}"] + macs[tag]
     for ds in eng.dense:
         N, Kd = ds.W.shape
         macs[f"linear_fwd:{ds.name}"] = B * N * Kd

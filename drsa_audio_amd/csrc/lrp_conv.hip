@@ -30,7 +30,7 @@ int env_int(const char* name, int dflt) {
   return v ? atoi(v) : dflt;
 }
 
-const Entry* find(int cin_p, int cout_p, int W, int ng, int amode, int epi, int et = 0, int pw = 2) {
+const Entry* find(int cin_p, int cout_p, int W, int ng, int amode, int epi, int et = 0, int pw = 2, int ff = 0) {
   int th = 8, tw, mw;
   static const int th16 = env_int("DRSA_AMD_CONV_TH16", 0);
   // 8x8 tiles at 8 < W < 32 (bits: 1 forward, 2 backward; measured faster than 8x16 at 16x16: conv_fwd
@@ -43,7 +43,7 @@ const Entry* find(int cin_p, int cout_p, int W, int ng, int amode, int epi, int 
     for (int i = 0; i < t->n; ++i) {
       const Entry& e = t->entries[i];
       if (e.cin_p == cin_p && e.cout_p == cout_p && e.th == th && e.tw == tw && e.mw == mw && e.ng == ng &&
-          e.amode == amode && e.epi == epi && e.et == et && e.pw == pw)
+          e.amode == amode && e.epi == epi && e.et == et && e.pw == pw && e.ff == ff)
         return &e;
     }
   return nullptr;
@@ -267,6 +267,37 @@ int drsa_amd_conv_bwd_den_ring(const float* g, const uint8_t* g_amax, const void
   a.den_const4 = den_const4; a.out = out; a.H = H; a.W = W; a.cin = cin; a.cout = cout;
   a.clones = clones; a.xmode = xmode; a.post = POST_DIV_RING; a.eps = eps;
   return launch(e, a, Bq, (hipStream_t)stream);
+}
+
+int drsa_amd_conv_bwd_has_kernel_first_fused(int cin, int cout, int H, int W) {
+  if (cout != 32 || H % 8 != 0 || W % 32 != 0) return 0;
+  return find(pad32(cin), 32, W, 1, A_POOLSPARSE, EPI_BWD, 0, 2, 1) != nullptr;
+}
+
+int drsa_amd_conv_bwd_first_fused(const float* g, const uint8_t* g_amax, const float* wts, const float* x,
+                                  const float* den, const float* den_const4, const uint8_t* first_amax,
+                                  const float* first_w2, float* out, float* first_out, int Bq, int clones, int cin,
+                                  int cout, int H, int W, float eps, void* stream) {
+  DRSA_REQUIRE(g && g_amax && wts && x && den && first_amax && first_w2 && out && first_out,
+               "conv_bwd_first_fused: null pointer");
+  DRSA_REQUIRE(Bq > 0 && clones > 0 && Bq % clones == 0, "conv_bwd_first_fused: bad batch/clones");
+  DRSA_REQUIRE(cout == 32 && H % 8 == 0 && W % 32 == 0,
+               "conv_bwd_first_fused: needs cout == 32, H %% 8 == 0 and W %% 32 == 0 (got cout=%d %dx%d)", cout, H, W);
+  DRSA_REQUIRE(!den_const4 || ((uintptr_t)den_const4 & 15) == 0, "conv_bwd_first_fused: den_const4 must be 16-byte aligned");
+  const Entry* e = find(pad32(cin), 32, W, 1, A_POOLSPARSE, EPI_BWD, 0, 2, 1);
+  if (!e) {
+    drsa::set_error("conv_bwd_first_fused: no kernel for cin=%d W=%d", cin, W);
+    return DRSA_EUNSUPPORTED;
+  }
+  ConvArgs a{};
+  a.in = g; a.in_amax = g_amax; a.wts = wts; a.x = x; a.den = den; a.den_const4 = den_const4; a.out = out;
+  a.H = H; a.W = W; a.cin = cin; a.cout = cout; a.clones = clones; a.xmode = XM_MUL;
+  a.post = den_const4 ? POST_DIV_RING : POST_DIV; a.eps = eps;
+  a.ff_amax = first_amax; a.ff_w2 = first_w2; a.ff_out = first_out;
+  const int rc = launch(e, a, Bq, (hipStream_t)stream);
+  if (rc != DRSA_OK) return rc;
+  return drsa_first_layer_border(out, first_amax, first_w2, first_out, Bq, clones, cout, 2 * H, 2 * W, 2 * e->th,
+                                 2 * e->tw, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -89,7 +89,8 @@ constexpr int bf_stride(int hx) {
 // chain), 1 = bf16 (v_mfma_f32_32x32x16_bf16, forward only: conv inputs and weights rounded to
 // bf16 when staged, fp32 accumulation, fp32 outputs).  The bf16 chunk is 16 input channels = one
 // tap per MFMA (k = tap * 16 + ci); its halo is pixel-major, 8 channels per 16-byte pixel slot.
-template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI, int ET = 0, int PW = 2>
+template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI, int ET = 0, int PW = 2,
+          int FF = 0>
 struct ConvCfg {
   static constexpr int CIN_ = CIN, COUT_ = COUT, TH_ = TH, TW_ = TW, MW_ = MW, CIC_ = CIC, NG_ = NG;
   static constexpr int AMODE_ = AMODE, EPI_ = EPI;
@@ -142,6 +143,14 @@ struct ConvCfg {
                 "bf16: 16-channel chunks; dense forward, or the per-clone backward (dense or pool-sparse g)");
   static_assert(PW == 2 || (PW == 4 && (EPI == EPI_FWD_POOL || (EPI == EPI_BWD && ET == 1 && AMODE == A_POOLSPARSE))),
                 "2x4 pool windows: the forward pool epilogue, or the bf16 backward's pool-sparse staging");
+  // FF: the first layer's w^2 contraction fused into the epilogue.  The pass's R is re-laid as
+  // the first layer's unpooled g (argmax pixel of each 2x2 cell) in FCH-channel slices of a pixel
+  // image [FCH][2TH][FPS] (pixel column X at X + 4) over the dead staging tile T
+  static constexpr int FCH = kThreads / (TH * TW / 4);
+  static constexpr int FPS = 2 * TW + 8;
+  static_assert(!FF || (EPI == EPI_BWD && NG == 1 && ET == 0 && ES == 2 && COUT == 32 && TH == 8 && TW == 32 &&
+                        (size_t)FCH * 2 * TH * FPS <= epi_floats),
+                "first-layer fusion: the fp32 8x32-tile backward into 32 channels");
   static constexpr int PW_ = PW;
 };
 
@@ -600,9 +609,10 @@ __device__ __forceinline__ void mfma_chunk_bf(const uint4* hb, const uint4* wb, 
 }
 
 // PW: pool window width of EPI_FWD_POOL (2 x PW windows; 4 = VGGish's (2,4) pool)
-template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI, int ET = 0, int PW = 2>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AMODE, EPI, ET, PW>::WPE))) void conv3x3_kernel(ConvArgs a) {
-  using Cfg = ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AMODE, EPI, ET, PW>;
+template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI, int ET = 0, int PW = 2,
+          int FF = 0>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AMODE, EPI, ET, PW, FF>::WPE))) void conv3x3_kernel(ConvArgs a) {
+  using Cfg = ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AMODE, EPI, ET, PW, FF>;
   constexpr int HY = Cfg::HY, HX = Cfg::HX, RS = Cfg::RS, PLANE = Cfg::PLANE;
   constexpr int MTH = Cfg::MTH, MTW = Cfg::MTW, MTX = Cfg::MTX;
   constexpr int WM = Cfg::WM, MPW = Cfg::MPW, NPW = Cfg::NPW;
@@ -732,6 +742,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
   const int ring_i = !pix_ok ? 0 : Y == 0 ? X : Y == H - 1 ? W + X : 2 * W + (Y - 1) * 8 + (X == 0 ? 0 : 4);
   const float* rsrc = ring ? a.den + (size_t)bs * a.cout * ring_n + ring_i : dsrc;
   const size_t dstride = ring ? (size_t)ring_n : (size_t)HW;
+  // FF: float4 groups on the tile's border ring still store R (the border pixels' contraction
+  // needs the neighbour tiles' cells: drsa_amd_first_layer_bwd_border); the first layer's argmax
+  // of the group's 4 cells is one 32-bit load; contraction thread (fr, fj) owns footprint pixels
+  // (fr, 4fj .. 4fj + 3) of the 2TH x 2TW footprint
+  const bool tile_ring = py == 0 || py == TH - 1 || px == 0 || px == TW - 4;
+  const uint8_t* ffa = FF ? a.ff_amax + (size_t)bs * a.cout * HW + pix : nullptr;
+  const int fr = tid / (TW / 2), fj = tid % (TW / 2);
+  typedef float ff2 __attribute__((ext_vector_type(2)));
+  ff2 ffacc[2] = {ff2{0.f, 0.f}, ff2{0.f, 0.f}};
   // epilogue x/den loads of (n-tile v, pass sub); (0, 0) is issued before the last chunk's MFMAs
   auto epi_loads = [&](int v, int sub, float4 (&xk)[V4T], float4 (&dk)[V4T], bool lx = true, bool ld = true,
                        int i0 = 0, int i1 = -1) {
@@ -1005,7 +1024,94 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
       } else {
         epi_loads(v, sub, xk, dk);
       }
+      uint32_t ak[V4T];
+      if constexpr (FF) {
+#pragma unroll
+        for (int it = 0; it < V4T; ++it) {
+          const int co = gchs(cl0 + it * CS, v, sub);
+          ak[it] = *reinterpret_cast<const uint32_t*>(ffa + (size_t)co * HW);
+        }
+      }
       stage(v, [&](int u, int r) { return acc[0][u][v][r]; }, sub);
+      if constexpr (FF) {
+        // R (the Epsilon-type rule and the division; the host requires XM_MUL and POST_DIV[_RING])
+        float4 Rf[V4T];
+#pragma unroll
+        for (int it = 0; it < V4T; ++it) {
+          const int cl = cl0 + it * CS;
+          const int co = gchs(cl, v, sub);
+          const float4 t = *reinterpret_cast<const float4*>(T + (cl * TH + py) * TWP + px);
+          const float4 x = xk[it], d = dk[it];
+          auto f = [&](float tt, float xx, float dd) {
+            const float q = div_nb(xx * tt, stab(dd, eps));
+            return (xx > 0.f) ? q : 0.f;
+          };
+          Rf[it] = make_float4(f(t.x, x.x, d.x), f(t.y, x.y, d.y), f(t.z, x.z, d.z), f(t.w, x.w, d.w));
+          if (tile_ring) *reinterpret_cast<float4*>(oqp + (size_t)co * HW) = Rf[it];
+        }
+        constexpr int FPS = Cfg::FPS, FH = 2 * TH;
+        float* P = T;
+#pragma unroll
+        for (int it = 0; it < V4T; ++it) {
+          // slice it = channels sub*TCH + it*CS + (0..CS-1); this thread's group is slot cl0:
+          // cell (py, px + i) -> pixels (2py + s/2, 2px + 2i + s%2), s = its argmax, zeros elsewhere
+          __syncthreads();
+          {
+            const uint32_t am = ak[it];
+            const float rv[4] = {Rf[it].x, Rf[it].y, Rf[it].z, Rf[it].w};
+            float o0[8], o1[8];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const uint32_t s = (am >> (8 * i)) & 0xffu;
+              o0[2 * i] = s == 0u ? rv[i] : 0.f;
+              o0[2 * i + 1] = s == 1u ? rv[i] : 0.f;
+              o1[2 * i] = s == 2u ? rv[i] : 0.f;
+              o1[2 * i + 1] = s == 3u ? rv[i] : 0.f;
+            }
+            float* pw = P + (cl0 * FH + 2 * py) * FPS + 2 * px + 4;
+            reinterpret_cast<float4*>(pw)[0] = make_float4(o0[0], o0[1], o0[2], o0[3]);
+            reinterpret_cast<float4*>(pw)[1] = make_float4(o0[4], o0[5], o0[6], o0[7]);
+            reinterpret_cast<float4*>(pw + FPS)[0] = make_float4(o1[0], o1[1], o1[2], o1[3]);
+            reinterpret_cast<float4*>(pw + FPS)[1] = make_float4(o1[4], o1[5], o1[6], o1[7]);
+          }
+          __syncthreads();
+          // the dense first-layer chain (first_layer_bwd_pooled_kernel): channel ascending, then
+          // dy, dx; rows / columns outside the footprint are clamped (only border pixels read them,
+          // and those are recomputed by the border kernel)
+#pragma unroll 1
+          for (int k = 0; k < CS; ++k) {
+            const int c = v * 32 + sub * TCH + it * CS + k;
+            float wv[9];
+#pragma unroll
+            for (int tp = 0; tp < 9; ++tp) wv[tp] = a.ff_w2[c * 9 + tp];
+            ff2 pr[3][5];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+              int rr = fr - 1 + i;
+              rr = rr < 0 ? 0 : rr > FH - 1 ? FH - 1 : rr;
+              const float* q = P + (k * FH + rr) * FPS + 4 * fj + 3;
+              const float p0 = q[0];
+              const float4 p4 = *reinterpret_cast<const float4*>(q + 1);
+              const float p5 = q[5];
+              pr[i][0] = ff2{p0, p4.x};
+              pr[i][1] = ff2{p4.x, p4.y};
+              pr[i][2] = ff2{p4.y, p4.z};
+              pr[i][3] = ff2{p4.z, p4.w};
+              pr[i][4] = ff2{p4.w, p5};
+            }
+#pragma unroll
+            for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+              for (int dx = -1; dx <= 1; ++dx) {
+                const float w = wv[(1 - dy) * 3 + (1 - dx)];
+                const ff2 ww = ff2{w, w};
+                ffacc[0] = __builtin_elementwise_fma(pr[1 + dy][1 + dx], ww, ffacc[0]);
+                ffacc[1] = __builtin_elementwise_fma(pr[1 + dy][3 + dx], ww, ffacc[1]);
+              }
+          }
+        }
+        continue;
+      }
       // the common mode (Epsilon-type rule: R = x * J^T g, then the next layer's division)
       // specialised: the loads above are already in flight, this branch is uniform
       if (NG == 1 && a.xmode == XM_MUL && post_div && !(a.dbg & 2)) {
@@ -1078,6 +1184,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
         if (ok && pix_ok) *reinterpret_cast<float4*>(oqp + (size_t)coc * HW) = R;
       }
      }
+      if constexpr (FF) {
+        // every footprint pixel is written; the border ones are overwritten by the border kernel
+        const int W2 = 2 * W;
+        *reinterpret_cast<float4*>(a.ff_out + ((size_t)bq * 2 * H + 2 * ty0 + fr) * W2 + 2 * tx0 + 4 * fj) =
+            make_float4(ffacc[0].x, ffacc[0].y, ffacc[1].x, ffacc[1].y);
+      }
     }
   }
 }
@@ -1090,7 +1202,15 @@ struct Entry {
   size_t lds;
   int et = 0;   // operand type (ConvCfg ET)
   int pw = 2;   // forward pool window width (ConvCfg PW)
+  int ff = 0;   // first-layer contraction fused into the backward epilogue (ConvCfg FF)
 };
+
+// fp32 pool-sparse backward of the layer above a WSquare first layer, with that layer's
+// contraction fused (drsa_amd_conv_bwd_first_fused)
+#define CONV_ENTRY_FF(CIN, COUT, CIC)                                                                       \
+  drsa_conv::Entry{CIN, COUT, 8, 32, 8, CIC, 1, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD,                \
+                   drsa_conv::conv3x3_kernel<CIN, COUT, 8, 32, 8, CIC, 1, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD, 0, 2, 1>, \
+                   drsa_conv::ConvCfg<CIN, COUT, 8, 32, 8, CIC, 1, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD, 0, 2, 1>::lds_floats * sizeof(float), 0, 2, 1}
 
 #define CONV_ENTRY(CIN, COUT, TH, TW, MW, CIC, NG, AM, EP)                                                 \
   drsa_conv::Entry{CIN, COUT, TH, TW, MW, CIC, NG, AM, EP,                                                 \

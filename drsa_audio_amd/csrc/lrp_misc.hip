@@ -988,6 +988,84 @@ __global__ __launch_bounds__(256) void first_layer_bwd_pooled_kernel(const float
   }
 }
 
+// The border pixels of drsa_amd_conv_bwd_first_fused's FY x FX footprints (rows 0 and FY-1 of
+// each footprint row band, then columns 0 and FX-1 of the remaining rows), one thread each: the
+// same chain as first_layer_bwd_pooled_kernel (channel ascending, then dy, dx; zero outside the
+// image) over the 2 x 2 cells under the pixel's 3 x 3 window, which lie on the footprints' cell
+// rings where the fused kernel stored g.
+__global__ __launch_bounds__(256) void first_layer_bwd_border_kernel(const float* __restrict__ g,
+                                                                     const uint8_t* __restrict__ amax,
+                                                                     const float* __restrict__ w2,
+                                                                     float* __restrict__ out, int C, int H, int W,
+                                                                     int clones, int FY, int FX, int nbr, int nbc,
+                                                                     int nb) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= nb) return;
+  int Y, X;
+  if (i < nbr * W) {
+    const int br = i / W;
+    X = i % W;
+    Y = (br >> 1) * FY + ((br & 1) ? FY - 1 : 0);
+  } else {
+    const int k = i - nbr * W, rr = k / nbc, bc = k % nbc;
+    Y = (rr / (FY - 2)) * FY + 1 + rr % (FY - 2);
+    X = (bc >> 1) * FX + ((bc & 1) ? FX - 1 : 0);
+  }
+  const int bq = blockIdx.y, bs = bq / clones;
+  const int H2 = H >> 1, W2 = W >> 1;
+  const size_t plane = (size_t)H2 * W2;
+  const float* gb = g + (size_t)bq * C * plane;
+  const uint8_t* ab = amax + (size_t)bs * C * plane;
+  const int cy0 = (Y - 1) >> 1, cx0 = (X - 1) >> 1;   // the window's top-left cell (may be -1)
+  size_t off[2][2];
+#pragma unroll
+  for (int iy = 0; iy < 2; ++iy)
+#pragma unroll
+    for (int ix = 0; ix < 2; ++ix) {
+      const int cy = cy0 + iy, cx = cx0 + ix;
+      const bool ok = cy >= 0 && cy < H2 && cx >= 0 && cx < W2;
+      off[iy][ix] = ok ? (size_t)cy * W2 + cx : 0;
+    }
+  // per tap: its cell (bit 1: row, bit 0: column), the argmax that selects it, in-image flag
+  int tc[9], ts[9];
+  bool tin[9];
+#pragma unroll
+  for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+    for (int dx = -1; dx <= 1; ++dx) {
+      const int t = (dy + 1) * 3 + dx + 1, yy = Y + dy, xx = X + dx;
+      tin[t] = yy >= 0 && yy < H && xx >= 0 && xx < W;
+      tc[t] = (((yy >> 1) - cy0) << 1) | ((xx >> 1) - cx0);
+      ts[t] = (yy & 1) * 2 + (xx & 1);
+    }
+  float acc = 0.f;
+#pragma unroll 4
+  for (int c = 0; c < C; ++c) {
+    float gv[4];
+    int av[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      gv[q] = gb[c * plane + off[q >> 1][q & 1]];
+      av[q] = ab[c * plane + off[q >> 1][q & 1]];
+    }
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int t = (dy + 1) * 3 + dx + 1;
+        float vq = 0.f;
+        int aq = 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (tc[t] == q) { vq = gv[q]; aq = av[q]; }
+        const float v = (tin[t] && aq == ts[t]) ? vq : 0.f;
+        acc = fmaf(v, w2[c * 9 + (1 - dy) * 3 + (1 - dx)], acc);
+      }
+  }
+  out[((size_t)bq * H + Y) * W + X] = acc;
+}
+
+
 // den[co][y][x] = sum_ci sum_{in-bounds taps} w2[co][ci][ky][kx] * 1 + b2[co]
 __global__ void first_layer_den_kernel(const float* __restrict__ w2, const float* __restrict__ b2, float* __restrict__ den,
                                        int C, int CI, int H, int W) {
@@ -1335,6 +1413,17 @@ bool proj_p_lds_fwd() { return proj_p_lds_env() == 1; }
 bool proj_p_lds_bwd() { return proj_p_lds_env() == 1; }
 
 }  // namespace
+
+int drsa_first_layer_border(const float* g, const uint8_t* amax, const float* w2, float* out, int Bq, int clones,
+                            int C, int H, int W, int FY, int FX, hipStream_t s) {
+  DRSA_REQUIRE(FY >= 4 && FX >= 4 && H % FY == 0 && W % FX == 0, "first_layer_border: bad footprint");
+  const int nbr = 2 * (H / FY), nbc = 2 * (W / FX);
+  const int nb = nbr * W + (H - nbr) * nbc;
+  hipLaunchKernelGGL(first_layer_bwd_border_kernel, dim3((nb + 255) / 256, Bq), dim3(256), 0, s, g, amax, w2, out, C,
+                     H, W, clones, FY, FX, nbr, nbc, nb);
+  DRSA_LAUNCH_CHECK();
+  return DRSA_OK;
+}
 
 extern "C" {
 

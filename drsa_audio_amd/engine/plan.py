@@ -56,6 +56,10 @@ _DEN_COPY = os.environ.get("DRSA_AMD_DEN_COPY", "0") == "1"
 # A/B switch: 0 = the (2,4) pool backward as a separate unpool (maxpool_bwd) before a dense-g bf16
 # backward conv, instead of folded into its pool-sparse staging (drsa_amd_conv_bwd_bf16_pw)
 _POOL24_SPARSE = os.environ.get("DRSA_AMD_BF16_POOL24_SPARSE", "1") == "1"
+# A/B switch: 0 = the WSquare first layer's contraction as its own kernel (first_layer_bwd) after the
+# second layer's backward, instead of fused into that backward's epilogue plus a border-pixel kernel
+# (drsa_amd_conv_bwd_first_fused: the second layer's R is stored on its tiles' border rings only)
+_FIRST_FUSE = os.environ.get("DRSA_AMD_FIRST_FUSE", "1") == "1"
 
 
 def _pad32(c: int) -> int:
@@ -721,6 +725,23 @@ class LRPEngine:
                     post, den, eps = POST_NONE, None, 0.0
             else:
                 post, den, eps = POST_NONE, None, 0.0
+            s0 = self.stages[0]
+            if (li == 1 and _FIRST_FUSE and stop_after is None and amax_in is not None
+                    and post in (POST_DIV, POST_DIV_RING) and st.den_kind not in (None, "ab")
+                    and st.ng_bwd == 1 and st.xmode_bwd == XM_MUL and st.wts_bwd_bf is None
+                    and s0.w2_first is not None and s0.pool and s0.pool_k == (2, 2) and s0.proj is None
+                    and _capi.lib().drsa_amd_conv_bwd_has_kernel_first_fused(st.cout, st.cin, h, w)):
+                # the first layer's w^2 contraction fused into this backward's epilogue: this
+                # stage's R exists only on the tiles' border rings, the input relevance comes out
+                rec0 = st0["stages"][0]
+                ring_R = self._buf((li, "R"), (Bq, st.cin, h, w))
+                first = self._buf((0, "R"), (Bq, 1, rec0["H"], rec0["W"]))
+                dr, dc4 = (den["den"], den["den_const4"]) if post == POST_DIV_RING else (den, None)
+                self._call(f"conv_bwd_first:{st.name}", "drsa_amd_conv_bwd_first_fused", g.data_ptr(),
+                           amax_in.data_ptr(), st.wts_bwd.data_ptr(), x_in.data_ptr(), dr.data_ptr(), _capi.ptr(dc4),
+                           rec0["amax"].data_ptr(), s0.w2_first.data_ptr(), ring_R.data_ptr(), first.data_ptr(), Bq,
+                           clones, st.cout, st.cin, h, w, float(eps), s)
+                return first
             if li == 0 and st.w2_first is not None:
                 out = self._buf((li, "R"), (Bq, 1, h, w))
                 self._call(f"first_layer_bwd:{st.name}", "drsa_amd_first_layer_bwd", g.data_ptr(), _capi.ptr(amax_in), st.w2_first.data_ptr(),
