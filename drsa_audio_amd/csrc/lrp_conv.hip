@@ -294,8 +294,11 @@ int drsa_amd_conv_bwd_first_fused(const float* g, const uint8_t* g_amax, const f
   a.H = H; a.W = W; a.cin = cin; a.cout = cout; a.clones = clones; a.xmode = XM_MUL;
   a.post = den_const4 ? POST_DIV_RING : POST_DIV; a.eps = eps;
   a.ff_amax = first_amax; a.ff_w2 = first_w2; a.ff_out = first_out;
-  const int rc = launch(e, a, Bq, (hipStream_t)stream);
+  static const int ff_dbg0 = env_int("DRSA_AMD_FF_DBG", 0);
+  const int rc = (ff_dbg0 & 2) ? DRSA_OK : launch(e, a, Bq, (hipStream_t)stream);
   if (rc != DRSA_OK) return rc;
+  static const int ff_dbg = env_int("DRSA_AMD_FF_DBG", 0);   // ablation only: 1 = no border kernel, 2 = border only
+  if (ff_dbg & 1) return DRSA_OK;
   return drsa_first_layer_border(out, first_amax, first_w2, first_out, Bq, clones, cout, 2 * H, 2 * W, 2 * e->th,
                                  2 * e->tw, (hipStream_t)stream);
 }

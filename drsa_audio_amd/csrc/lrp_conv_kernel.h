@@ -127,8 +127,10 @@ struct ConvCfg {
   static constexpr size_t staging_floats =
       BF ? bf_halo_floats + bf_w_floats : (size_t)CIC * PLANE + (size_t)NG * KCP * COUT;
   static constexpr size_t epi_floats = (size_t)TCH * TH * TWP;
+  // FF: + the first layer's w^2 [COUT][12] (9 used) behind the staging / epilogue area
+  static constexpr size_t ff_w_floats = FF ? (size_t)COUT * 12 : 0;
   static constexpr size_t lds_floats =
-      staging_floats > epi_floats ? staging_floats : epi_floats;
+      (staging_floats > epi_floats ? staging_floats : epi_floats) + ff_w_floats;
   // minimum waves per SIMD the register allocation must allow (1 block = 1 wave per SIMD)
   static constexpr int WPE = BF ? (COUT <= 64 ? DRSA_CONV_BF_WPE : 1)
                              : (EPI == EPI_BWD && NG == 1) ? (SMALL_BWD ? 4 : DRSA_CONV_BWD_WPE)
@@ -608,6 +610,15 @@ __device__ __forceinline__ void mfma_chunk_bf(const uint4* hb, const uint4* wb, 
   }
 }
 
+// first-layer fusion ablation (experiments only): 1 = no contraction, 2 = no pixel image either
+#ifndef DRSA_FF_DBG
+#define DRSA_FF_DBG 0
+#endif
+// first-layer fusion: unroll of the contraction's channel loop (4 = all, spills)
+#ifndef DRSA_FF_UNROLL
+#define DRSA_FF_UNROLL 1
+#endif
+
 // PW: pool window width of EPI_FWD_POOL (2 x PW windows; 4 = VGGish's (2,4) pool)
 template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI, int ET = 0, int PW = 2,
           int FF = 0>
@@ -694,6 +705,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
   auto gchs = [&](int cl, int v, int sub) { return ES == 1 ? gch(cl, v) : v * 32 + sub * TCH + cl; };
   typename std::conditional<Cfg::BF, StagerBF<Cfg>, Stager<Cfg>>::type stg;
   stg.load(a, 0, tid, ty0, tx0, bq, bs);
+  float* const WL = smem + (Cfg::lds_floats - Cfg::ff_w_floats);
+  if constexpr (FF) {
+    // read in the epilogue with uniform addresses (LDS broadcasts; the scalar cache cannot be used
+    // for a buffer the compiler cannot prove unaliased with the kernel's stores)
+    for (int i = tid; i < COUT * 9; i += kThreads) WL[(i / 9) * 12 + i % 9] = a.ff_w2[i];
+  }
   // backward: all chunks but the last here, the last one peeled below (after the epilogue
   // addressing is set up, so that none of it is live across the loop)
   for (int chunk = 0; chunk + (EPI == EPI_BWD ? 1 : 0) < Cfg::NCHUNK; ++chunk) {
@@ -1052,7 +1069,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
         constexpr int FPS = Cfg::FPS, FH = 2 * TH;
         float* P = T;
 #pragma unroll
-        for (int it = 0; it < V4T; ++it) {
+        for (int it = 0; it < ((DRSA_FF_DBG & 2) ? 0 : V4T); ++it) {
           // slice it = channels sub*TCH + it*CS + (0..CS-1); this thread's group is slot cl0:
           // cell (py, px + i) -> pixels (2py + s/2, 2px + 2i + s%2), s = its argmax, zeros elsewhere
           __syncthreads();
@@ -1078,12 +1095,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
           // the dense first-layer chain (first_layer_bwd_pooled_kernel): channel ascending, then
           // dy, dx; rows / columns outside the footprint are clamped (only border pixels read them,
           // and those are recomputed by the border kernel)
-#pragma unroll 1
-          for (int k = 0; k < CS; ++k) {
+#pragma unroll DRSA_FF_UNROLL
+          for (int k = 0; k < ((DRSA_FF_DBG & 1) ? 0 : CS); ++k) {
             const int c = v * 32 + sub * TCH + it * CS + k;
-            float wv[9];
-#pragma unroll
-            for (int tp = 0; tp < 9; ++tp) wv[tp] = a.ff_w2[c * 9 + tp];
+            const float4 w03 = *reinterpret_cast<const float4*>(WL + c * 12);
+            const float4 w47 = *reinterpret_cast<const float4*>(WL + c * 12 + 4);
+            const float wv[9] = {w03.x, w03.y, w03.z, w03.w, w47.x, w47.y, w47.z, w47.w, WL[c * 12 + 8]};
             ff2 pr[3][5];
 #pragma unroll
             for (int i = 0; i < 3; ++i) {

@@ -573,27 +573,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
     const int pl = w * 16 + pc;
     const int py = y0 + pl / TW, px = x0 + pl % TW;
     const size_t pixl = (size_t)py * W + px;
-    // a at rows c = i*16 + 4 rg + r: the output layout of every GEMM below; the relevance R at a'
-    // (pool backward folded in) is loaded here too, so its latency hides under the h GEMM (it is
-    // first needed after the a' GEMM); den follows after the a' GEMM (needed by the clones only)
-    float av[NB * 4], dv[PF ? NB * 4 : 1], Rv0[NB * 4];
+    // a (and den) at rows c = i*16 + 4 rg + r: the output layout of every GEMM below
+    float av[NB * 4], dv[PF ? NB * 4 : 1];
 #pragma unroll
     for (int i = 0; i < NB; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int c = i * 16 + rg * 4 + r;
         const bool ok = c < d;
-        const int cc = ok ? c : 0;
-        const size_t os = ((size_t)b * d + cc) * HW + pixl;
+        const size_t os = ((size_t)b * d + (ok ? c : 0)) * HW + pixl;
         const float aa = a[os];
         av[i * 4 + r] = ok ? aa : 0.f;
-        if (sparse) {
-          const size_t q = ((size_t)b * d + cc) * H2 * W2 + (py >> 1) * W2 + (px >> 1);
-          const float gv = gp[q];   // unconditional load, then the argmax select
-          Rv0[i * 4 + r] = (amax[q] == (((py & 1) << 1) | (px & 1))) ? gv : 0.f;
-        } else {
-          Rv0[i * 4 + r] = gp[os];
-        }
+        if constexpr (PF) dv[i * 4 + r] = has_den ? den[os] : 1.f;
       }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -640,20 +631,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
         for (int r = 0; r < 4; ++r) {
           const int c = cb * 16 + rg * 4 + r;
           const bool ok = c < d;
-          const float R = Rv0[cb * 4 + r];
+          const int cc = ok ? c : 0;
+          float R;
+          if (sparse) {
+            const size_t q = ((size_t)b * d + cc) * H2 * W2 + (py >> 1) * W2 + (px >> 1);
+            const float gv = gp[q];   // unconditional load, then the argmax select
+            R = (amax[q] == (((py & 1) << 1) | (px & 1))) ? gv : 0.f;
+          } else {
+            R = gp[((size_t)b * d + cc) * HW + pixl];
+          }
           const float apv = av[cb * 4 + r] + acc[cb][r];
           const float v = R / stab(apv, eps_proj);
           RA[c * PW + pc] = ok ? v : 0.f;
-        }
-    }
-    if constexpr (PF) {
-#pragma unroll
-      for (int i = 0; i < NB; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = i * 16 + rg * 4 + r;
-          const size_t os = ((size_t)b * d + (c < d ? c : 0)) * HW + pixl;
-          dv[i * 4 + r] = has_den ? den[os] : 1.f;
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -988,83 +977,101 @@ __global__ __launch_bounds__(256) void first_layer_bwd_pooled_kernel(const float
   }
 }
 
-// The border pixels of drsa_amd_conv_bwd_first_fused's FY x FX footprints (rows 0 and FY-1 of
-// each footprint row band, then columns 0 and FX-1 of the remaining rows), one thread each: the
-// same chain as first_layer_bwd_pooled_kernel (channel ascending, then dy, dx; zero outside the
-// image) over the 2 x 2 cells under the pixel's 3 x 3 window, which lie on the footprints' cell
-// rings where the fused kernel stored g.
+// The border pixels of drsa_amd_conv_bwd_first_fused's FY x FX footprints (FY = 2 TH2, FX = 2 TW2):
+// workgroup (k, bq) takes the horizontal band of pixel rows FY k - 1, FY k (cell rows TH2 k - 1,
+// TH2 k, all columns) and, for k < H2 / TH2, the vertical strips of footprint row k (pixel rows
+// FY k + 1 .. FY k + FY - 2 at pixel columns FX m - 1, FX m: cell columns TW2 m - 1, TW2 m).  The
+// cells are staged in LDS (coalesced loads, zero / no-match outside the image); each pixel runs
+// the chain of first_layer_bwd_pooled_kernel (channel ascending, then dy, dx; zero terms included)
+// over the 2 x 2 cells under its 3 x 3 window -- cells on the footprints' rings, where the fused
+// kernel stored g.
 __global__ __launch_bounds__(256) void first_layer_bwd_border_kernel(const float* __restrict__ g,
                                                                      const uint8_t* __restrict__ amax,
                                                                      const float* __restrict__ w2,
                                                                      float* __restrict__ out, int C, int H, int W,
-                                                                     int clones, int FY, int FX, int nbr, int nbc,
-                                                                     int nb) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= nb) return;
-  int Y, X;
-  if (i < nbr * W) {
-    const int br = i / W;
-    X = i % W;
-    Y = (br >> 1) * FY + ((br & 1) ? FY - 1 : 0);
-  } else {
-    const int k = i - nbr * W, rr = k / nbc, bc = k % nbc;
-    Y = (rr / (FY - 2)) * FY + 1 + rr % (FY - 2);
-    X = (bc >> 1) * FX + ((bc & 1) ? FX - 1 : 0);
-  }
-  const int bq = blockIdx.y, bs = bq / clones;
-  const int H2 = H >> 1, W2 = W >> 1;
+                                                                     int clones, int TH2, int TW2) {
+  extern __shared__ __attribute__((aligned(16))) float bsm[];
+  const int tid = threadIdx.x;
+  const int H2 = H >> 1, W2 = W >> 1, WP = W2 + 2, FY = 2 * TH2, FX = 2 * TW2;
+  const int NV = 2 * (W2 / TW2 + 1);
+  float* HV = bsm;                                              // [C][2][WP]   band cells (column + 1)
+  float* VV = HV + (size_t)C * 2 * WP;                          // [C][TH2][NV] strip cells
+  uint8_t* HA = reinterpret_cast<uint8_t*>(VV + (size_t)C * TH2 * NV);
+  uint8_t* VA = HA + (size_t)C * 2 * WP;
+  const int k = blockIdx.x, bq = blockIdx.y, bs = bq / clones;
+  const bool vert = k < H2 / TH2;
   const size_t plane = (size_t)H2 * W2;
   const float* gb = g + (size_t)bq * C * plane;
   const uint8_t* ab = amax + (size_t)bs * C * plane;
-  const int cy0 = (Y - 1) >> 1, cx0 = (X - 1) >> 1;   // the window's top-left cell (may be -1)
-  size_t off[2][2];
-#pragma unroll
-  for (int iy = 0; iy < 2; ++iy)
-#pragma unroll
-    for (int ix = 0; ix < 2; ++ix) {
-      const int cy = cy0 + iy, cx = cx0 + ix;
-      const bool ok = cy >= 0 && cy < H2 && cx >= 0 && cx < W2;
-      off[iy][ix] = ok ? (size_t)cy * W2 + cx : 0;
+  for (int i = tid; i < C * 2 * WP; i += 256) {
+    const int c = i / (2 * WP), rem = i % (2 * WP);
+    const int cy = k * TH2 - 1 + rem / WP, cx = rem % WP - 1;
+    const bool ok = cy >= 0 && cy < H2 && cx >= 0 && cx < W2;
+    const size_t o = ok ? c * plane + (size_t)cy * W2 + cx : 0;
+    const float v = gb[o];
+    const int a8 = ab[o];
+    HV[i] = ok ? v : 0.f;
+    HA[i] = (uint8_t)(ok ? a8 : 4);
+  }
+  if (vert) {
+    for (int i = tid; i < C * TH2 * NV; i += 256) {
+      const int c = i / (TH2 * NV), rem = i % (TH2 * NV), j = rem % NV;
+      const int cy = k * TH2 + rem / NV, cx = TW2 * (j >> 1) - 1 + (j & 1);
+      const bool ok = cx >= 0 && cx < W2;
+      const size_t o = ok ? c * plane + (size_t)cy * W2 + cx : 0;
+      const float v = gb[o];
+      const int a8 = ab[o];
+      VV[i] = ok ? v : 0.f;
+      VA[i] = (uint8_t)(ok ? a8 : 4);
     }
-  // per tap: its cell (bit 1: row, bit 0: column), the argmax that selects it, in-image flag
-  int tc[9], ts[9];
-  bool tin[9];
-#pragma unroll
-  for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-    for (int dx = -1; dx <= 1; ++dx) {
-      const int t = (dy + 1) * 3 + dx + 1, yy = Y + dy, xx = X + dx;
-      tin[t] = yy >= 0 && yy < H && xx >= 0 && xx < W;
-      tc[t] = (((yy >> 1) - cy0) << 1) | ((xx >> 1) - cx0);
-      ts[t] = (yy & 1) * 2 + (xx & 1);
-    }
-  float acc = 0.f;
-#pragma unroll 4
-  for (int c = 0; c < C; ++c) {
-    float gv[4];
-    int av[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      gv[q] = gb[c * plane + off[q >> 1][q & 1]];
-      av[q] = ab[c * plane + off[q >> 1][q & 1]];
-    }
+  }
+  __syncthreads();
+  // one pixel: cells (iy, ix) of its window at V[c * cs + (r0 + iy) * rs + c0 + ix]
+  auto pixel = [&](int Y, int X, const float* V, const uint8_t* A, int cs, int rs, int r0, int c0) {
+    int toff[9], ts[9];
+    bool tin[9];
 #pragma unroll
     for (int dy = -1; dy <= 1; ++dy)
 #pragma unroll
       for (int dx = -1; dx <= 1; ++dx) {
-        const int t = (dy + 1) * 3 + dx + 1;
-        float vq = 0.f;
-        int aq = 4;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (tc[t] == q) { vq = gv[q]; aq = av[q]; }
-        const float v = (tin[t] && aq == ts[t]) ? vq : 0.f;
-        acc = fmaf(v, w2[c * 9 + (1 - dy) * 3 + (1 - dx)], acc);
+        const int t = (dy + 1) * 3 + dx + 1, yy = Y + dy, xx = X + dx;
+        tin[t] = yy >= 0 && yy < H && xx >= 0 && xx < W;
+        toff[t] = (r0 + ((yy >> 1) - ((Y - 1) >> 1))) * rs + c0 + ((xx >> 1) - ((X - 1) >> 1));
+        ts[t] = (yy & 1) * 2 + (xx & 1);
       }
+    float acc = 0.f;
+#pragma unroll 2
+    for (int c = 0; c < C; ++c) {
+      float wv[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) wv[t] = w2[c * 9 + t];
+#pragma unroll
+      for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+          const int t = (dy + 1) * 3 + dx + 1;
+          const int o = c * cs + toff[t];
+          const float vq = V[o];
+          const bool hit = tin[t] && A[o] == ts[t];
+          acc = fmaf(hit ? vq : 0.f, wv[(1 - dy) * 3 + (1 - dx)], acc);
+        }
+    }
+    out[((size_t)bq * H + Y) * W + X] = acc;
+  };
+  for (int p = tid; p < 2 * W; p += 256) {
+    const int Y = k * FY - 1 + p / W, X = p % W;
+    // band cell row 0 = TH2 k - 1, column index = cell column + 1
+    if (Y >= 0 && Y < H) pixel(Y, X, HV, HA, 2 * WP, WP, ((Y - 1) >> 1) - (k * TH2 - 1), ((X - 1) >> 1) + 1);
   }
-  out[((size_t)bq * H + Y) * W + X] = acc;
+  if (vert) {
+    for (int p = tid; p < (FY - 2) * NV; p += 256) {
+      const int j = p % NV, Y = k * FY + 1 + p / NV, X = FX * (j >> 1) - 1 + (j & 1);
+      // strip cell row 0 = TH2 k; strip column 2m + 0/1 = cell column TW2 m - 1 / TW2 m
+      if (X >= 0 && X < W)
+        pixel(Y, X, VV, VA, TH2 * NV, NV, ((Y - 1) >> 1) - k * TH2, 2 * (j >> 1) + (((X - 1) >> 1) - (TW2 * (j >> 1) - 1)));
+    }
+  }
 }
-
 
 // den[co][y][x] = sum_ci sum_{in-bounds taps} w2[co][ci][ky][kx] * 1 + b2[co]
 __global__ void first_layer_den_kernel(const float* __restrict__ w2, const float* __restrict__ b2, float* __restrict__ den,
@@ -1416,11 +1423,14 @@ bool proj_p_lds_bwd() { return proj_p_lds_env() == 1; }
 
 int drsa_first_layer_border(const float* g, const uint8_t* amax, const float* w2, float* out, int Bq, int clones,
                             int C, int H, int W, int FY, int FX, hipStream_t s) {
-  DRSA_REQUIRE(FY >= 4 && FX >= 4 && H % FY == 0 && W % FX == 0, "first_layer_border: bad footprint");
-  const int nbr = 2 * (H / FY), nbc = 2 * (W / FX);
-  const int nb = nbr * W + (H - nbr) * nbc;
-  hipLaunchKernelGGL(first_layer_bwd_border_kernel, dim3((nb + 255) / 256, Bq), dim3(256), 0, s, g, amax, w2, out, C,
-                     H, W, clones, FY, FX, nbr, nbc, nb);
+  DRSA_REQUIRE(FY >= 4 && FX >= 4 && FY % 2 == 0 && FX % 2 == 0 && H % FY == 0 && W % FX == 0,
+               "first_layer_border: bad footprint");
+  const int TH2 = FY / 2, TW2 = FX / 2, W2 = W / 2, NV = 2 * (W2 / TW2 + 1);
+  const size_t lds = (sizeof(float) + 1) * ((size_t)C * 2 * (W2 + 2) + (size_t)C * TH2 * NV);
+  DRSA_REQUIRE(lds <= 64 * 1024, "first_layer_border: %d channels x %d columns do not fit the LDS", C, W2);
+  DRSA_SMEM(first_layer_bwd_border_kernel, lds);
+  hipLaunchKernelGGL(first_layer_bwd_border_kernel, dim3(H / FY + 1, Bq), dim3(256), lds, s, g, amax, w2, out, C, H,
+                     W, clones, TH2, TW2);
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;
 }

@@ -56,10 +56,11 @@ _DEN_COPY = os.environ.get("DRSA_AMD_DEN_COPY", "0") == "1"
 # A/B switch: 0 = the (2,4) pool backward as a separate unpool (maxpool_bwd) before a dense-g bf16
 # backward conv, instead of folded into its pool-sparse staging (drsa_amd_conv_bwd_bf16_pw)
 _POOL24_SPARSE = os.environ.get("DRSA_AMD_BF16_POOL24_SPARSE", "1") == "1"
-# A/B switch: 0 = the WSquare first layer's contraction as its own kernel (first_layer_bwd) after the
-# second layer's backward, instead of fused into that backward's epilogue plus a border-pixel kernel
-# (drsa_amd_conv_bwd_first_fused: the second layer's R is stored on its tiles' border rings only)
-_FIRST_FUSE = os.environ.get("DRSA_AMD_FIRST_FUSE", "1") == "1"
+# 1 = the WSquare first layer's contraction fused into the second layer's backward epilogue plus a
+# border-pixel kernel (drsa_amd_conv_bwd_first_fused: the second layer's R stored on its tiles'
+# border rings only) instead of its own kernel (first_layer_bwd) after that backward.  Off by
+# default: bit-identical, but measured slower
+_FIRST_FUSE = os.environ.get("DRSA_AMD_FIRST_FUSE", "0") == "1"
 
 
 def _pad32(c: int) -> int:

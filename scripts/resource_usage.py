@@ -6,10 +6,10 @@ import sys
 ROOT = __file__.rsplit("/scripts/", 1)[0]
 
 
-def usage(src):
-    cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off",
+def usage(src, defs=()):
+    cmd = [*()] + ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off",
            "-I", f"{ROOT}/drsa_audio_amd/csrc", "-I", f"{ROOT}/include", "-c", src, "-o", "/dev/null",
-           "-Rpass-analysis=kernel-resource-usage"]
+           "-Rpass-analysis=kernel-resource-usage", *defs]
     out = subprocess.run(cmd, capture_output=True, text=True).stderr
     rows, cur = [], None
     for line in out.splitlines():
@@ -28,8 +28,9 @@ def usage(src):
 
 
 if __name__ == "__main__":
-    for src in sys.argv[1:]:
-        for r in usage(src):
+    defs = [a for a in sys.argv[1:] if a.startswith("-D")]
+    for src in [a for a in sys.argv[1:] if not a.startswith("-D")]:
+        for r in usage(src, defs):
             name = r["name"].replace("(anonymous namespace)::", "")
             name = re.sub(r"\(.*", "", name)
             print(f"{name[:70]:70s} V{r.get('VGPRs'):>4} A{r.get('AGPRs'):>4} occ{r.get('Occupancy [waves/SIMD]'):>2} "

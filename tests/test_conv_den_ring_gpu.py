@@ -158,7 +158,7 @@ def test_plan_ring_equals_den_copy(monkeypatch, hg):
 
 @pytest.mark.parametrize("cin,H,W,sparse,bf16,pool_w", [(64, 16, 256, False, False, 2), (64, 16, 32, True, False, 2),
                                                         (64, 16, 256, True, True, 4), (64, 16, 64, False, True, 2),
-                                                        (32, 8, 16, True, True, 2)])
+                                                        (64, 8, 16, True, True, 2)])
 def test_conv_bwd_den_map_equals_post_div_on_copy(cin, H, W, sparse, bf16, pool_w):
     """drsa_amd_conv_bwd_den_map (the next layer's denominator = its map, one plane for every
     sample: a WSquare layer without a pool, VGGish conv0 -> conv3) equals POST_DIV on the
