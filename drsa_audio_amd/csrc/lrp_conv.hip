@@ -270,7 +270,8 @@ int drsa_amd_conv_bwd_den_ring(const float* g, const uint8_t* g_amax, const void
 }
 
 int drsa_amd_conv_bwd_has_kernel_first_fused(int cin, int cout, int H, int W) {
-  if (cout != 32 || H % 8 != 0 || W % 32 != 0) return 0;
+  // the border kernel runs one band (2W pixels) + 14 rows of strip pairs per workgroup of 256
+  if (cout != 32 || H % 8 != 0 || W % 32 != 0 || 2 * W + 14 * (W / 32 + 1) > 256) return 0;
   return find(pad32(cin), 32, W, 1, A_POOLSPARSE, EPI_BWD, 0, 2, 1) != nullptr;
 }
 
@@ -281,8 +282,9 @@ int drsa_amd_conv_bwd_first_fused(const float* g, const uint8_t* g_amax, const f
   DRSA_REQUIRE(g && g_amax && wts && x && den && first_amax && first_w2 && out && first_out,
                "conv_bwd_first_fused: null pointer");
   DRSA_REQUIRE(Bq > 0 && clones > 0 && Bq % clones == 0, "conv_bwd_first_fused: bad batch/clones");
-  DRSA_REQUIRE(cout == 32 && H % 8 == 0 && W % 32 == 0,
-               "conv_bwd_first_fused: needs cout == 32, H %% 8 == 0 and W %% 32 == 0 (got cout=%d %dx%d)", cout, H, W);
+  DRSA_REQUIRE(cout == 32 && H % 8 == 0 && W % 32 == 0 && 2 * W + 14 * (W / 32 + 1) <= 256,
+               "conv_bwd_first_fused: needs cout == 32, H %% 8 == 0, W %% 32 == 0 and W <= 96 (got cout=%d %dx%d)",
+               cout, H, W);
   DRSA_REQUIRE(!den_const4 || ((uintptr_t)den_const4 & 15) == 0, "conv_bwd_first_fused: den_const4 must be 16-byte aligned");
   const Entry* e = find(pad32(cin), 32, W, 1, A_POOLSPARSE, EPI_BWD, 0, 2, 1);
   if (!e) {

@@ -614,6 +614,11 @@ __device__ __forceinline__ void mfma_chunk_bf(const uint4* hb, const uint4* wb, 
 #ifndef DRSA_FF_DBG
 #define DRSA_FF_DBG 0
 #endif
+// first-layer fusion: 1 = a pixel row's neighbour columns from the adjacent lanes (DPP) instead of
+// two more LDS reads
+#ifndef DRSA_FF_DPP
+#define DRSA_FF_DPP 1
+#endif
 // first-layer fusion: unroll of the contraction's channel loop (4 = all, spills)
 #ifndef DRSA_FF_UNROLL
 #define DRSA_FF_UNROLL 1
@@ -1107,9 +1112,20 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
               int rr = fr - 1 + i;
               rr = rr < 0 ? 0 : rr > FH - 1 ? FH - 1 : rr;
               const float* q = P + (k * FH + rr) * FPS + 4 * fj + 3;
+#if DRSA_FF_DPP
+              // the row's 4 pixels as one ds_read_b128 (8 lanes cover all banks), the neighbours'
+              // edge pixels from the adjacent lanes of the same 16-lane row (DPP row shifts; the
+              // footprint's outer columns only feed border pixels, recomputed elsewhere)
+              const float4 p4 = *reinterpret_cast<const float4*>(q + 1);
+              const float p0 = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                                   0, __builtin_bit_cast(int, p4.w), 0x111, 0xf, 0xf, true));
+              const float p5 = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                                   0, __builtin_bit_cast(int, p4.x), 0x101, 0xf, 0xf, true));
+#else
               const float p0 = q[0];
               const float4 p4 = *reinterpret_cast<const float4*>(q + 1);
               const float p5 = q[5];
+#endif
               pr[i][0] = ff2{p0, p4.x};
               pr[i][1] = ff2{p4.x, p4.y};
               pr[i][2] = ff2{p4.y, p4.z};

@@ -846,6 +846,19 @@ __global__ __launch_bounds__(256) void first_layer_bwd_kernel(const float* __res
 #ifndef DRSA_FQ_C
 #define DRSA_FQ_C 1
 #endif
+// 1: two channel groups of loads in flight (two register sets; 106 VGPRs, 4 waves/SIMD, or spills
+// at 6: the single set at 8 waves/SIMD keeps as many bytes in flight)
+#ifndef DRSA_FQ_DEPTH2
+#define DRSA_FQ_DEPTH2 0
+#endif
+#define FQ_DEPTH2 DRSA_FQ_DEPTH2
+#ifndef DRSA_FQ_WPE
+#define DRSA_FQ_WPE 8
+#endif
+// 1: the 6 x 6 patch streamed row by row (one row of pairs live: fewer VGPRs, more waves)
+#ifndef DRSA_FQ_STREAM
+#define DRSA_FQ_STREAM 1
+#endif
 constexpr int FQ_Y = 16, FQ_X = 64, FQ_C = DRSA_FQ_C;
 constexpr int FQ_RY = FQ_Y + 2, FQ_RX = FQ_X + 2;            // cells incl. halo
 constexpr int FQ_PY = 2 * FQ_RY, FQ_PX = 2 * FQ_RX + 4;      // pixel image (row pad 4)
@@ -866,7 +879,7 @@ __device__ __forceinline__ void fq_put(float* img, int ci, int ry, int rx, float
   d[FQ_PX + 1] = sb == 3 ? v : 0.f;
 }
 
-__global__ __launch_bounds__(256) void first_layer_bwd_pooled_kernel(const float* __restrict__ g,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRSA_FQ_WPE))) void first_layer_bwd_pooled_kernel(const float* __restrict__ g,
                                                                      const uint8_t* __restrict__ amax,
                                                                      const float* __restrict__ w2,
                                                                      float* __restrict__ out, int C, int H, int W,
@@ -886,10 +899,10 @@ __global__ __launch_bounds__(256) void first_layer_bwd_pooled_kernel(const float
   const int hci = tid / (2 * FQ_RY), hr = tid % (2 * FQ_RY);
   const int hry = hr >> 1, hrx = (hr & 1) ? FQ_RX - 1 : 0;
   const bool hact = tid < 2 * FQ_RY * FQ_C;
-  float v[FQ_NS];
-  int sb[FQ_NS];
+  float v[FQ_NS], v2[FQ_DEPTH2 ? FQ_NS : 1];
+  int sb[FQ_NS], sb2[FQ_DEPTH2 ? FQ_NS : 1];
   // loads are unconditional from a clamped (always valid) address and masked afterwards
-  auto fetch = [&](int c0) {
+  auto fetch = [&](int c0, auto& v, auto& sb) {
     const int cx = qx0 + lane;
 #pragma unroll
     for (int ci = 0; ci < FQ_C; ++ci)
@@ -898,40 +911,39 @@ __global__ __launch_bounds__(256) void first_layer_bwd_pooled_kernel(const float
         const int ry = wv4 + 4 * k, cy = qy0 - 1 + ry, c = c0 + ci;
         const bool ok = ry < FQ_RY && c < C && cy >= 0 && cy < H2 && cx < W2;
         const size_t o = ok ? c * plane + (size_t)cy * W2 + cx : 0;
-        const float gv = gb[o];
-        const int av = (int)ab[o];
-        v[ci * FQ_KR + k] = ok ? gv : 0.f;
-        sb[ci * FQ_KR + k] = ok ? av : 4;
+        v[ci * FQ_KR + k] = gb[o];
+        sb[ci * FQ_KR + k] = (int)ab[o];
       }
     {
       const int c = c0 + hci, cy = qy0 - 1 + hry, cxh = qx0 - 1 + hrx;
       const bool ok = hact && c < C && cy >= 0 && cy < H2 && cxh >= 0 && cxh < W2;
       const size_t o = ok ? c * plane + (size_t)cy * W2 + cxh : 0;
-      const float gv = gb[o];
-      const int av = (int)ab[o];
-      v[FQ_NS - 1] = ok ? gv : 0.f;
-      sb[FQ_NS - 1] = ok ? av : 4;
+      v[FQ_NS - 1] = gb[o];
+      sb[FQ_NS - 1] = (int)ab[o];
     }
   };
-  auto stage = [&]() {
+  // the masks are re-evaluated here rather than kept live from the loads: a cell outside the
+  // image / channel range gets argmax 4, i.e. zeros at all four pixels
+  auto stage = [&](int c0, auto& v, auto& sb) {
+    const int cx = qx0 + lane;
 #pragma unroll
     for (int ci = 0; ci < FQ_C; ++ci)
 #pragma unroll
       for (int k = 0; k < FQ_KR; ++k) {
-        const int ry = wv4 + 4 * k;
-        if (ry < FQ_RY) fq_put(img, ci, ry, 1 + lane, v[ci * FQ_KR + k], sb[ci * FQ_KR + k]);
+        const int ry = wv4 + 4 * k, cy = qy0 - 1 + ry, c = c0 + ci;
+        const bool ok = ry < FQ_RY && c < C && cy >= 0 && cy < H2 && cx < W2;
+        if (ry < FQ_RY) fq_put(img, ci, ry, 1 + lane, v[ci * FQ_KR + k], ok ? sb[ci * FQ_KR + k] : 4);
       }
-    if (hact) fq_put(img, hci, hry, hrx, v[FQ_NS - 1], sb[FQ_NS - 1]);
+    {
+      const int c = c0 + hci, cy = qy0 - 1 + hry, cxh = qx0 - 1 + hrx;
+      const bool ok = hact && c < C && cy >= 0 && cy < H2 && cxh >= 0 && cxh < W2;
+      if (hact) fq_put(img, hci, hry, hrx, v[FQ_NS - 1], ok ? sb[FQ_NS - 1] : 4);
+    }
   };
   fq2 acc[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = fq2{0.f, 0.f};
-  fetch(0);
-  for (int c0 = 0; c0 < C; c0 += FQ_C) {
-    __syncthreads();
-    stage();
-    __syncthreads();
-    if (c0 + FQ_C < C) fetch(c0 + FQ_C);
+  auto compute = [&](int c0) {
 #pragma unroll
     for (int ci = 0; ci < FQ_C; ++ci) {
       const int c = c0 + ci;
@@ -940,8 +952,31 @@ __global__ __launch_bounds__(256) void first_layer_bwd_pooled_kernel(const float
       for (int t = 0; t < 9; ++t) wv[t] = (c < C) ? w2[c * 9 + t] : 0.f;
       // patch P[i][j] = pixel (2qy0 + 4ty - 1 + i, 2qx0 + 4tx - 1 + j) = img[4ty + 1 + i][4tx + FQ_C0 + 1 + j];
       // pair q (q = 0..4) = (P[i][q], P[i][q + 1])
-      fq2 pr[6][5];
       const float* base = img + (ci * FQ_PY + 4 * ty + 1) * FQ_PX + 4 * tx + FQ_C0 + 1;
+#if DRSA_FQ_STREAM
+      // patch rows streamed: row i feeds output rows py = i - 1 - dy, i.e. each output row takes
+      // its taps in dy order (then dx) -- the chain order -- with only one patch row live
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const float* r = base + i * FQ_PX;
+        const float4 q4 = *reinterpret_cast<const float4*>(r);
+        const fq2 q2 = *reinterpret_cast<const fq2*>(r + 4);
+        const fq2 rp[5] = {fq2{q4.x, q4.y}, fq2{q4.y, q4.z}, fq2{q4.z, q4.w}, fq2{q4.w, q2.x}, q2};
+#pragma unroll
+        for (int py = 0; py < 4; ++py) {
+          const int dy = i - py - 1;
+          if (dy < -1 || dy > 1) continue;
+#pragma unroll
+          for (int dx = -1; dx <= 1; ++dx) {
+            const float w = wv[(1 - dy) * 3 + (1 - dx)];
+            const fq2 ww = fq2{w, w};
+            acc[py][0] = __builtin_elementwise_fma(rp[1 + dx], ww, acc[py][0]);
+            acc[py][1] = __builtin_elementwise_fma(rp[3 + dx], ww, acc[py][1]);
+          }
+        }
+      }
+#else
+      fq2 pr[6][5];
 #pragma unroll
       for (int i = 0; i < 6; ++i) {
         const float* r = base + i * FQ_PX;
@@ -964,8 +999,36 @@ __global__ __launch_bounds__(256) void first_layer_bwd_pooled_kernel(const float
             acc[py][0] = __builtin_elementwise_fma(pr[py + 1 + dy][1 + dx], ww, acc[py][0]);
             acc[py][1] = __builtin_elementwise_fma(pr[py + 1 + dy][3 + dx], ww, acc[py][1]);
           }
+#endif
     }
+  };
+#if FQ_DEPTH2
+  // two register sets: channel group c + 2 is in flight while c is computed (c + 1 already landed)
+  fetch(0, v, sb);
+  if (FQ_C < C) fetch(FQ_C, v2, sb2);
+  for (int c0 = 0; c0 < C; c0 += 2 * FQ_C) {
+    __syncthreads();
+    stage(c0, v, sb);
+    __syncthreads();
+    if (c0 + 2 * FQ_C < C) fetch(c0 + 2 * FQ_C, v, sb);
+    compute(c0);
+    if (c0 + FQ_C >= C) break;
+    __syncthreads();
+    stage(c0 + FQ_C, v2, sb2);
+    __syncthreads();
+    if (c0 + 3 * FQ_C < C) fetch(c0 + 3 * FQ_C, v2, sb2);
+    compute(c0 + FQ_C);
   }
+#else
+  fetch(0, v, sb);
+  for (int c0 = 0; c0 < C; c0 += FQ_C) {
+    __syncthreads();
+    stage(c0, v, sb);
+    __syncthreads();
+    if (c0 + FQ_C < C) fetch(c0 + FQ_C, v, sb);
+    compute(c0);
+  }
+#endif
   const int oy = 2 * qy0 + 4 * ty, ox = 2 * qx0 + 4 * tx;
   if (2 * (qx0 + 2 * tx) < W && ox < W) {
 #pragma unroll
@@ -978,98 +1041,107 @@ __global__ __launch_bounds__(256) void first_layer_bwd_pooled_kernel(const float
 }
 
 // The border pixels of drsa_amd_conv_bwd_first_fused's FY x FX footprints (FY = 2 TH2, FX = 2 TW2):
-// workgroup (k, bq) takes the horizontal band of pixel rows FY k - 1, FY k (cell rows TH2 k - 1,
-// TH2 k, all columns) and, for k < H2 / TH2, the vertical strips of footprint row k (pixel rows
-// FY k + 1 .. FY k + FY - 2 at pixel columns FX m - 1, FX m: cell columns TW2 m - 1, TW2 m).  The
-// cells are staged in LDS (coalesced loads, zero / no-match outside the image); each pixel runs
-// the chain of first_layer_bwd_pooled_kernel (channel ascending, then dy, dx; zero terms included)
-// over the 2 x 2 cells under its 3 x 3 window -- cells on the footprints' rings, where the fused
-// kernel stored g.
+// workgroup (k, bq) takes the horizontal band of pixel rows FY k - 1, FY k and, for k < H / FY,
+// the vertical strips of footprint row k (pixel rows FY k + 1 .. FY k + FY - 2 at pixel columns
+// FX m - 1, FX m).  The cells under them (on the footprints' rings, where the fused kernel stored
+// g) are expanded once into pixel images in LDS (value at the argmax pixel, zeros elsewhere and
+// outside the image): the band image holds pixel rows FY k - 2 .. FY k + 1 (column X at X + 4),
+// the strip image pixel rows FY k .. FY k + FY - 1 x columns FX m - 2 .. FX m + 1.  Each thread
+// then runs one pixel pair through the chain of first_layer_bwd_pooled_kernel (channel
+// ascending, then dy, dx; zero terms included) with packed fmas.
+constexpr int FLB_CG = 8;   // channels per staged group of the border kernel
+
 __global__ __launch_bounds__(256) void first_layer_bwd_border_kernel(const float* __restrict__ g,
                                                                      const uint8_t* __restrict__ amax,
                                                                      const float* __restrict__ w2,
                                                                      float* __restrict__ out, int C, int H, int W,
                                                                      int clones, int TH2, int TW2) {
   extern __shared__ __attribute__((aligned(16))) float bsm[];
+  typedef float bf2 __attribute__((ext_vector_type(2)));
   const int tid = threadIdx.x;
-  const int H2 = H >> 1, W2 = W >> 1, WP = W2 + 2, FY = 2 * TH2, FX = 2 * TW2;
-  const int NV = 2 * (W2 / TW2 + 1);
-  float* HV = bsm;                                              // [C][2][WP]   band cells (column + 1)
-  float* VV = HV + (size_t)C * 2 * WP;                          // [C][TH2][NV] strip cells
-  uint8_t* HA = reinterpret_cast<uint8_t*>(VV + (size_t)C * TH2 * NV);
-  uint8_t* VA = HA + (size_t)C * 2 * WP;
+  const int H2 = H >> 1, W2 = W >> 1, FY = 2 * TH2, FX = 2 * TW2;
+  const int WB = W + 8, NM = W / FX + 1, WS = 4 * NM;
+  float* BI = bsm;                                   // [CG][4][WB]
+  float* SI = BI + (size_t)FLB_CG * 4 * WB;          // [CG][FY][WS]
   const int k = blockIdx.x, bq = blockIdx.y, bs = bq / clones;
-  const bool vert = k < H2 / TH2;
+  const bool vert = k < H / FY;
   const size_t plane = (size_t)H2 * W2;
   const float* gb = g + (size_t)bq * C * plane;
   const uint8_t* ab = amax + (size_t)bs * C * plane;
-  for (int i = tid; i < C * 2 * WP; i += 256) {
-    const int c = i / (2 * WP), rem = i % (2 * WP);
-    const int cy = k * TH2 - 1 + rem / WP, cx = rem % WP - 1;
-    const bool ok = cy >= 0 && cy < H2 && cx >= 0 && cx < W2;
+  // expand cell (cy, cx) of channel c into the 2 x 2 pixels at image row r0, column x0 of slot cl
+  auto cell = [&](float* img, int ws, int rows, int cl, int c, int cy, int cx, int r0, int x0) {
+    const bool ok = c < C && cy >= 0 && cy < H2 && cx >= 0 && cx < W2;
     const size_t o = ok ? c * plane + (size_t)cy * W2 + cx : 0;
     const float v = gb[o];
-    const int a8 = ab[o];
-    HV[i] = ok ? v : 0.f;
-    HA[i] = (uint8_t)(ok ? a8 : 4);
-  }
-  if (vert) {
-    for (int i = tid; i < C * TH2 * NV; i += 256) {
-      const int c = i / (TH2 * NV), rem = i % (TH2 * NV), j = rem % NV;
-      const int cy = k * TH2 + rem / NV, cx = TW2 * (j >> 1) - 1 + (j & 1);
-      const bool ok = cx >= 0 && cx < W2;
-      const size_t o = ok ? c * plane + (size_t)cy * W2 + cx : 0;
-      const float v = gb[o];
-      const int a8 = ab[o];
-      VV[i] = ok ? v : 0.f;
-      VA[i] = (uint8_t)(ok ? a8 : 4);
-    }
-  }
-  __syncthreads();
-  // one pixel: cells (iy, ix) of its window at V[c * cs + (r0 + iy) * rs + c0 + ix]
-  auto pixel = [&](int Y, int X, const float* V, const uint8_t* A, int cs, int rs, int r0, int c0) {
-    int toff[9], ts[9];
-    bool tin[9];
-#pragma unroll
-    for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-      for (int dx = -1; dx <= 1; ++dx) {
-        const int t = (dy + 1) * 3 + dx + 1, yy = Y + dy, xx = X + dx;
-        tin[t] = yy >= 0 && yy < H && xx >= 0 && xx < W;
-        toff[t] = (r0 + ((yy >> 1) - ((Y - 1) >> 1))) * rs + c0 + ((xx >> 1) - ((X - 1) >> 1));
-        ts[t] = (yy & 1) * 2 + (xx & 1);
-      }
-    float acc = 0.f;
-#pragma unroll 2
-    for (int c = 0; c < C; ++c) {
-      float wv[9];
-#pragma unroll
-      for (int t = 0; t < 9; ++t) wv[t] = w2[c * 9 + t];
-#pragma unroll
-      for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-        for (int dx = -1; dx <= 1; ++dx) {
-          const int t = (dy + 1) * 3 + dx + 1;
-          const int o = c * cs + toff[t];
-          const float vq = V[o];
-          const bool hit = tin[t] && A[o] == ts[t];
-          acc = fmaf(hit ? vq : 0.f, wv[(1 - dy) * 3 + (1 - dx)], acc);
-        }
-    }
-    out[((size_t)bq * H + Y) * W + X] = acc;
+    const int s = ok ? (int)ab[o] : 4;
+    float* d = img + ((size_t)cl * rows + r0) * ws + x0;
+    d[0] = s == 0 ? v : 0.f;
+    d[1] = s == 1 ? v : 0.f;
+    d[ws] = s == 2 ? v : 0.f;
+    d[ws + 1] = s == 3 ? v : 0.f;
   };
-  for (int p = tid; p < 2 * W; p += 256) {
-    const int Y = k * FY - 1 + p / W, X = p % W;
-    // band cell row 0 = TH2 k - 1, column index = cell column + 1
-    if (Y >= 0 && Y < H) pixel(Y, X, HV, HA, 2 * WP, WP, ((Y - 1) >> 1) - (k * TH2 - 1), ((X - 1) >> 1) + 1);
+  // pair p: band pairs first (row FY k - 1 + p / (W / 2), columns 2 (p % (W / 2)) + 0, 1), then the
+  // strip pairs (row FY k + 1 + q / NM, columns FX m - 1, FX m with m = q % NM); one per thread
+  const int nband = W, nstrip = vert ? (FY - 2) * NM : 0;
+  const int p = tid;
+  int Y = -1, X0 = 0, ws = WB, cstride = 4 * WB;
+  const float* rowp = BI;   // image row of pixel row Y - 1, at the column of pixel X0 - 1
+  if (p < nband) {
+    const int r = p / (W / 2);
+    Y = k * FY - 1 + r;
+    X0 = 2 * (p % (W / 2));
+    rowp = BI + r * WB + X0 + 3;
+  } else if (p < nband + nstrip) {
+    const int q = p - nband, m = q % NM;
+    Y = k * FY + 1 + q / NM;
+    X0 = FX * m - 1;
+    rowp = SI + (Y - 1 - k * FY) * WS + 4 * m;
+    ws = WS;
+    cstride = FY * WS;
   }
-  if (vert) {
-    for (int p = tid; p < (FY - 2) * NV; p += 256) {
-      const int j = p % NV, Y = k * FY + 1 + p / NV, X = FX * (j >> 1) - 1 + (j & 1);
-      // strip cell row 0 = TH2 k; strip column 2m + 0/1 = cell column TW2 m - 1 / TW2 m
-      if (X >= 0 && X < W)
-        pixel(Y, X, VV, VA, TH2 * NV, NV, ((Y - 1) >> 1) - k * TH2, 2 * (j >> 1) + (((X - 1) >> 1) - (TW2 * (j >> 1) - 1)));
+  const bool act = p < nband + nstrip;
+  bf2 acc = bf2{0.f, 0.f};
+  for (int c0 = 0; c0 < C; c0 += FLB_CG) {
+    if (c0) __syncthreads();
+    // band: cell rows TH2 k - 1 (image rows 0, 1) and TH2 k (rows 2, 3); cell columns -2 .. W2 + 1
+    for (int i = tid; i < FLB_CG * 2 * (W2 + 4); i += 256) {
+      const int cl = i / (2 * (W2 + 4)), rem = i % (2 * (W2 + 4));
+      const int rr = rem / (W2 + 4), cx = rem % (W2 + 4) - 2;
+      cell(BI, WB, 4, cl, c0 + cl, k * TH2 - 1 + rr, cx, 2 * rr, 2 * cx + 4);
     }
+    if (vert) {
+      // strips: cell rows TH2 k .. TH2 k + TH2 - 1, cell columns TW2 m - 1, TW2 m
+      for (int i = tid; i < FLB_CG * TH2 * 2 * NM; i += 256) {
+        const int cl = i / (TH2 * 2 * NM), rem = i % (TH2 * 2 * NM);
+        const int ry = rem / (2 * NM), j = rem % (2 * NM), m = j >> 1;
+        cell(SI, WS, FY, cl, c0 + cl, k * TH2 + ry, TW2 * m - 1 + (j & 1), 2 * ry, 4 * m + 2 * (j & 1));
+      }
+    }
+    __syncthreads();
+    if (act) {
+#pragma unroll 2
+      for (int cl = 0; cl < FLB_CG; ++cl) {
+        const int c = c0 + cl;
+        if (c >= C) break;
+        float wv[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) wv[t] = w2[c * 9 + t];
+        const float* rp = rowp + (size_t)cl * cstride;
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy) {
+          const float* r = rp + (dy + 1) * ws;
+          const float e0 = r[0], e1 = r[1], e2 = r[2], e3 = r[3];
+          const bf2 q0 = bf2{e0, e1}, q1 = bf2{e1, e2}, q2 = bf2{e2, e3};
+          acc = __builtin_elementwise_fma(q0, bf2{wv[(1 - dy) * 3 + 2], wv[(1 - dy) * 3 + 2]}, acc);
+          acc = __builtin_elementwise_fma(q1, bf2{wv[(1 - dy) * 3 + 1], wv[(1 - dy) * 3 + 1]}, acc);
+          acc = __builtin_elementwise_fma(q2, bf2{wv[(1 - dy) * 3], wv[(1 - dy) * 3]}, acc);
+        }
+      }
+    }
+  }
+  if (act) {
+    if (Y >= 0 && Y < H && X0 >= 0) out[((size_t)bq * H + Y) * W + X0] = acc.x;
+    if (Y >= 0 && Y < H && X0 + 1 < W) out[((size_t)bq * H + Y) * W + X0 + 1] = acc.y;
   }
 }
 
@@ -1425,12 +1497,12 @@ int drsa_first_layer_border(const float* g, const uint8_t* amax, const float* w2
                             int C, int H, int W, int FY, int FX, hipStream_t s) {
   DRSA_REQUIRE(FY >= 4 && FX >= 4 && FY % 2 == 0 && FX % 2 == 0 && H % FY == 0 && W % FX == 0,
                "first_layer_border: bad footprint");
-  const int TH2 = FY / 2, TW2 = FX / 2, W2 = W / 2, NV = 2 * (W2 / TW2 + 1);
-  const size_t lds = (sizeof(float) + 1) * ((size_t)C * 2 * (W2 + 2) + (size_t)C * TH2 * NV);
-  DRSA_REQUIRE(lds <= 64 * 1024, "first_layer_border: %d channels x %d columns do not fit the LDS", C, W2);
+  const size_t lds = sizeof(float) * ((size_t)FLB_CG * 4 * (W + 8) + (size_t)FLB_CG * FY * 4 * (W / FX + 1));
+  DRSA_REQUIRE(lds <= 64 * 1024 && W + (H / FY > 0 ? (FY - 2) * (W / FX + 1) : 0) <= 256,
+               "first_layer_border: %d x %d pixels do not fit one workgroup", H, W);
   DRSA_SMEM(first_layer_bwd_border_kernel, lds);
   hipLaunchKernelGGL(first_layer_bwd_border_kernel, dim3(H / FY + 1, Bq), dim3(256), lds, s, g, amax, w2, out, C, H,
-                     W, clones, TH2, TW2);
+                     W, clones, FY / 2, FX / 2);
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;
 }

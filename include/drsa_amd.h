@@ -236,7 +236,7 @@ int drsa_amd_conv_bwd_has_kernel_bf16(int cin, int cout, int W, int ng, int spar
  * order (channel ascending, then dy, dx); `out` receives R only on the tiles' border cell rings,
  * from which a second kernel computes the footprints' border pixels.  first_out is bit-identical
  * to drsa_amd_conv_bwd (or _den_ring) + drsa_amd_first_layer_bwd; `out` is NOT the full R.
- * Needs cout == 32 (the first layer's channels), H % 8 == 0, W % 32 == 0; H, W at pooled
+ * Needs cout == 32 (the first layer's channels), H % 8 == 0, W % 32 == 0, W <= 96; H, W at pooled
  * resolution.  drsa_amd_conv_bwd_has_kernel_first_fused reports support for (cin, cout, H, W). */
 int drsa_amd_conv_bwd_first_fused(const float* g, const uint8_t* g_amax, const float* wts, const float* x,
                                   const float* den, const float* den_const4, const uint8_t* first_amax,

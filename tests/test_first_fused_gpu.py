@@ -106,6 +106,7 @@ def test_fused_first_layer_rejects():
     assert lib.drsa_amd_conv_bwd_has_kernel_first_fused(32, 32, 64, 48) == 0     # W % 32
     assert lib.drsa_amd_conv_bwd_has_kernel_first_fused(32, 64, 64, 64) == 0     # cout != 32
     assert lib.drsa_amd_conv_bwd_has_kernel_first_fused(128, 32, 64, 64) == 0    # no instance
+    assert lib.drsa_amd_conv_bwd_has_kernel_first_fused(32, 32, 64, 128) == 0    # border workgroup width
     assert lib.drsa_amd_conv_bwd_first_fused(None, None, None, None, None, None, None, None, None, None, 2, 1, 32, 32,
                                              8, 32, 0.0, None) == -1
 
