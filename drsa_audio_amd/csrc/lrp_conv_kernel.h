@@ -610,6 +610,10 @@ __device__ __forceinline__ void mfma_chunk_bf(const uint4* hb, const uint4* wb, 
   }
 }
 
+// backward: XCD-aware (sample, tile, clone) order of the workgroups (1) or the launch order (0)
+#ifndef DRSA_CONV_BWD_REMAP
+#define DRSA_CONV_BWD_REMAP 0   // measured: no change at 4 clones
+#endif
 // first-layer fusion ablation (experiments only): 1 = no contraction, 2 = no pixel image either
 #ifndef DRSA_FF_DBG
 #define DRSA_FF_DBG 0
@@ -641,9 +645,22 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
   const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
   const int H = a.H, W = a.W;
   const int tiles_x = (W + TW - 1) / TW;
-  const int ty0 = (blockIdx.x / tiles_x) * TH;
-  const int tx0 = (blockIdx.x % tiles_x) * TW;
-  const int bq = blockIdx.y;                  // batch index (incl. clones)
+  int tile_id = blockIdx.x, bq = blockIdx.y;  // bq: batch index (incl. clones)
+  if constexpr (EPI == EPI_BWD && DRSA_CONV_BWD_REMAP) {
+    // XCD-aware order: dispatch id d runs on XCD d % 8; give each XCD a contiguous run of
+    // (sample, tile, clone) items, clones fastest, so the clones of a tile (which read the same
+    // x / den tile) and the neighbouring tiles (which share g halo rows) meet in one L2
+    const int ntile = gridDim.x, total = ntile * gridDim.y;
+    if (total % 8 == 0) {
+      const int id = blockIdx.x + blockIdx.y * ntile;
+      const int L = (id & 7) * (total >> 3) + (id >> 3);
+      const int q = L % a.clones, rest = L / a.clones;
+      tile_id = rest % ntile;
+      bq = (rest / ntile) * a.clones + q;
+    }
+  }
+  const int ty0 = (tile_id / tiles_x) * TH;
+  const int tx0 = (tile_id % tiles_x) * TW;
   const int bs = bq / a.clones;               // sample index (shared forward state)
   const int wm = w % WM, wn = w / WM;
   const bool active = w < WM * Cfg::WN;

@@ -719,7 +719,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
 //   R[y][x] = sum_co sum_{dy,dx} G[co][y+dy][x+dx] * W2[co][1-dy][1-dx]
 //   G from pool-sparse (gp, argmax) or dense; 16 x 64 output tile, 4 pixels per thread
 // ===========================================================================
-constexpr int FL_TH = 16, FL_TW = 64, FL_CC = 8;
+#ifndef DRSA_FL_TH
+#define DRSA_FL_TH 16
+#endif
+#ifndef DRSA_FL_CC
+#define DRSA_FL_CC 4
+#endif
+constexpr int FL_TH = DRSA_FL_TH, FL_TW = 64, FL_CC = DRSA_FL_CC;
 constexpr int FL_HY = FL_TH + 2, FL_RS = FL_TW + 8;           // LDS row: halo col 3, interior 4..67, halo 68
 constexpr int FL_ROWS = FL_CC * FL_HY;                        // staged rows per channel group
 constexpr int FL_NV4 = FL_ROWS * (FL_TW / 4);                 // interior float4 per group
