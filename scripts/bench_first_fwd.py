@@ -21,9 +21,15 @@ s = _capi.stream_ptr()
 
 
 NODEN = os.environ.get("NODEN") == "1"
+RING = os.environ.get("RING", "1") == "1"   # the engine's form: den copy on the border ring only
+den_ring = torch.empty(B, C, 2 * (W // 2) + 8 * (H // 2 - 2), device=dev)
 
 
 def run():
+    if RING and not NODEN:
+        _capi.call("drsa_amd_conv_fwd_den_ring", x.data_ptr(), wts.data_ptr(), bias.data_ptr(), den_map.data_ptr(),
+                   out.data_ptr(), amax.data_ptr(), den_ring.data_ptr(), B, C, H, W, 1, s)
+        return
     _capi.call("drsa_amd_conv_fwd", x.data_ptr(), wts.data_ptr(), bias.data_ptr(), None if NODEN else den_map.data_ptr(),
                out.data_ptr(), amax.data_ptr(), None if NODEN else den.data_ptr(), B, 1, C, H, W, 1, 1, s)
 
@@ -41,4 +47,5 @@ for cs in sys.argv[1:] or ["0"]:
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 20
     byts = x.numel() * 4 + out.numel() * 9
-    print(json.dumps({"noden": NODEN, "csplit": cs, "ms": ms, "GBs": byts / ms / 1e6}))
+    print(json.dumps({"lib": os.environ.get("DRSA_AMD_LIB", "base"), "noden": NODEN, "ring": RING, "csplit": cs,
+                      "ms": ms, "GBs": byts / ms / 1e6}))
