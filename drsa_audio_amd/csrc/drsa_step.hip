@@ -725,6 +725,9 @@ struct PartialPlan {
 PartialPlan plan_partial(int64_t N) {
   const int64_t rbt = (N + 15) / 16;
   int64_t grid = drsa::cu_count();   // one workgroup per CU; rows are split in 16-row blocks
+  // tuning knob (experiments): at most this many workgroups (fewer slabs for the reduce)
+  static const int gmax = getenv("DRSA_AMD_PARTIAL_GRID") ? atoi(getenv("DRSA_AMD_PARTIAL_GRID")) : 0;
+  if (gmax > 0 && grid > gmax) grid = gmax;
   if (grid > rbt) grid = rbt;
   if (grid < 1) grid = 1;
   return {(int)grid, rbt};
