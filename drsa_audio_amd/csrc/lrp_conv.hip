@@ -50,6 +50,9 @@ const Entry* find(int cin_p, int cout_p, int W, int ng, int amode, int epi, int 
 }
 
 int launch(const Entry* e, const ConvArgs& args, int batch, hipStream_t s) {   // batch = grid.y
+  // the kernels address one sample's planes with 32-bit offsets from a per-sample base
+  DRSA_REQUIRE((int64_t)(args.cin > args.cout ? args.cin : args.cout) * args.H * args.W < ((int64_t)1 << 31),
+               "conv: one sample's channels x H x W must stay below 2^31");
   DRSA_SMEM(e->fn, e->lds);   // per device, thread-safe
   const int tiles = ((args.H + e->th - 1) / e->th) * ((args.W + e->tw - 1) / e->tw);
   hipLaunchKernelGGL(e->fn, dim3(tiles, batch), dim3(kThreads), e->lds, s, args);

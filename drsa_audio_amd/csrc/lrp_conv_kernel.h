@@ -184,6 +184,10 @@ struct Stager {
   __device__ __forceinline__ void load(const ConvArgs& a, int c0, int tid, int ty0, int tx0, int bq, int bs) {
     const int H = a.H, W = a.W, H2 = H >> 1, W2 = W >> 1;
     const bool noload = (a.dbg & 1) != 0;
+    // per-sample bases (uniform) + 32-bit per-lane offsets: saddr + voffset loads instead of a
+    // 64-bit multiply-add per element (the host keeps one sample's cin x H x W below 2^31)
+    const float* __restrict__ inb = a.in + (size_t)bq * a.cin * (DENSE ? H * W : H2 * W2);
+    const uint8_t* __restrict__ amb = DENSE ? nullptr : a.in_amax + (size_t)bs * a.cin * H2 * W2;
     if constexpr (DENSE) {
       if ((W & 3) == 0) {
 #pragma unroll
@@ -193,8 +197,8 @@ struct Stager {
           const int ci = row / HY, hy = row % HY;
           const int gy = ty0 - 1 + hy, gx = tx0 + 4 * q, c = c0 + ci;
           const bool ok = i < DROWS * Q4 && gy >= 0 && gy < H && c < a.cin && gx < W && !noload;
-          const size_t o = ok ? (((size_t)bq * a.cin + c) * H + gy) * W + gx : 0;
-          const float4 v = *reinterpret_cast<const float4*>(a.in + o);
+          const int o = ok ? (c * H + gy) * W + gx : 0;
+          const float4 v = *reinterpret_cast<const float4*>(inb + o);
           st_i[it] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
         }
       } else {
@@ -209,8 +213,8 @@ struct Stager {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const bool ok = rok && gx + e < W;
-            const size_t o = ok ? (((size_t)bq * a.cin + c) * H + gy) * W + gx + e : 0;
-            const float v = a.in[o];
+            const int o = ok ? (c * H + gy) * W + gx + e : 0;
+            const float v = inb[o];
             vv[e] = ok ? v : 0.f;
           }
           st_i[it] = make_float4(vv[0], vv[1], vv[2], vv[3]);
@@ -223,8 +227,8 @@ struct Stager {
         const int ci = row / HY, hy = row % HY;
         const int gy = ty0 - 1 + hy, gx = side ? tx0 + TW : tx0 - 1, c = c0 + ci;
         const bool ok = i < DROWS * 2 && gy >= 0 && gy < H && gx >= 0 && gx < W && c < a.cin && !noload;
-        const size_t o = ok ? (((size_t)bq * a.cin + c) * H + gy) * W + gx : 0;
-        const float v = a.in[o];
+        const int o = ok ? (c * H + gy) * W + gx : 0;
+        const float v = inb[o];
         st_h[it] = ok ? v : 0.f;
       }
     } else {
@@ -237,10 +241,9 @@ struct Stager {
           const int ci = row / CY, ry = row % CY;
           const int cy = qy0 + ry, cx = qx0 + 1 + 4 * q, c = c0 + ci;
           const bool ok = i < SROWS * Q8 && 4 * q < TW / 2 && cy >= 0 && cy < H2 && c < a.cin && cx < W2 && !noload;
-          const size_t o = ok ? (((size_t)bq * a.cin + c) * H2 + cy) * W2 + cx : 0;
-          const size_t oa = ok ? (((size_t)bs * a.cin + c) * H2 + cy) * W2 + cx : 0;
-          const float4 v = *reinterpret_cast<const float4*>(a.in + o);
-          const uint32_t am = *reinterpret_cast<const uint32_t*>(a.in_amax + oa);
+          const int o = ok ? (c * H2 + cy) * W2 + cx : 0;
+          const float4 v = *reinterpret_cast<const float4*>(inb + o);
+          const uint32_t am = *reinterpret_cast<const uint32_t*>(amb + o);
           st_i[it] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
           st_ia[it] = ok ? am : 0x04040404u;
         }
@@ -257,10 +260,9 @@ struct Stager {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const bool ok = rok && cx + e < W2 && 4 * q + e < TW / 2;
-            const size_t o = ok ? (((size_t)bq * a.cin + c) * H2 + cy) * W2 + cx + e : 0;
-            const size_t oa = ok ? (((size_t)bs * a.cin + c) * H2 + cy) * W2 + cx + e : 0;
-            const float v = a.in[o];
-            const uint32_t am = a.in_amax[oa];
+            const int o = ok ? (c * H2 + cy) * W2 + cx + e : 0;
+            const float v = inb[o];
+            const uint32_t am = amb[o];
             vv[e] = ok ? v : 0.f;
             aa |= (ok ? am : 4u) << (8 * e);
           }
@@ -275,10 +277,9 @@ struct Stager {
         const int ci = row / CY, ry = row % CY;
         const int cy = qy0 + ry, cx = side ? qx0 + CX - 1 : qx0, c = c0 + ci;
         const bool ok = i < SROWS * 2 && cy >= 0 && cy < H2 && cx >= 0 && cx < W2 && c < a.cin && !noload;
-        const size_t o = ok ? (((size_t)bq * a.cin + c) * H2 + cy) * W2 + cx : 0;
-        const size_t oa = ok ? (((size_t)bs * a.cin + c) * H2 + cy) * W2 + cx : 0;
-        const float v = a.in[o];
-        const int am = (int)a.in_amax[oa];
+        const int o = ok ? (c * H2 + cy) * W2 + cx : 0;
+        const float v = inb[o];
+        const int am = (int)amb[o];
         st_h[it] = ok ? v : 0.f;
         st_ha[it] = ok ? am : 4;
       }
@@ -781,6 +782,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
   const int ring_i = !pix_ok ? 0 : Y == 0 ? X : Y == H - 1 ? W + X : 2 * W + (Y - 1) * 8 + (X == 0 ? 0 : 4);
   const float* rsrc = ring ? a.den + (size_t)bs * a.cout * ring_n + ring_i : dsrc;
   const size_t dstride = ring ? (size_t)ring_n : (size_t)HW;
+  // x loads and R stores as a uniform per-sample base + a 32-bit per-lane offset (saddr + voffset
+  // addressing; the host keeps one sample's cout x H x W below 2^31)
+  const unsigned upix = (unsigned)pix;
+  float* const obase = a.out + (size_t)bq * a.cout * HW;
+  const float* const xbase = a.x ? a.x + (size_t)bs * a.cout * HW : obase;
   // FF: float4 groups on the tile's border ring still store R (the border pixels' contraction
   // needs the neighbour tiles' cells: drsa_amd_first_layer_bwd_border); the first layer's argmax
   // of the group's 4 cells is one 32-bit load; contraction thread (fr, fj) owns footprint pixels
@@ -800,7 +806,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
       const int co = gchs(cl, v, sub);
       const bool ok = cl < TCH && co < a.cout;
       const int coc = ok ? co : 0;
-      if (lx) xk[it] = *reinterpret_cast<const float4*>(xsrc + (size_t)coc * HW);
+      if (lx) xk[it] = *reinterpret_cast<const float4*>(xbase + (upix + (unsigned)coc * (unsigned)HW));
       if (ld) dk[it] = *reinterpret_cast<const float4*>(use_c4 ? a.den_const4 + (size_t)coc * 4 : rsrc + coc * dstride);
     }
   };
@@ -1178,7 +1184,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
             return (xx > 0.f) ? q : 0.f;
           };
           const float4 R = make_float4(f(t.x, x.x, d.x), f(t.y, x.y, d.y), f(t.z, x.z, d.z), f(t.w, x.w, d.w));
-          if (ok && pix_ok) *reinterpret_cast<float4*>(oqp + (size_t)coc * HW) = R;
+          if (ok && pix_ok) *reinterpret_cast<float4*>(obase + (upix + (unsigned)coc * (unsigned)HW)) = R;
         }
         continue;
       }
@@ -1231,7 +1237,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
           return (post_any && !(xx > 0.f)) ? 0.f : y;
         };
         R = make_float4(post(R.x, x.x, d.x), post(R.y, x.y, d.y), post(R.z, x.z, d.z), post(R.w, x.w, d.w));
-        if (ok && pix_ok) *reinterpret_cast<float4*>(oqp + (size_t)coc * HW) = R;
+        if (ok && pix_ok) *reinterpret_cast<float4*>(obase + (upix + (unsigned)coc * (unsigned)HW)) = R;
       }
      }
       if constexpr (FF) {

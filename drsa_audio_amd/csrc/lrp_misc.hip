@@ -248,6 +248,10 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
   const int TW = W < 32 ? W : 32, RPT = P / TW;      // tile = RPT rows x TW cols
   const int HW = H * W, xt = W / TW;
   const int d4 = (d + 3) & ~3;
+  // per-sample bases + 32-bit per-lane offsets (saddr + voffset addressing; d * H * W < 2^31)
+  const float* __restrict__ a_b = a + (size_t)b * d * HW;
+  float* __restrict__ h_b = h ? h + (size_t)b * d * HW : nullptr;
+  float* __restrict__ ap_b = ap ? ap + (size_t)b * d * HW : nullptr;
   stage_u_padded<DP>(Us, U, d, tid);
   if constexpr (PLDS) stage_p<DP>(Ps, Pm, d, tid);
   constexpr int NB = DP / 16;
@@ -275,7 +279,7 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
     for (int u = 0; u < (PFT ? NPF : 0); ++u) {
       const int i = tid + 256 * u, c = i / P, p = i % P;
       const bool ok = c < d;
-      const float v = a[((size_t)b * d + (ok ? c : 0)) * HW + (y0 + p / TW) * W + x0 + p % TW];
+      const float v = a_b[(ok ? c : 0) * HW + (y0 + p / TW) * W + x0 + p % TW];
       pf[u] = ok ? v : 0.f;
     }
   };
@@ -296,7 +300,7 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
       for (int i = tid; i < DP * P; i += 256) {
         const int c = i / P, p = i % P;
         const bool ok = c < d;
-        const float v = a[((size_t)b * d + (ok ? c : 0)) * HW + (y0 + p / TW) * W + x0 + p % TW];
+        const float v = a_b[(ok ? c : 0) * HW + (y0 + p / TW) * W + x0 + p % TW];
         as[c * PL + p] = ok ? v : 0.f;
       }
     }
@@ -339,11 +343,11 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int j = jb * 16 + (lane >> 4) * 4 + r, p = w * 16 + (lane & 15);
-          const size_t og = ((size_t)b * d + j) * HW + (y0 + p / TW) * W + x0 + p % TW;
-          if (h && j < d) h[og] = acc[jb][r];
+          const int og = j * HW + (y0 + p / TW) * W + x0 + p % TW;
+          if (h_b && j < d) h_b[og] = acc[jb][r];
           const float v = as[j * PL + p] + dl[jb][r];
           as[j * PL + p] = v;   // a tile no longer needed: holds a' now
-          if (ap && j < d) ap[og] = v;
+          if (ap_b && j < d) ap_b[og] = v;
         }
     }
     if (pool) {
@@ -359,9 +363,9 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
         float m = v[0];
         for (int s4 = 1; s4 < 4; ++s4)
           if (v[s4] > m || (v[s4] != v[s4] && m == m)) { m = v[s4]; am = s4; }
-        const size_t o = ((size_t)b * d + c) * H2 * W2 + (y0 / 2 + cy) * W2 + x0 / 2 + cx;
-        pooled[o] = m;
-        amax[o] = (uint8_t)am;
+        const int o = c * H2 * W2 + (y0 / 2 + cy) * W2 + x0 / 2 + cx;
+        pooled[(size_t)b * d * H2 * W2 + o] = m;
+        amax[(size_t)b * d * H2 * W2 + o] = (uint8_t)am;
       }
     }
   }
@@ -559,6 +563,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
   const int b = blockIdx.y;
   const int TW = W < 32 ? W : 32, RPT = P / TW;
   const int HW = H * W, xt = W / TW, H2 = H / 2, W2 = W / 2;
+  // per-sample bases (uniform, 64-bit) + 32-bit per-lane offsets: saddr + voffset addressing
+  // instead of a 64-bit multiply-add per element (the host keeps d * H * W < 2^31)
+  const float* __restrict__ a_b = a + (size_t)b * d * HW;
+  const float* __restrict__ den_b = has_den ? den + (size_t)b * d * HW : a_b;
+  const float* __restrict__ gp_b = gp + (size_t)b * d * (sparse ? H2 * W2 : HW);
+  const uint8_t* __restrict__ am_b = sparse ? amax + (size_t)b * d * H2 * W2 : nullptr;
   const int dk = d / K, d4 = (d + 3) & ~3;
   // fanout 1: K+1 clones (standard + K subspaces); 2: the K subspace clones only; 0: replicated rows
   const int nq = fanout == 1 ? (K + 1) : fanout == 2 ? K : 1;
@@ -572,7 +582,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
     const int y0 = (tile / xt) * RPT, x0 = (tile % xt) * TW;
     const int pl = w * 16 + pc;
     const int py = y0 + pl / TW, px = x0 + pl % TW;
-    const size_t pixl = (size_t)py * W + px;
+    const int pixl = py * W + px;
+    const int cell = (py >> 1) * W2 + (px >> 1);
     // a (and den) at rows c = i*16 + 4 rg + r: the output layout of every GEMM below
     float av[NB * 4], dv[PF ? NB * 4 : 1];
 #pragma unroll
@@ -581,10 +592,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
       for (int r = 0; r < 4; ++r) {
         const int c = i * 16 + rg * 4 + r;
         const bool ok = c < d;
-        const size_t os = ((size_t)b * d + (ok ? c : 0)) * HW + pixl;
-        const float aa = a[os];
+        const int os = (ok ? c : 0) * HW + pixl;
+        const float aa = a_b[os];
         av[i * 4 + r] = ok ? aa : 0.f;
-        if constexpr (PF) dv[i * 4 + r] = has_den ? den[os] : 1.f;
+        if constexpr (PF) dv[i * 4 + r] = has_den ? den_b[os] : 1.f;
       }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -634,11 +645,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
           const int cc = ok ? c : 0;
           float R;
           if (sparse) {
-            const size_t q = ((size_t)b * d + cc) * H2 * W2 + (py >> 1) * W2 + (px >> 1);
-            const float gv = gp[q];   // unconditional load, then the argmax select
-            R = (amax[q] == (((py & 1) << 1) | (px & 1))) ? gv : 0.f;
+            const int q = cc * H2 * W2 + cell;
+            const float gv = gp_b[q];   // unconditional load, then the argmax select
+            R = (am_b[q] == (((py & 1) << 1) | (px & 1))) ? gv : 0.f;
           } else {
-            R = gp[((size_t)b * d + cc) * HW + pixl];
+            R = gp_b[cc * HW + pixl];
           }
           const float apv = av[cb * 4 + r] + acc[cb][r];
           const float v = R / stab(apv, eps_proj);
@@ -675,6 +686,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
       const int q = fanout == 1 ? qi : fanout == 2 ? qi + 1 : b % (K + 1);
       const int j0 = q == 0 ? 0 : (q - 1) * dk, j1 = q == 0 ? d : q * dk;
       const size_t orow = fanout ? (size_t)b * nq + qi : (size_t)b;
+      float* __restrict__ G_q = G + orow * d * HW;
       f32x4 acc[NB];
 #pragma unroll
       for (int cb = 0; cb < NB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -691,11 +703,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
         for (int r = 0; r < 4; ++r) {
           const int c = cb * 16 + rg * 4 + r;
           const bool cok = c < d;
-          const size_t os = ((size_t)b * d + (cok ? c : 0)) * HW + pixl;
+          const int os = (cok ? c : 0) * HW + pixl;
           const float ax = av[cb * 4 + r];
           float dx = 1.f;
           if constexpr (PF) dx = dv[cb * 4 + r];
-          else if (has_den) dx = den[os];
+          else if (has_den) dx = den_b[os];
           const float Rv = ax * acc[cb][r];
           float gq;
           if (has_den) {
@@ -705,9 +717,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
             gq = (ax > 0.f) ? Rv : 0.f;
           }
 #if DRSA_PROJ_DBG & 1
-          if (cok && gq == 12345.f) G[(orow * d + c) * HW + pixl] = gq;   // ablation: no G stores
+          if (cok && gq == 12345.f) G_q[c * HW + pixl] = gq;   // ablation: no G stores
 #else
-          if (cok) G[(orow * d + c) * HW + pixl] = gq;
+          if (cok) G_q[c * HW + pixl] = gq;
 #endif
         }
     }
@@ -745,6 +757,7 @@ __global__ __launch_bounds__(256) void first_layer_bwd_kernel(const float* __res
   const int bq = blockIdx.y;
   const int ly = tid / 16, lx = (tid % 16) * 4;   // 16 rows x 16 threads, 4 px each
   const size_t plane = (size_t)H * W;
+  const int iplane = H * W;   // 32-bit per-lane offsets from the per-sample base (C * H * W < 2^31)
   const float* gb = g + (size_t)bq * C * plane;
   float4 rv[FL_IV];
   float rh[FL_IH];
@@ -759,14 +772,14 @@ __global__ __launch_bounds__(256) void first_layer_bwd_kernel(const float* __res
       const bool rok = i < FL_NV4 && c < C && gy >= 0 && gy < H;
       if constexpr (VEC) {
         const bool ok = rok && gx < W;
-        const float4 v = *reinterpret_cast<const float4*>(gb + (ok ? c * plane + (size_t)gy * W + gx : 0));
+        const float4 v = *reinterpret_cast<const float4*>(gb + (ok ? c * iplane + gy * W + gx : 0));
         rv[it] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
       } else {
         float e[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const bool ok = rok && gx + k < W;
-          const float v = gb[ok ? c * plane + (size_t)gy * W + gx + k : 0];
+          const float v = gb[ok ? c * iplane + gy * W + gx + k : 0];
           e[k] = ok ? v : 0.f;
         }
         rv[it] = make_float4(e[0], e[1], e[2], e[3]);
@@ -779,7 +792,7 @@ __global__ __launch_bounds__(256) void first_layer_bwd_kernel(const float* __res
       const int ci = row / FL_HY, hy = row % FL_HY;
       const int gy = ty0 - 1 + hy, gx = side ? tx0 + FL_TW : tx0 - 1, c = c0 + ci;
       const bool ok = i < FL_ROWS * 2 && c < C && gy >= 0 && gy < H && gx >= 0 && gx < W;
-      const float v = gb[ok ? c * plane + (size_t)gy * W + gx : 0];
+      const float v = gb[ok ? c * iplane + gy * W + gx : 0];
       rh[it] = ok ? v : 0.f;
     }
   };
@@ -898,6 +911,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRSA_FQ_WPE
   const int bq = blockIdx.y, bs = bq / clones;
   const int ty = tid / (FQ_X / 2), tx = tid % (FQ_X / 2);      // 8 x 32 threads, 2x2 cells each
   const size_t plane = (size_t)H2 * W2;
+  const int iplane = H2 * W2;
   const float* gb = g + (size_t)bq * C * plane;
   const uint8_t* ab = amax + (size_t)bs * C * plane;
   // staging map: interior columns rx = 1 + lane, rows ry = wave + 4k; the two halo columns
@@ -916,14 +930,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRSA_FQ_WPE
       for (int k = 0; k < FQ_KR; ++k) {
         const int ry = wv4 + 4 * k, cy = qy0 - 1 + ry, c = c0 + ci;
         const bool ok = ry < FQ_RY && c < C && cy >= 0 && cy < H2 && cx < W2;
-        const size_t o = ok ? c * plane + (size_t)cy * W2 + cx : 0;
+        const int o = ok ? c * iplane + cy * W2 + cx : 0;   // 32-bit offsets: saddr + voffset loads
         v[ci * FQ_KR + k] = gb[o];
         sb[ci * FQ_KR + k] = (int)ab[o];
       }
     {
       const int c = c0 + hci, cy = qy0 - 1 + hry, cxh = qx0 - 1 + hrx;
       const bool ok = hact && c < C && cy >= 0 && cy < H2 && cxh >= 0 && cxh < W2;
-      const size_t o = ok ? c * plane + (size_t)cy * W2 + cxh : 0;
+      const int o = ok ? c * iplane + cy * W2 + cxh : 0;
       v[FQ_NS - 1] = gb[o];
       sb[FQ_NS - 1] = (int)ab[o];
     }
@@ -1560,6 +1574,7 @@ int drsa_amd_projection_fwd(const float* a, const float* U, const float* P, floa
   DRSA_REQUIRE((W == 8 || W == 16 || W % 32 == 0) && H % (64 / TW) == 0,
                "projection_fwd: W must be 8, 16 or a multiple of 32 and H a multiple of 64/min(W,32) (got %dx%d)", H, W);
   DRSA_REQUIRE(!pool || (pooled && amax), "projection_fwd: pool needs outputs");
+  DRSA_REQUIRE((int64_t)D * H * W < ((int64_t)1 << 31), "projection_fwd: one sample's d x H x W must stay below 2^31");
   DRSA_REQUIRE(pool || ap, "projection_fwd: without pool a' (ap) is the output");
   hipStream_t s = (hipStream_t)stream;
   const int tiles = (H / (64 / TW)) * (W / TW);
@@ -1592,6 +1607,7 @@ int drsa_amd_projection_bwd(const float* gp, const uint8_t* amax, const float* a
                             int K, float eps_proj, float eps_den, int fanout, void* stream) {
   const int TW = W < 32 ? W : 32;
   DRSA_REQUIRE(fanout >= 0 && fanout <= 2, "projection_bwd: fanout must be 0, 1 or 2");
+  DRSA_REQUIRE((int64_t)D * H * W < ((int64_t)1 << 31), "projection_bwd: one sample's d x H x W must stay below 2^31");
   DRSA_REQUIRE(gp && a && U && G && ((ap && h) || P),
                "projection_bwd: gp, a, U, G and P (when h / a' are recomputed) are required");
   DRSA_REQUIRE((W == 8 || W == 16 || W % 32 == 0) && H % (64 / TW) == 0,
@@ -1647,6 +1663,7 @@ int drsa_amd_projection_bwd(const float* gp, const uint8_t* amax, const float* a
 int drsa_amd_first_layer_bwd(const float* g, const uint8_t* amax, const float* w2f, float* out, int Bq, int clones,
                              int C, int H, int W, void* stream) {
   DRSA_REQUIRE(Bq > 0 && clones > 0 && Bq % clones == 0, "first_layer_bwd: bad batch");
+  DRSA_REQUIRE((int64_t)C * H * W < ((int64_t)1 << 31), "first_layer_bwd: one sample's C x H x W must stay below 2^31");
   if (amax) {
     DRSA_REQUIRE(H % 2 == 0 && W % 4 == 0, "first_layer_bwd: pooled path needs even H and W % 4 == 0");
     const int H2 = H / 2, W2 = W / 2;
