@@ -328,7 +328,7 @@ def drsa_joint_bench(device, steps=200):
             "objective_final": [float(t[-1]) for _, t in out]}
 
 
-def vggish_lrp_bench(device, B=32, iters=5):
+def vggish_lrp_bench(device, B=32, iters=10):
     """C5 model: VGGish-BN, 128x256 log-mel.  Standard LRP (compute_relevances), the engine forward
     alone, and the C5 CNN leg (DRSA data capture at j = 26: forward + relevance backward to the
     layer), each on the fp32 plan, on the bf16 plan (model.bfloat16(): conv forwards on

@@ -434,25 +434,30 @@ struct StagerBF {
 
   __device__ __forceinline__ void load(const ConvArgs& a, int c0, int tid, int ty0, int tx0, int bq, int bs) {
     const int H = a.H, W = a.W;
-    const size_t HW = (size_t)H * W;
+    const unsigned HW = (unsigned)(H * W);
+    // per-sample bases (uniform) + 32-bit per-lane offsets (saddr + voffset loads)
+    const int H2s = H >> 1, W2s = W / (P4 ? 4 : Cfg::PW_);
+    const float* __restrict__ inb =
+        a.in + (size_t)bq * a.cin * (Cfg::AMODE_ == A_POOLSPARSE || P4 ? (size_t)H2s * W2s : (size_t)HW);
+    const uint8_t* __restrict__ amb = (Cfg::AMODE_ == A_POOLSPARSE || P4) ? a.in_amax + (size_t)bs * a.cin * H2s * W2s
+                                                                          : nullptr;
     if constexpr (P4) {
       const int H2 = H >> 1, W2 = W >> 2;
-      const size_t HW2 = (size_t)H2 * W2;
+      const unsigned HW2 = (unsigned)(H2 * W2);
 #pragma unroll
       for (int it = 0; it < IT4; ++it) {
         const int i = tid + it * NT_;
         const int cs = i % NCR, r = i / NCR, hy = r % HY, half = r / HY;
         const int gy = ty0 - 1 + hy, cx = (tx0 >> 2) - 1 + cs, cb = c0 + 8 * half;
         const bool ok = i < NITEM4 && gy >= 0 && gy < H && cx >= 0 && cx < W2;
-        const size_t cell = ok ? (size_t)(gy >> 1) * W2 + cx : 0;
-        const size_t base = ok ? ((size_t)bq * a.cin + cb) * HW2 + cell : 0;
-        const size_t abase = ok ? ((size_t)bs * a.cin + cb) * HW2 + cell : 0;
+        const unsigned cell = ok ? (unsigned)((gy >> 1) * W2 + cx) : 0u;
+        const unsigned base = ok ? (unsigned)cb * HW2 + cell : 0u;
         uint32_t ab[2] = {0u, 0u};
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const bool okc = ok && cb + j < a.cin;
-          const float v = a.in[okc ? base + j * HW2 : 0];
-          const uint32_t am = a.in_amax[okc ? abase + j * HW2 : 0];
+          const float v = inb[okc ? base + j * HW2 : 0u];
+          const uint32_t am = amb[okc ? base + j * HW2 : 0u];
           st_f[it][j] = okc ? v : 0.f;
           ab[j >> 2] |= (okc ? am : 0xffu) << (8 * (j & 3));   // 0xff matches no pixel
         }
@@ -465,22 +470,21 @@ struct StagerBF {
       // argmax (row-major window position) is this pixel, else 0
       constexpr int PWB = Cfg::PW_;
       const int H2 = H >> 1, W2 = W / PWB;
-      const size_t HW2 = (size_t)H2 * W2;
+      const unsigned HW2 = (unsigned)(H2 * W2);
 #pragma unroll
       for (int it = 0; it < IT; ++it) {
         const int i = tid + it * NT_;
         const int hx = i % HX, r = i / HX, hy = r % HY, half = r / HY;
         const int gy = ty0 - 1 + hy, gx = tx0 - 1 + hx, cb = c0 + 8 * half;
         const bool ok = i < NITEM && gy >= 0 && gy < H && gx >= 0 && gx < W;
-        const size_t cell = ok ? (size_t)(gy >> 1) * W2 + (gx / PWB) : 0;
-        const size_t base = ok ? ((size_t)bq * a.cin + cb) * HW2 + cell : 0;
-        const size_t abase = ok ? ((size_t)bs * a.cin + cb) * HW2 + cell : 0;
+        const unsigned cell = ok ? (unsigned)((gy >> 1) * W2 + (gx / PWB)) : 0u;
+        const unsigned base = ok ? (unsigned)cb * HW2 + cell : 0u;
         const uint32_t sub = (uint32_t)((gy & 1) * PWB + (gx % PWB));
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const bool okc = ok && cb + j < a.cin;
-          const float v = a.in[okc ? base + j * HW2 : 0];
-          const uint32_t am = a.in_amax[okc ? abase + j * HW2 : 0];
+          const float v = inb[okc ? base + j * HW2 : 0u];
+          const uint32_t am = amb[okc ? base + j * HW2 : 0u];
           st_f[it][j] = (okc && am == sub) ? v : 0.f;
         }
       }
@@ -491,11 +495,11 @@ struct StagerBF {
         const int hx = i % HX, r = i / HX, hy = r % HY, half = r / HY;
         const int gy = ty0 - 1 + hy, gx = tx0 - 1 + hx, cb = c0 + 8 * half;
         const bool ok = i < NITEM && gy >= 0 && gy < H && gx >= 0 && gx < W;
-        const size_t base = ok ? ((size_t)bq * a.cin + cb) * HW + (size_t)gy * W + gx : 0;
+        const unsigned base = ok ? (unsigned)cb * HW + (unsigned)(gy * W + gx) : 0u;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const bool okc = ok && cb + j < a.cin;
-          const float v = a.in[okc ? base + j * HW : 0];
+          const float v = inb[okc ? base + j * HW : 0u];
           st_f[it][j] = okc ? v : 0.f;
         }
       }
@@ -889,7 +893,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
             }
             am_keep[it] = am;
             if (co < a.cout && qy < H2 && qx < W2) {
-              const size_t o = (((size_t)bq * a.cout + co) * H2 + qy) * W2 + qx;
+              const size_t o = (size_t)bq * a.cout * H2 * W2 + (unsigned)((co * H2 + qy) * W2 + qx);
               a.out[o] = m;
               a.out_amax[o] = (uint8_t)am;
             }
@@ -921,7 +925,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
                 if (yy[s4] > m || (yy[s4] != yy[s4] && m == m)) { m = yy[s4]; am = s4; }
               am_keep[it] = am;
               if (co < a.cout && qy < H2 && qx < W2) {
-                const size_t o = (((size_t)bq * a.cout + co) * H2 + qy) * W2 + qx;
+                const size_t o = (size_t)bq * a.cout * H2 * W2 + (unsigned)((co * H2 + qy) * W2 + qx);
                 a.out[o] = m;
                 a.out_amax[o] = (uint8_t)am;
               }
@@ -938,7 +942,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
             const int co = gch(cl, v);
             if (co < a.cout && ty0 + py < H && tx0 + px < W) {
               const float4 val = *reinterpret_cast<const float4*>(T + (cl * TH + py) * TWP + px);
-              *reinterpret_cast<float4*>(a.out + (((size_t)bq * a.cout + co) * H + ty0 + py) * W + tx0 + px) = val;
+              *reinterpret_cast<float4*>(a.out + (size_t)bq * a.cout * H * W + (unsigned)((co * H + ty0 + py) * W + tx0 + px)) = val;
             }
           }
         }
@@ -952,8 +956,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
               const int co = gch(cl, v);
               const int am = am_keep[it];
               if (co < a.cout && qy < H2 && qx < W2)
-                a.out_den[(((size_t)bq * a.cout + co) * H2 + qy) * W2 + qx] =
-                    a.den_map[((size_t)co * H + 2 * qy + am / PWc) * W + PWc * qx + am % PWc];
+                a.out_den[(size_t)bq * a.cout * H2 * W2 + (unsigned)((co * H2 + qy) * W2 + qx)] =
+                    a.den_map[(unsigned)((co * H + 2 * qy + am / PWc) * W + PWc * qx + am % PWc)];
             });
           };
           if constexpr (PW == 4) {
@@ -970,8 +974,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
                 const int qy = (ty0 >> 1) + cy, qx = (tx0 >> 1) + cx;
                 const int am = am_keep[it];
                 if (co < a.cout && qy < H2 && qx < W2)
-                  a.out_den[(((size_t)bq * a.cout + co) * H2 + qy) * W2 + qx] =
-                      a.den_map[((size_t)co * H + 2 * qy + (am >> 1)) * W + 2 * qx + (am & 1)];
+                  a.out_den[(size_t)bq * a.cout * H2 * W2 + (unsigned)((co * H2 + qy) * W2 + qx)] =
+                      a.den_map[(unsigned)((co * H + 2 * qy + (am >> 1)) * W + 2 * qx + (am & 1))];
               }
             }
           }
@@ -984,8 +988,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
               const int py = rem / (TW / 4), px = (rem % (TW / 4)) * 4;
               const int co = gch(cl, v);
               if (co < a.cout && ty0 + py < H && tx0 + px < W)
-                *reinterpret_cast<float4*>(a.out_den + (((size_t)bq * a.cout + co) * H + ty0 + py) * W + tx0 + px) =
-                    *reinterpret_cast<const float4*>(a.den_map + ((size_t)co * H + ty0 + py) * W + tx0 + px);
+                *reinterpret_cast<float4*>(a.out_den + (size_t)bq * a.cout * H * W + (unsigned)((co * H + ty0 + py) * W + tx0 + px)) =
+                    *reinterpret_cast<const float4*>(a.den_map + (unsigned)((co * H + ty0 + py) * W + tx0 + px));
             }
           }
         }
@@ -1008,7 +1012,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
               const int co = gch(cl, v);
               const int am = am_keep[it];
               if (co < a.cout && qy < H2 && qx < W2)
-                a.out_den[(((size_t)bq * a.cout + co) * H2 + qy) * W2 + qx] =
+                a.out_den[(size_t)bq * a.cout * H2 * W2 + (unsigned)((co * H2 + qy) * W2 + qx)] =
                     T[(cl * TH + 2 * cy + am / PWc) * TWP + PWc * cx + am % PWc];
             });
           };
@@ -1026,7 +1030,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
                 const int qy = (ty0 >> 1) + cy, qx = (tx0 >> 1) + cx;
                 const int am = am_keep[it];
                 if (co < a.cout && qy < H2 && qx < W2)
-                  a.out_den[(((size_t)bq * a.cout + co) * H2 + qy) * W2 + qx] =
+                  a.out_den[(size_t)bq * a.cout * H2 * W2 + (unsigned)((co * H2 + qy) * W2 + qx)] =
                       T[(cl * TH + 2 * cy + (am >> 1)) * TWP + 2 * cx + (am & 1)];
               }
             }
@@ -1041,7 +1045,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
               const int co = gch(cl, v);
               if (co < a.cout && ty0 + py < H && tx0 + px < W) {
                 const float4 val = *reinterpret_cast<const float4*>(T + (cl * TH + py) * TWP + px);
-                *reinterpret_cast<float4*>(a.out_den + (((size_t)bq * a.cout + co) * H + ty0 + py) * W + tx0 + px) = val;
+                *reinterpret_cast<float4*>(a.out_den + (size_t)bq * a.cout * H * W + (unsigned)((co * H + ty0 + py) * W + tx0 + px)) = val;
               }
             }
           }
