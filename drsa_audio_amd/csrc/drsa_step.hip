@@ -182,12 +182,18 @@ __device__ __forceinline__ void partial_core(const void* __restrict__ A_, const 
   auto load_tile = [&](int t) {
     const int64_t r0 = (rb0 + (int64_t)t * (RT / 16)) * 16;
     const int64_t rmax = rb1 * 16 < N ? rb1 * 16 : N;
+    // the tile's first row as a uniform base, the lane's element as a 32-bit offset from it
+    // (saddr + voffset loads); a masked lane reads the base itself
+    const float* A = reinterpret_cast<const float*>(A_) + r0 * d;
+    const float* C = reinterpret_cast<const float*>(C_) + r0 * d;
+    const uint16_t* Ab = reinterpret_cast<const uint16_t*>(A_) + r0 * d;
+    const uint16_t* Cb = reinterpret_cast<const uint16_t*>(C_) + r0 * d;
 #pragma unroll
     for (int p = 0; p < PFN; ++p) {
       const int i = tid + p * NT;
       const int row = (i / (DP / 4)) % RT, col = 4 * (i % (DP / 4));
       const bool ok = i < NV && r0 + row < rmax && col < d;
-      const size_t off = ok ? (size_t)(r0 + row) * d + col : 0;
+      const unsigned off = ok ? (unsigned)(row * d + col) : 0u;
       float4 a, c;
       if constexpr (BF) {   // 4 x 16-bit -> 4 fp32 (exact)
         if constexpr (VEC) {
@@ -201,7 +207,7 @@ __device__ __forceinline__ void partial_core(const void* __restrict__ A_, const 
           float va[4], vc[4];
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            const size_t o = (ok && col + u < d) ? off + u : 0;
+            const unsigned o = (ok && col + u < d) ? off + u : 0u;
             const uint32_t xa = Ab[o], xc = Cb[o];
             va[u] = keep_or_zero(wid16<DT>(xa), col + u < d);
             vc[u] = keep_or_zero(wid16<DT>(xc), col + u < d);
@@ -217,7 +223,7 @@ __device__ __forceinline__ void partial_core(const void* __restrict__ A_, const 
           float va[4], vc[4];
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            const size_t o = (ok && col + u < d) ? off + u : 0;
+            const unsigned o = (ok && col + u < d) ? off + u : 0u;
             const float xa = A[o], xc = C[o];
             va[u] = keep_or_zero(xa, col + u < d);
             vc[u] = keep_or_zero(xc, col + u < d);
