@@ -36,7 +36,10 @@ const Entry* find(int cin_p, int cout_p, int W, int ng, int amode, int epi, int 
   // 8x8 tiles at 8 < W < 32 (bits: 1 forward, 2 backward; measured faster than 8x16 at 16x16: conv_fwd
   // features.9 0.287 -> 0.266 ms, conv_bwd 0.218 -> 0.214 at B = 512); DRSA_AMD_CONV_W16_TILE8=0 restores 8x16
   static const int w16_as8 = env_int("DRSA_AMD_CONV_W16_TILE8", 3);
+  // forward into 64 channels at W = 32 with 8 x 16 tiles (half the accumulators: 2 waves/SIMD instead of 1)
+  static const int fwd64_t16 = env_int("DRSA_AMD_CONV_FWD64_T16", 1);
   if (W >= 32) { tw = 32; mw = 8; th = (th16 && cout_p == 32 && ng <= 2) ? 16 : 8; }
+  if (W == 32 && fwd64_t16 && epi != EPI_BWD && cout_p == 64) { tw = 16; mw = 8; th = 8; }
   else if (W > 8 && !(w16_as8 & (epi == EPI_BWD ? 2 : 1))) { tw = 16; mw = 8; }
   else { tw = 8; mw = 4; }
   for (const drsa_conv::Table* t : kTables)
