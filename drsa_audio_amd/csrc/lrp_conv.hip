@@ -40,6 +40,9 @@ const Entry* find(int cin_p, int cout_p, int W, int ng, int amode, int epi, int 
   static const int fwd64_t16 = env_int("DRSA_AMD_CONV_FWD64_T16", 1);
   if (W >= 32) { tw = 32; mw = 8; th = (th16 && cout_p == 32 && ng <= 2) ? 16 : 8; }
   if (W == 32 && fwd64_t16 && epi != EPI_BWD && cout_p == 64) { tw = 16; mw = 8; th = 8; }
+  // the same at every width >= 32 for the fp32 forward (VGGish features.3: 1.50 -> 1.33 ms)
+  static const int fwd64_t16w = env_int("DRSA_AMD_CONV_FWD64_T16_WIDE", 1);
+  if (W > 32 && fwd64_t16w && epi != EPI_BWD && cout_p == 64 && et == 0) { tw = 16; mw = 8; th = 8; }
   else if (W > 8 && !(w16_as8 & (epi == EPI_BWD ? 2 : 1))) { tw = 16; mw = 8; }
   else { tw = 8; mw = 4; }
   for (const drsa_conv::Table* t : kTables)
