@@ -579,6 +579,10 @@ def main():
                           standard="sum")
     x = synthetic_logmel(B, seed=1 + rank, device=device)
 
+    props = torch.cuda.get_device_properties(device)
+    dev_info = {"name": props.name, "cus": props.multi_processor_count,
+                "gcn_arch": getattr(props, "gcnArchName", ""), "clock_khz": getattr(props, "clock_rate", None)}
+    log(f"[bench] device {dev_info}")
     log(f"[bench] rank {rank}/{world}: headline B={B}, {args.warmup} warm-up + {args.steps} timed steps")
     for _ in range(args.warmup):
         hg.generate_subspace_heatmaps(x, to_host=False)

@@ -36,13 +36,15 @@ const Entry* find(int cin_p, int cout_p, int W, int ng, int amode, int epi, int 
   // 8x8 tiles at 8 < W < 32 (bits: 1 forward, 2 backward; measured faster than 8x16 at 16x16: conv_fwd
   // features.9 0.287 -> 0.266 ms, conv_bwd 0.218 -> 0.214 at B = 512); DRSA_AMD_CONV_W16_TILE8=0 restores 8x16
   static const int w16_as8 = env_int("DRSA_AMD_CONV_W16_TILE8", 3);
-  // forward into 64 channels at W = 32 with 8 x 16 tiles (half the accumulators: 2 waves/SIMD instead of 1)
+  // forward into 64 channels at W >= 32 with 8 x 16 tiles (half the accumulators: 2 waves/SIMD
+  // instead of 1; GTZAN conv_fwd:features.6 0.391 -> 0.356 ms, VGGish features.3 fp32 1.43 -> 1.36 ms)
   static const int fwd64_t16 = env_int("DRSA_AMD_CONV_FWD64_T16", 1);
-  if (W >= 32) { tw = 32; mw = 8; th = (th16 && cout_p == 32 && ng <= 2) ? 16 : 8; }
-  if (W == 32 && fwd64_t16 && epi != EPI_BWD && cout_p == 64) { tw = 16; mw = 8; th = 8; }
-  // the same at every width >= 32 for the fp32 forward (VGGish features.3: 1.50 -> 1.33 ms)
-  static const int fwd64_t16w = env_int("DRSA_AMD_CONV_FWD64_T16_WIDE", 1);
-  if (W > 32 && fwd64_t16w && epi != EPI_BWD && cout_p == 64 && et == 0) { tw = 16; mw = 8; th = 8; }
+  // (measured slower, off) 32-channel fp32 forwards on 8 x 16 tiles (123 VGPRs: 4 waves/SIMD instead
+  // of 3): conv_fwd:features.3 0.632 -> 0.659 ms
+  static const int fwd32_t16 = env_int("DRSA_AMD_CONV_FWD32_T16", 0);
+  const bool fwd_t16 = epi != EPI_BWD && et == 0 && ((fwd64_t16 && cout_p == 64) || (fwd32_t16 && cout_p == 32 && !th16));
+  if (W >= 32 && fwd_t16) { tw = 16; mw = 8; th = 8; }
+  else if (W >= 32) { tw = 32; mw = 8; th = (th16 && cout_p == 32 && ng <= 2) ? 16 : 8; }
   else if (W > 8 && !(w16_as8 & (epi == EPI_BWD ? 2 : 1))) { tw = 16; mw = 8; }
   else { tw = 8; mw = 4; }
   for (const drsa_conv::Table* t : kTables)
