@@ -2,10 +2,14 @@
 // build compiles them in parallel.
 #include "lrp_conv_kernel.h"
 
+#ifndef DRSA_CONV_CIC_FWD64_128
+#define DRSA_CONV_CIC_FWD64_128 8
+#endif
+
 namespace drsa_conv {
 static const Entry kTableFwdC_e[] = {
     FWD_SET(64, 64, 8),
-    FWD_SET(64, 128, 8),
+    FWD_SET(64, 128, DRSA_CONV_CIC_FWD64_128),
 };
 extern const Table kTableFwdC = {kTableFwdC_e, (int)(sizeof(kTableFwdC_e) / sizeof(kTableFwdC_e[0]))};
 }  // namespace drsa_conv
