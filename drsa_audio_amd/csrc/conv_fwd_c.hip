@@ -3,7 +3,7 @@
 #include "lrp_conv_kernel.h"
 
 #ifndef DRSA_CONV_CIC_FWD64_128
-#define DRSA_CONV_CIC_FWD64_128 8
+#define DRSA_CONV_CIC_FWD64_128 4   // 8 x 8 tiles at 3 waves/SIMD (166 VGPRs)
 #endif
 
 namespace drsa_conv {

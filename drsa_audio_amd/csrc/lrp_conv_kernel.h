@@ -46,6 +46,9 @@
 #ifndef DRSA_CONV_BF_WPE
 #define DRSA_CONV_BF_WPE 2
 #endif
+#ifndef DRSA_CONV_FWD_WPE_128
+#define DRSA_CONV_FWD_WPE_128 3    // 8 x 8-tile forwards into 128 channels with 4-channel chunks: 2 -> 3 waves/SIMD
+#endif
 #ifndef DRSA_CONV_FWD_WPE_WIDE
 #define DRSA_CONV_FWD_WPE_WIDE 3   // forwards into 64 channels (CIC <= 8, NG <= 2): 1 -> 3 conv_fwd:features.6 0.361 -> 0.343 ms
 #endif
@@ -138,7 +141,8 @@ struct ConvCfg {
   static constexpr int WPE = BF ? (COUT <= 64 ? DRSA_CONV_BF_WPE : 1)
                              : (EPI == EPI_BWD && NG == 1) ? (SMALL_BWD ? 4 : DRSA_CONV_BWD_WPE)
                              : (EPI != EPI_BWD && CIC <= 8 && COUT <= 32 && NG <= 2 ? DRSA_CONV_FWD_WPE
-                                : EPI != EPI_BWD && CIC <= 8 && NG <= 2 && COUT == 64 ? DRSA_CONV_FWD_WPE_WIDE : 1);
+                                : EPI != EPI_BWD && CIC <= 8 && NG <= 2 && COUT == 64 ? DRSA_CONV_FWD_WPE_WIDE
+                                : EPI != EPI_BWD && CIC <= 4 && NG <= 2 && COUT == 128 && TW == 8 ? DRSA_CONV_FWD_WPE_128 : 1);
   // operand prefetch distance of the MFMA loop (k-steps)
   static constexpr int PD = DRSA_CONV_PD_BWD > 0 && EPI >= EPI_BWD ? DRSA_CONV_PD_BWD : 1;
   static_assert(TH % MTH == 0 && TW % MTW == 0, "tile must be a multiple of the M-tile");
