@@ -46,7 +46,9 @@ const Entry* find(int cin_p, int cout_p, int W, int ng, int amode, int epi, int 
   // fp32 backward into 64 channels at W >= 32 (VGGish) on 8 x 16 tiles: the 8 x 32 tile with 16-channel
   // chunks spills 91-115 VGPRs at 3 waves/SIMD, the 8 x 16 one none
   static const int bwd64_t16 = env_int("DRSA_AMD_CONV_BWD64_T16", 1);
-  const bool bwd_t16 = epi == EPI_BWD && et == 0 && bwd64_t16 && cout_p == 64 && cin_p <= 128;
+  static const int bwd32_t16 = env_int("DRSA_AMD_CONV_BWD32_T16", 0);   // (experiment) the same into 32 channels
+  const bool bwd_t16 = epi == EPI_BWD && et == 0 &&
+                       ((bwd64_t16 && cout_p == 64 && cin_p <= 128) || (bwd32_t16 && cout_p == 32 && !th16));
   if (W >= 32 && (fwd_t16 || bwd_t16)) { tw = 16; mw = 8; th = 8; }
   else if (W >= 32) { tw = 32; mw = 8; th = (th16 && cout_p == 32 && ng <= 2) ? 16 : 8; }
   else if (W > 8 && !(w16_as8 & (epi == EPI_BWD ? 2 : 1))) { tw = 16; mw = 8; }
