@@ -3,7 +3,7 @@
 #include "lrp_conv_kernel.h"
 
 #ifndef DRSA_CONV_CIC_FWD64_64
-#define DRSA_CONV_CIC_FWD64_64 8
+#define DRSA_CONV_CIC_FWD64_64 4   // 8 x 8 tiles: 116 VGPRs, 4 waves/SIMD (conv_fwd:features.9 0.266 -> 0.257 ms)
 #endif
 #ifndef DRSA_CONV_CIC_FWD64_128
 #define DRSA_CONV_CIC_FWD64_128 4   // 8 x 8 tiles at 3 waves/SIMD (166 VGPRs)
