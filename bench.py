@@ -61,10 +61,14 @@ def load_u():
 
 
 # --------------------------------------------------------------------------- FLOP model
-def kernel_macs(eng, B, K, standard="sum"):
+def kernel_macs(eng, B, K, standard="sum", launched=None):
     """Algorithmic multiply-accumulates per launch of each kernel tag for one batch of B
     explained samples ('Algorithmic work').  standard="sum": K relevance clones below
-    the projection (the standard heatmap is their sum); "clone": K+1."""
+    the projection (the standard heatmap is their sum); "clone": K+1.
+
+    `launched` (the tags one traced step actually ran) restricts the table to those kernels: the
+    plan runs EITHER the fused conv_bwd_first:<layer 1> OR the pair conv_bwd:<layer 1> +
+    first_layer_bwd:<layer 0>, and a whole-path sum over both would count that work twice."""
     macs = {}
     rec = eng.last["stages"]
     clones_below = False
@@ -89,7 +93,16 @@ def kernel_macs(eng, B, K, standard="sum"):
         N, Kd = ds.W.shape
         macs[f"linear_fwd:{ds.name}"] = B * N * Kd
         macs[f"linear_bwd:{ds.name}"] = B * N * Kd
+    if launched is not None:
+        launched = set(launched)
+        macs = {k: v for k, v in macs.items() if k in launched}
     return macs
+
+
+def whole_path_macs(macs, per, steps):
+    """MACs of one traced step: each launched tag's per-launch MACs x its launches per step
+    (`per`: tag -> list of event times over `steps` traced steps, as collected below)."""
+    return sum(macs.get(tag, 0) * len(ts) for tag, ts in per.items()) / steps
 
 
 # --------------------------------------------------------------------------- CPU baseline
@@ -174,7 +187,7 @@ def cpu_drsa_baseline(reps=7):
     eigh orthogonalize; pinned bit-exact to the reference's own fixtures), median of `reps` steps."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import drsa_ref
-    from gen_fixtures import drsa_inputs
+    from drsa_audio_amd.utils.synthetic import drsa_inputs
     threads, aff, quota = _cpu_threads()
     log(f"[bench] CPU baseline (DRSA C3 step): {threads} threads")
     A, C = (torch.from_numpy(v) for v in drsa_inputs(20000, 64, 3))
@@ -186,8 +199,7 @@ def cpu_drsa_baseline(reps=7):
 
 # --------------------------------------------------------------------------- DRSA
 def drsa_bench(device, steps=200):
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    from gen_fixtures import drsa_inputs
+    from drsa_audio_amd.utils.synthetic import drsa_inputs
     from drsa_audio_amd import _capi
     from drsa_audio_amd.xai.drsa.drsa import DrsaWorkspace, drsa_run
     N, d, K = 20000, 64, 4
@@ -246,14 +258,10 @@ def frontend_bench(device, n_songs=64, iters=20):
     """R17 log-mel front end: n_songs synthetic 29.5 s songs x 8 chunks -> [512, 1, 128, 128] in one
     launch (get_slice + peak_normalizer + STFT + mel + log10 + clamp).  HBM roofline: the chunk's
     48 000 samples read once + the 128x128 log-mel written once = 257 KB per chunk."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import logmel_ref
     from drsa_audio_amd.utils.dataloading import Loader
-    songs = torch.from_numpy(logmel_ref.synthetic_songs(n_songs, seed=3)).to(device)
+    from drsa_audio_amd.utils.synthetic import synthetic_songs
+    songs = torch.from_numpy(synthetic_songs(n_songs, seed=3)).to(device)
     ld = Loader("gtzan", device=device)
-    out = ld.load_songs(songs)
-    ref = logmel_ref.load_songs(songs[:1].cpu().numpy(), "gtzan", mode="f64")
-    err = float(np.abs(out[:8].cpu().numpy() - ref).max())
     s = torch.cuda.current_stream(device)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(3):
@@ -271,14 +279,13 @@ def frontend_bench(device, n_songs=64, iters=20):
             "chunks_per_s": chunks / (ms * 1e-3), "ms_per_launch": ms, "algorithmic_bytes_per_launch": byts,
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": gbs / HBM_PEAK_GBS},
-            "max_abs_logmel_err_vs_f64_oracle_song0": err}
+            "parity": "tests/test_logmel_gpu.py (f64-anchored gates); not re-checked here"}
 
 
 def drsa_joint_bench(device, steps=200):
     """C5 DRSA: layers j=26 and j=33 of VGGish (d=128, K=16 each, 20000 rows each) optimised
     together in one hipGraph (drsa_amd_drsa_run_multi)."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    from gen_fixtures import drsa_inputs
+    from drsa_audio_amd.utils.synthetic import drsa_inputs
     from drsa_audio_amd.xai.drsa.drsa import drsa_run, drsa_run_joint
     N, d, K = 20000, 128, 16
     probs = []
@@ -380,7 +387,7 @@ def vggish_lrp_bench(device, B=32, iters=10):
             for tag, e0, e1 in eng.trace:
                 per.setdefault(tag, []).append(e0.elapsed_time(e1))
             eng.trace = None
-            macs = kernel_macs(eng, B, 0)
+            macs = kernel_macs(eng, B, 0, launched=per)
             top = max(per, key=lambda k: float(np.mean(per[k])))
             # the roofline line: the slowest MFMA conv kernel (the top kernel can be the VALU
             # first-layer backward, reported beside it)
@@ -408,8 +415,7 @@ def drsa_sharded_bench(device, world, rank, steps=100):
     """C4 row-sharded DRSA: 20000 rows per rank (weak; 160000 at 8 ranks), d=64, K=8; one RCCL
     all-reduce of the [d*d+K] partial per step (drsa_audio_amd/xai/drsa/distributed.py)."""
     import torch.distributed as dist
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    from gen_fixtures import drsa_inputs
+    from drsa_audio_amd.utils.synthetic import drsa_inputs
     from drsa_audio_amd.xai.drsa.distributed import sharded_run
     n, d, K = 20000, 64, 8
     A, C = drsa_inputs(n, d, 100 + rank)
@@ -623,7 +629,7 @@ def main():
         L = len(tags) // 3
         with open(args.tag_order, "w") as fh:
             json.dump({"tags": tags[:L], "main_steps": args.warmup + args.steps + 3, "batch": B}, fh)
-    macs = kernel_macs(eng, B, K, hg.standard)
+    macs = kernel_macs(eng, B, K, hg.standard, launched=per)
     kernels = {}
     for tag, ts in per.items():
         avg = float(np.mean(ts))
@@ -645,7 +651,7 @@ def main():
             traffic_src = f"profiles/pmc_traffic.json ({pm.get('profile', 'unlabelled')}), not measured in this run"
         except Exception:
             traffic = None
-    total_macs = sum(macs.values())
+    total_macs = whole_path_macs(macs, per, 3)
 
     log(f"[bench] headline {value:.0f} explained samples/s ({ms:.3f} ms/step); secondaries next")
     # ---- secondary: standard LRP (C2, bs=64) ----

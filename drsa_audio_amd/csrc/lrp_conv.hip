@@ -266,7 +266,10 @@ int drsa_amd_conv_bwd_den_ring(const float* g, const uint8_t* g_amax, const void
                                int cout, int H, int W, int ng, int xmode, float eps, void* stream) {
   DRSA_REQUIRE(Bq > 0 && clones > 0 && Bq % clones == 0, "conv_bwd_den_ring: bad batch/clones");
   DRSA_REQUIRE(x && den_ring && den_const4, "conv_bwd_den_ring: needs x, den_ring and den_const4");
-  DRSA_REQUIRE(H % 2 == 0 && W % 4 == 0, "conv_bwd_den_ring: H must be even and W %% 4 == 0 (got %dx%d)", H, W);
+  // the compact ring (2W + 8(H - 2) floats per channel at the pooled resolution) needs distinct
+  // first / last float4 groups per row and at least two rows: the forward's W % 16, H >= 4 unpooled
+  DRSA_REQUIRE(H >= 2 && W >= 8 && W % 8 == 0,
+               "conv_bwd_den_ring: needs pooled H >= 2 and W >= 8, W %% 8 == 0 (got %dx%d)", H, W);
   DRSA_REQUIRE(xmode == XM_NONE || xmode == XM_MUL || xmode == XM_SPLIT, "conv_bwd_den_ring: bad xmode");
   DRSA_REQUIRE(((uintptr_t)den_const4 & 15) == 0, "conv_bwd_den_ring: den_const4 must be 16-byte aligned");
   const int et = wts_bf16 ? 1 : 0;

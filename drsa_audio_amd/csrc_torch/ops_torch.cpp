@@ -13,9 +13,11 @@
 //                                           the zennit rule passes attribute.py:98-107 drives
 //   heatmap_sort                            explainer.py:99-123, 151-176
 #include <ATen/ATen.h>
+#include <ATen/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
+#include <initializer_list>
 #include <tuple>
 
 #include "drsa_amd.h"
@@ -36,6 +38,19 @@ void need(const Tensor& t, const char* name, at::ScalarType dt = at::kFloat) {
   TORCH_CHECK(t.is_contiguous(), "drsa_amd: ", name, " must be contiguous");
 }
 
+// Every op runs on the device of its first tensor argument (guard below: the current stream is
+// that device's) and refuses tensors on another device instead of queueing kernels that would
+// touch another GPU's memory.
+void same_device(const Tensor& ref, std::initializer_list<const Tensor*> ts) {
+  for (const Tensor* t : ts)
+    TORCH_CHECK(!t->defined() || t->numel() == 0 || t->device() == ref.device(),
+                "drsa_amd: all tensor arguments must be on ", ref.device(), ", got one on ", t->device());
+}
+void same_device(const Tensor& ref, const c10::optional<Tensor>& t) {
+  if (t.has_value()) same_device(ref, {&*t});
+}
+#define DRSA_GUARD(t) const at::OptionalDeviceGuard device_guard_(at::device_of(t))
+
 template <class T = float>
 const T* cptr(const c10::optional<Tensor>& t) { return t.has_value() ? t->data_ptr<T>() : nullptr; }
 
@@ -52,6 +67,7 @@ struct Ws {   // DRSA workspace (DrsaWorkspace in xai/drsa/drsa.py)
 
 void check_problem(const Tensor& A, const Tensor& C, const Tensor& U, int64_t K) {
   need(A, "activation_vecs"), need(C, "context_vecs"), need(U, "U");
+  same_device(A, {&C, &U});
   TORCH_CHECK(A.dim() == 2 && A.sizes() == C.sizes(), "drsa_amd: activation and context vectors must be [N, d]");
   const int64_t d = A.size(1);
   TORCH_CHECK(U.dim() == 2 && U.size(0) == d && U.size(1) == d, "drsa_amd: U must be [", d, ", ", d, "]");
@@ -59,6 +75,7 @@ void check_problem(const Tensor& A, const Tensor& C, const Tensor& U, int64_t K)
 }
 
 std::tuple<Tensor, Tensor> drsa_step(const Tensor& A, const Tensor& C, const Tensor& U, int64_t K) {
+  DRSA_GUARD(A);
   check_problem(A, C, U, K);
   Ws ws(A.size(0), A.size(1), K, A.options());
   Tensor Un = at::empty_like(U);
@@ -70,6 +87,7 @@ std::tuple<Tensor, Tensor> drsa_step(const Tensor& A, const Tensor& C, const Ten
 }
 
 Tensor drsa_objective(const Tensor& A, const Tensor& C, const Tensor& U, int64_t K) {
+  DRSA_GUARD(A);
   check_problem(A, C, U, K);
   Ws ws(A.size(0), A.size(1), K, A.options());
   check(drsa_amd_drsa_objective(A.data_ptr<float>(), C.data_ptr<float>(), A.size(0), (int)A.size(1), (int)K,
@@ -79,7 +97,42 @@ Tensor drsa_objective(const Tensor& A, const Tensor& C, const Tensor& U, int64_t
   return ws.f.reshape({});
 }
 
+std::tuple<Tensor, Tensor> drsa_run_16(const Tensor& A, const Tensor& C, const Tensor& U0, int64_t K, int64_t steps) {
+  // C5 bf16 / fp16 activation and context rows: the one-problem form of drsa_amd_drsa_run_multi
+  // (U-projection GEMM on bf16 / fp16 MFMA, fp32 accumulation and polar), as drsa_run_joint does
+  const at::ScalarType dt = A.scalar_type();
+  need(A, "activation_vecs", dt), need(C, "context_vecs", dt), need(U0, "U");
+  same_device(A, {&C, &U0});
+  TORCH_CHECK(A.dim() == 2 && A.sizes() == C.sizes(), "drsa_amd: activation and context vectors must be [N, d]");
+  const int64_t d = A.size(1);
+  TORCH_CHECK(U0.dim() == 2 && U0.size(0) == d && U0.size(1) == d, "drsa_amd: U must be [", d, ", ", d, "]");
+  TORCH_CHECK(K > 0 && d % K == 0, "drsa_amd: num_concepts must be a positive divisor of d");
+  TORCH_CHECK(steps >= 0, "drsa_amd: steps must be >= 0");
+  Ws ws(A.size(0), d, K, A.options());
+  Tensor U = U0.clone();
+  Tensor Ut = at::empty_like(U);
+  Tensor traj = at::empty({steps + 1}, U0.options());
+  drsa_amd_problem_t p{};
+  p.A = static_cast<const float*>(A.data_ptr());
+  p.C = static_cast<const float*>(C.data_ptr());
+  p.N = A.size(0);
+  p.d = (int)d;
+  p.K = (int)K;
+  p.U_io = U.data_ptr<float>();
+  p.U_tmp = Ut.data_ptr<float>();
+  p.f_traj = traj.data_ptr<float>();
+  p.counter = ws.counter.data_ptr<int>();
+  p.ws = ws.buf.data_ptr();
+  p.ws_size = ws.buf.numel();
+  p.dtype = dt == at::kBFloat16 ? 1 : 2;
+  void* s = cur_stream();
+  check(drsa_amd_drsa_run_multi(1, &p, (int)steps, s != nullptr ? 1 : 0, s), "drsa_run (16-bit rows)");
+  return {U, traj};
+}
+
 std::tuple<Tensor, Tensor> drsa_run(const Tensor& A, const Tensor& C, const Tensor& U0, int64_t K, int64_t steps) {
+  DRSA_GUARD(A);
+  if (A.scalar_type() == at::kBFloat16 || A.scalar_type() == at::kHalf) return drsa_run_16(A, C, U0, K, steps);
   check_problem(A, C, U0, K);
   TORCH_CHECK(steps >= 0, "drsa_amd: steps must be >= 0");
   Ws ws(A.size(0), A.size(1), K, A.options());
@@ -97,6 +150,7 @@ std::tuple<Tensor, Tensor> drsa_run(const Tensor& A, const Tensor& C, const Tens
 }
 
 Tensor polar(const Tensor& V_) {
+  DRSA_GUARD(V_);
   Tensor V = V_.contiguous();
   need(V, "V");
   TORCH_CHECK(V.dim() == 2 && V.size(0) == V.size(1), "drsa_amd: polar needs a square matrix");
@@ -105,10 +159,15 @@ Tensor polar(const Tensor& V_) {
   return out;
 }
 
-Tensor subspace_relevances(const Tensor& act, const Tensor& ctx, const Tensor& U, int64_t K) {
+Tensor subspace_relevances(const Tensor& act, const Tensor& ctx, const Tensor& U_, int64_t K) {
+  DRSA_GUARD(act);
   TORCH_CHECK(act.dim() < 4 || ctx.dim() < 4, "drsa_amd: act and ctx must be [batch, N, d] or [N, d]");
-  Tensor a = act.dim() == 3 ? act : act.unsqueeze(0);
-  Tensor c = ctx.dim() == 3 ? ctx : ctx.unsqueeze(0);
+  TORCH_CHECK(act.is_cuda(), "drsa_amd: act must be a GPU tensor (there is no CPU kernel)");
+  same_device(act, {&ctx, &U_});
+  // explainer.py:168-180 semantics: any float dtype / layout, computed in fp32
+  Tensor a = (act.dim() == 3 ? act : act.unsqueeze(0)).to(at::kFloat).contiguous();
+  Tensor c = (ctx.dim() == 3 ? ctx : ctx.unsqueeze(0)).to(at::kFloat).contiguous();
+  Tensor U = U_.to(at::kFloat).contiguous();
   need(a, "act"), need(c, "ctx"), need(U, "U");
   TORCH_CHECK(a.dim() == 3 && c.sizes() == a.sizes(), "drsa_amd: act and ctx must have one shape [b, N, d]");
   const int64_t b = a.size(0), N = a.size(1), d = a.size(2);
@@ -127,7 +186,9 @@ Tensor subspace_relevances(const Tensor& act, const Tensor& ctx, const Tensor& U
 std::tuple<Tensor, Tensor, Tensor> lrp_conv_fwd(const Tensor& x, const Tensor& wts, const Tensor& bias3,
                                                 const c10::optional<Tensor>& den_map, int64_t cout, int64_t ng,
                                                 bool pool) {
+  DRSA_GUARD(x);
   need(x, "x"), need(wts, "wts"), need(bias3, "bias3");
+  same_device(x, {&wts, &bias3}), same_device(x, den_map);
   TORCH_CHECK(x.dim() == 4, "drsa_amd: x must be [B, C, H, W]");
   const int64_t B = x.size(0), cin = x.size(1), H = x.size(2), W = x.size(3);
   const int64_t Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
@@ -144,7 +205,9 @@ std::tuple<Tensor, Tensor, Tensor> lrp_conv_fwd(const Tensor& x, const Tensor& w
 Tensor lrp_conv_bwd(const Tensor& g, const c10::optional<Tensor>& amax, const Tensor& wts,
                     const c10::optional<Tensor>& x, const c10::optional<Tensor>& den, int64_t cin, int64_t H, int64_t W,
                     int64_t clones, int64_t ng, int64_t xmode, int64_t post, double eps) {
+  DRSA_GUARD(g);
   need(g, "g"), need(wts, "wts");
+  same_device(g, {&wts}), same_device(g, amax), same_device(g, x), same_device(g, den);
   const int64_t Bq = g.size(0), cout = g.size(1);
   Tensor out = at::empty({Bq, cin, H, W}, g.options());
   check(drsa_amd_conv_bwd(g.data_ptr<float>(), cptr<uint8_t>(amax), wts.data_ptr<float>(), cptr(x), cptr(den),
@@ -156,7 +219,9 @@ Tensor lrp_conv_bwd(const Tensor& g, const c10::optional<Tensor>& amax, const Te
 
 std::tuple<Tensor, Tensor> lrp_linear_fwd(const Tensor& x, const Tensor& Wt, const c10::optional<Tensor>& b,
                                           bool relu) {
+  DRSA_GUARD(x);
   need(x, "x"), need(Wt, "W");
+  same_device(x, {&Wt}), same_device(x, b);
   const int64_t M = x.size(0), K = x.size(1), N = Wt.size(0);
   Tensor z = at::empty({M, N}, x.options());
   Tensor a = relu ? at::empty({M, N}, x.options()) : at::empty({0}, x.options());
@@ -169,7 +234,9 @@ std::tuple<Tensor, Tensor> lrp_linear_fwd(const Tensor& x, const Tensor& Wt, con
 Tensor lrp_linear_bwd(const c10::optional<Tensor>& R, const c10::optional<Tensor>& cls, bool one_hot, const Tensor& z,
                       bool relu_mask, bool rule_eps, double eps, const Tensor& Wt, const Tensor& x, int64_t xmode,
                       const c10::optional<Tensor>& den, int64_t post, double eps_post) {
+  DRSA_GUARD(z);
   need(z, "z"), need(Wt, "W"), need(x, "x");
+  same_device(z, {&Wt, &x}), same_device(z, R), same_device(z, cls), same_device(z, den);
   const int64_t M = z.size(0), Nout = z.size(1), Kin = Wt.size(1);
   Tensor out = at::empty({M, Kin}, z.options());
   check(drsa_amd_linear_bwd(cptr(R), cptr<int>(cls), one_hot ? 1 : 0, z.data_ptr<float>(), relu_mask ? 1 : 0,
@@ -188,7 +255,9 @@ Tensor residual(const Tensor& U) {   // P = U U^T - I (drsa_amd_projection_resid
 }
 
 std::tuple<Tensor, Tensor> projection_fwd(const Tensor& a, const Tensor& U, bool pool) {
+  DRSA_GUARD(a);
   need(a, "a"), need(U, "U");
+  same_device(a, {&U});
   const int64_t B = a.size(0), D = a.size(1), H = a.size(2), W = a.size(3);
   Tensor P = residual(U);
   if (pool) {
@@ -210,7 +279,9 @@ std::tuple<Tensor, Tensor> projection_fwd(const Tensor& a, const Tensor& U, bool
 Tensor projection_bwd(const Tensor& g, const c10::optional<Tensor>& amax, const Tensor& a,
                       const c10::optional<Tensor>& den, const Tensor& U, int64_t K, double eps_proj, double eps_den,
                       bool fanout) {
+  DRSA_GUARD(a);
   need(g, "g"), need(a, "a"), need(U, "U");
+  same_device(a, {&g, &U}), same_device(a, amax), same_device(a, den);
   const int64_t B = a.size(0), D = a.size(1), H = a.size(2), W = a.size(3);
   const int64_t nq = fanout ? K + 1 : 1;
   Tensor G = at::empty({B * nq, D, H, W}, a.options());
@@ -223,6 +294,7 @@ Tensor projection_bwd(const Tensor& g, const c10::optional<Tensor>& amax, const 
 }
 
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> heatmap_sort(const Tensor& hm, int64_t K, bool std_from_sum) {
+  DRSA_GUARD(hm);
   need(hm, "hm");
   const int64_t H = hm.size(-2), W = hm.size(-1);
   const int64_t B = hm.numel() / ((std_from_sum ? K : K + 1) * H * W);

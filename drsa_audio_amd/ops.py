@@ -90,7 +90,7 @@ def _(V):
 @_fake("subspace_relevances")
 def _(act, ctx, U, K):
     b = act.shape[0] if act.dim() == 3 else 1
-    return act.new_empty(b, K)
+    return act.new_empty(b, K, dtype=torch.float32)
 
 
 @_fake("lrp_conv_fwd")

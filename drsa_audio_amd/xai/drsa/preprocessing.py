@@ -123,10 +123,23 @@ def preprocess_data(model: nn.Module, input_batch, composite, layer_idx: int, cl
     name = _layer_name(model, layer_idx)
     eng = get_engine(model, composite)
     B = x.size(0)
-    if B == 0:
+    # with a group every rank joins the size exchange first, so an empty slice on one rank cannot
+    # strand the others in a collective; an empty GLOBAL batch raises on every rank together
+    off, B_all = (0, B) if group is None else _sample_offset(B, group, dev)
+    if B_all == 0:
         raise _capi.DrsaAmdError("preprocess_data: empty input batch")
-    off, B_all = (0, B) if group is None else _sample_offset(B, group)
     li, where = eng.capture_stage(name)
+    if B == 0:
+        # this rank holds no samples: empty rows of the layer's width (one dummy sample through the
+        # engine gives the geometry); the numpy stream still advances over all B_all draws
+        cap = eng.capture(torch.zeros((1,) + tuple(x.shape[1:]), device=dev, dtype=x.dtype), name,
+                          cls=None if class_idx is None else _class_rows(1, class_idx, dev),
+                          one_hot=one_hot_encoded, seed_fn=_seed_fn(class_idx, num_classes, one_hot_encoded))
+        C, H, W = cap["C"], cap["H"], cap["W"]
+        if num_locations:
+            sample_spatial_locations(B_all, (H, W), num_locations)
+            return torch.empty(0, C, device=dev), torch.empty(0, C, device=dev)
+        return torch.empty(0, H * W, C, device=dev), torch.empty(0, H * W, C, device=dev)
     idx_all = None
     out_a = out_c = None
     step = max(1, int(attr_batch_size))
@@ -196,7 +209,11 @@ def _all_gather_rows(t: torch.Tensor, group) -> torch.Tensor:
     """[world, *t.shape] with rank r's ``t`` in row r (RCCL on the device, gloo through the host)."""
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    src = t if dist.get_backend(group) == "nccl" else t.cpu()
+    if dist.get_backend(group) == "nccl":
+        # RCCL moves device tensors only: a host tensor (e.g. a size) goes to this rank's device
+        src = t if t.is_cuda else t.to(torch.device("cuda", torch.cuda.current_device()))
+    else:
+        src = t.cpu()
     parts = [torch.empty_like(src) for _ in range(world)]
     dist.all_gather(parts, src.contiguous(), group=group)
     return torch.stack(parts).to(t.device)
@@ -232,11 +249,11 @@ def normalize_vectors(vectors: torch.Tensor, out: Optional[torch.Tensor] = None,
     return out
 
 
-def _sample_offset(b_local: int, group) -> Tuple[int, int]:
+def _sample_offset(b_local: int, group, device=None) -> Tuple[int, int]:
     """(first global sample index of this rank, global batch size): ranks hold consecutive slices."""
     import torch.distributed as dist
     rank = dist.get_rank(group)
-    sizes = _all_gather_rows(torch.tensor([b_local], dtype=torch.int64), group).reshape(-1).tolist()
+    sizes = _all_gather_rows(torch.tensor([b_local], dtype=torch.int64, device=device), group).reshape(-1).tolist()
     return int(sum(sizes[:rank])), int(sum(sizes))
 
 

@@ -1,7 +1,10 @@
 """Generate golden fixtures under tests/golden/ by running the REFERENCE code.
 
-Runs only in the build container (needs /root/reference).  Never imported by the
-product, never run on the GPU box.  The reference's ``cxai/xai/drsa/drsa.py`` has an
+Runs only in the build container (needs /root/reference); nothing here is imported by the
+product.  Tests import this module for its input-case tables (SORT_CASES, SUBREL_CASES, ...);
+the reference itself is imported only inside the generator functions, never at import time.
+The seeded DRSA row generator lives in ``drsa_audio_amd/utils/synthetic.py`` (re-exported here
+for the fixture scripts).  The reference's ``cxai/xai/drsa/drsa.py`` has an
 import typo (``from pathilib import Path``, drsa.py:4, defect D1); a one-line
 ``sys.modules['pathilib']`` shim supplies the name, the file itself is unmodified.
 
@@ -33,6 +36,11 @@ import types
 import numpy as np
 import torch
 
+_ROOT = str(pathlib.Path(__file__).resolve().parent.parent)
+if _ROOT not in sys.path:
+    sys.path.insert(0, _ROOT)
+from drsa_audio_amd.utils.synthetic import drsa_inputs  # noqa: E402,F401  (fixture rows)
+
 REF = "/root/reference"
 OUT = pathlib.Path(__file__).resolve().parent.parent / "tests" / "golden"
 
@@ -45,20 +53,6 @@ def _import_reference():
     from cxai.model import create_model as rcm
     from cxai.model import modify_model as rmm
     return rdrsa, rcm, rmm
-
-
-def drsa_inputs(N: int, d: int, seed: int):
-    """Synthetic DRSA data: A = |N(0,1)| (post-ReLU-like), C ~ N(0,1), both normalised
-    with preprocessing.normalize_vectors semantics (v / rms / d^{1/4})."""
-    rng = np.random.default_rng(seed)
-    A = np.abs(rng.standard_normal((N, d))).astype(np.float32)
-    C = rng.standard_normal((N, d)).astype(np.float32)
-
-    def norm(v):
-        t = torch.from_numpy(v)
-        E = torch.sqrt(torch.mean(torch.square(t)))
-        return (t / E / d ** 0.25).numpy()
-    return norm(A), norm(C)
 
 
 def _drsa(rdrsa):

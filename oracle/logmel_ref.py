@@ -164,24 +164,5 @@ def load_songs(songs: np.ndarray, case="gtzan", num_chunks=None, mode="f64"):
     return np.concatenate(out, axis=0)
 
 
-def synthetic_songs(n_songs: int, seconds: float = 29.5, sample_rate: int = 16000, seed: int = 0) -> np.ndarray:
-    """Music-like synthetic waveforms: a few harmonic tones with vibrato and decaying
-    envelopes plus coloured noise, random gain per song.  float32 [S, T]."""
-    rng = np.random.default_rng(seed)
-    T = int(seconds * sample_rate)
-    t = np.arange(T) / sample_rate
-    out = np.empty((n_songs, T), dtype=np.float32)
-    for i in range(n_songs):
-        x = np.zeros(T)
-        for _ in range(4):
-            f0 = rng.uniform(60, 1500)
-            vib = 1 + 0.003 * np.sin(2 * np.pi * rng.uniform(3, 7) * t)
-            env = np.exp(-((t * rng.uniform(0.5, 4)) % 1.0) * rng.uniform(1, 6))
-            for h in range(1, 6):
-                if f0 * h < 7800:
-                    x += rng.uniform(0.1, 1) / h * env * np.sin(2 * np.pi * f0 * h * t * vib + rng.uniform(0, 6.3))
-        noise = np.cumsum(rng.standard_normal(T)) * 1e-3
-        noise -= np.convolve(noise, np.ones(64) / 64, mode="same")
-        x += noise + 0.02 * rng.standard_normal(T)
-        out[i] = (x * rng.uniform(0.05, 0.9) / np.abs(x).max()).astype(np.float32)
-    return out
+# the synthetic songs generator moved to the product's data module (bench.py may not import the oracle)
+from drsa_audio_amd.utils.synthetic import synthetic_songs  # noqa: E402,F401

@@ -13,7 +13,7 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 from drsa_audio_amd import _capi  # noqa: E402
 from drsa_audio_amd.xai.drsa.drsa import DrsaWorkspace  # noqa: E402
-from gen_fixtures import drsa_inputs  # noqa: E402
+from drsa_audio_amd.utils.synthetic import drsa_inputs  # noqa: E402
 
 
 def ns_iters(dev, N, d, K, seed):

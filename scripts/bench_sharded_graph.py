@@ -11,7 +11,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from gen_fixtures import drsa_inputs
+from drsa_audio_amd.utils.synthetic import drsa_inputs
 
 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
 os.environ.setdefault("MASTER_PORT", "29533")

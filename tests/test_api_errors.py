@@ -97,6 +97,10 @@ def test_c_abi_argument_validation_without_gpu():
     assert lib.drsa_amd_drsa_slab_floats(100, 4) == 128 * 128 + 4
     assert lib.drsa_amd_drsa_slab_floats(64, 4) == 64 * 64 + 4
     assert lib.drsa_amd_drsa_workspace_bytes(100, 128, 3) == 0
+    # compact den ring backward: pooled W >= 8 (W % 8 == 0) and H >= 2, as the forward's layout needs
+    for H, W in ((4, 4), (0, 8), (4, 12)):
+        with pytest.raises(_capi.DrsaAmdError, match="pooled H >= 2"):
+            _capi.call("drsa_amd_conv_bwd_den_ring", p, None, p, 0, p, p, p, p, 1, 1, 32, 32, H, W, 1, 1, 1e-7, None)
 
 
 def test_alphabeta_parameter_checks_like_zennit():

@@ -147,27 +147,33 @@ def test_prototype_search_matches_oracle():
     assert sp is not None and len(sp) == n
 
 
-def _rank_local_worker(rank, world, port, x_local, q):
+def _rank_local_worker(rank, world, port, x_local, q, backend="gloo", steps=30):
     import os
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "tests"), os.path.join(root, "oracle")]
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     from lrp_common import gtzan128
     from drsa_audio_amd.xai.drsa.preprocessing import drsa_training_data
     from drsa_audio_amd.xai.drsa.distributed import sharded_run
     from drsa_audio_amd.utils.constants import LRP_NAME_MAP_GTZAN
     from drsa_audio_amd.zennit.composites import NameMapComposite
-    dev = torch.device("cuda", 0)
-    torch.cuda.set_device(dev)
     np.random.seed(7)
     A, C = drsa_training_data(gtzan128().to(dev), x_local.to(dev), NameMapComposite(LRP_NAME_MAP_GTZAN), 7, 3,
                               num_locations=20, group=dist.group.WORLD)
     U0 = torch.from_numpy(np.linalg.qr(np.random.default_rng(0).standard_normal((64, 64)))[0].astype(np.float32))
-    U, traj = sharded_run(A, C, U0.to(dev), 4, 30)
-    q.put((rank, A.cpu().numpy(), C.cpu().numpy(), traj, U.cpu().numpy()))
+    if steps:
+        U, traj = sharded_run(A, C, U0.to(dev), 4, steps)
+    else:
+        U, traj = U0, np.zeros(0)
+    q.put((rank, A.cpu().numpy(), C.cpu().numpy(), traj, U.cpu().numpy(), float(np.random.rand())))
     dist.destroy_process_group()
 
 
@@ -210,3 +216,54 @@ def test_rank_local_training_data_two_ranks_equals_single_process():
     _, traj1 = drsa_run(A, C, U0.to(DEV), 4, 30, DrsaWorkspace(A.size(0), 64, 4, DEV))
     traj1 = traj1.cpu().numpy()
     assert np.max(np.abs(res[0][2] - traj1) / np.abs(traj1)) < 1e-5
+
+
+def _spawn_ranks(parts, backend="gloo", steps=30):
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_local_worker, args=(r, len(parts), port, parts[r], q, backend, steps))
+             for r in range(len(parts))]
+    for p in procs:
+        p.start()
+    res = {r[0]: r[1:] for r in (q.get(timeout=300) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def test_rank_local_training_data_rccl_world1():
+    """drsa_training_data(group=) over an RCCL ('nccl') group, whose size exchange
+    starts from a host tensor: one rank, rows equal to the ungrouped call bit for bit."""
+    from drsa_audio_amd.xai.drsa.preprocessing import drsa_training_data
+    x = logmel(4, seed=9)
+    np.random.seed(7)
+    A, C = drsa_training_data(_gpu(gtzan128()), x.to(DEV), NameMapComposite(LRP_NAME_MAP_GTZAN), 7, 3,
+                              num_locations=20)
+    r_after = float(np.random.rand())
+    res = _spawn_ranks([x.clone()], backend="nccl", steps=0)
+    assert np.array_equal(res[0][0], A.cpu().numpy()) and np.array_equal(res[0][1], C.cpu().numpy())
+    assert res[0][4] == r_after                       # the numpy stream advanced identically
+
+
+def test_rank_local_training_data_empty_slice():
+    """a rank with an empty slice returns empty rows instead of raising before the
+    collectives (which stranded the other ranks); the other rank's rows equal the single-process
+    result within 1 ulp and both ranks leave the numpy stream where one process would."""
+    from drsa_audio_amd.xai.drsa.preprocessing import drsa_training_data
+    x = logmel(3, seed=12)
+    np.random.seed(7)
+    A, C = drsa_training_data(_gpu(gtzan128()), x.to(DEV), NameMapComposite(LRP_NAME_MAP_GTZAN), 7, 3,
+                              num_locations=20)
+    r_after = float(np.random.rand())
+    res = _spawn_ranks([x.clone(), x[:0].clone()], steps=0)
+    assert res[1][0].shape == (0, 64) and res[1][1].shape == (0, 64)
+    for got, ref in ((res[0][0], A.cpu().numpy()), (res[0][1], C.cpu().numpy())):
+        ulp = np.abs(got.view(np.int32).astype(np.int64) - ref.view(np.int32).astype(np.int64))
+        assert ulp.max() <= 1, ulp.max()
+    assert res[0][4] == res[1][4] == r_after
