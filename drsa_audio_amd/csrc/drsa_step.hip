@@ -99,14 +99,36 @@ struct PCfg {
   static constexpr int NW = (DP * CW > 4096) ? 4 : ((DP <= 64 && CW == 16) ? 16 : 8);
   static constexpr int NT = NW * 64;
   static constexpr int KP = DP / DKP;
-  static constexpr int RT = DP <= 64 ? 128 : 96;   // rows per staged tile (one tile at N/CUs <= RT)
+  // rows per staged tile (one tile per leaf at N / kLeaves <= RT).  DP = 128: 80 rows, so the
+  // grouped kernel's LDS accumulator (DP x SLD) fits beside the tiles in 160 KB
+  static constexpr int RT = DP <= 64 ? 128 : 80;
   static constexpr int LDA = DP + 4;               // staging row stride (16-B aligned rows)
   static constexpr int NV = RT * DP / 4;           // float4 slots per matrix per tile
   static constexpr int PFN = (NV + NT - 1) / NT;   // prefetch registers (float4) per matrix per thread
   static constexpr size_t tile_floats = 2 * (size_t)RT * LDA;
   static constexpr size_t red_floats = (size_t)NW * DP * CW + (size_t)NW * 64 * NCB;
   static constexpr size_t lds_bytes = (tile_floats > red_floats ? tile_floats : red_floats) * sizeof(float);
+  // grouped kernel (drsa_partial_grouped_kernel): only the waves w >= CG park their Gt in LDS (the
+  // partners w % CG fold them), beside the S-partials; the leaf-group accumulator has its own area
+  static constexpr int SLD = DP + 4;               // accumulator row stride: lanes 4 rows apart on other banks
+  static constexpr size_t gred_floats = (size_t)(NW - CG) * DP * CW + (size_t)NW * 64 * NCB;
+  static constexpr size_t gtile_floats = tile_floats > gred_floats ? tile_floats : gred_floats;
+  static constexpr size_t gacc_floats = (size_t)DP * SLD + KP;
+  static constexpr size_t glds_bytes = (gtile_floats + gacc_floats) * sizeof(float);
+  static_assert(glds_bytes <= 160 * 1024, "grouped partial: LDS");
 };
+
+// The row partition of every fp32 gradient (drsa_run, drsa_partial, the fused and sharded steps,
+// run_multi, the batched grid): L = min(kLeaves, ceil(N / 16)) LEAVES, leaf l = row blocks
+// [l R / L, (l + 1) R / L) of the R 16-row blocks, each reduced by the partial's fixed wave order
+// into a leaf slab; leaves form groups of kLeafGroup (ascending); the gradient is the left fold over
+// groups of the left fold over each group's leaves.  drsa_partial_kernel runs one workgroup per
+// leaf; drsa_partial_grouped_kernel (the batched grid) runs whole groups per workgroup and folds
+// them on chip -- the same leaf slabs added in the same order, so the same bits for any number of
+// workgroups per problem.  Fixed constants (not the CU count): results do not depend on the device.
+constexpr int kLeaves = 256;
+constexpr int kLeafGroup = 8;
+constexpr int kMaxGroups = kLeaves / kLeafGroup;
 
 // 16-bit A/C element (DT 1 bf16, DT 2 fp16 bit patterns) -> fp32 (exact), fp32 that came from
 // such an element -> its bits (exact), and fp32 -> 16-bit with round-to-nearest-even (U)
@@ -149,6 +171,122 @@ constexpr int partial_threads() { return PCfg<DP, DKP>::NT; }
 // read (the fused step computes U there, see drsa_fused_step_kernel), `uval(k, j, jp)` returns
 // U[k][j] (jp: its padded column), `mid()` runs after U is in registers and before the first LDS
 // tile store.
+// One 16-row block of a staged tile (rows Ar / Cr, LDA stride) for this wave's column group:
+// GEMM1 (XA = A U, XC = C U), s = sum over the concept block of XA (.) XC, r = relu(s), the S
+// partials (sacc) and GEMM2 (Gt += A^T (r XC) + C^T (r XA)) accumulated in g.  Shared by the
+// per-leaf and the grouped partial kernels, so both add the same terms in the same order.
+template <int DP, int DKP, int DT>
+__device__ __forceinline__ void rowblock_step(const float* __restrict__ Ar, const float* __restrict__ Cr,
+                                              const float (&ureg)[DT ? 1 : PCfg<DP, DKP>::NCB][DT ? 1 : DP / 16][4],
+                                              const u16x8 (&ubf)[DT ? PCfg<DP, DKP>::NCB : 1][DT ? (DP / 32 > 0 ? DP / 32 : 1) : 1],
+                                              f32x4 (&g)[DP / 16][PCfg<DP, DKP>::NCB], float (&sacc)[PCfg<DP, DKP>::NCB],
+                                              int nq_live, int l15, int lg) {
+  using Cfg = PCfg<DP, DKP>;
+  constexpr bool BF = DT != 0;
+  constexpr int NCB = Cfg::NCB, NIB = Cfg::NIB, LDA = Cfg::LDA;
+  constexpr int NQ = DP / 16, NQ2 = DP / 32 > 0 ? DP / 32 : 1;
+  // ---- GEMM1: XA, XC for the 16 rows and this wave's NCB column blocks ----
+  f32x4 xa[NCB], xc[NCB];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) { xa[cb] = f32x4{0.f, 0.f, 0.f, 0.f}; xc[cb] = xa[cb]; }
+  if constexpr (!BF) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      if (q >= nq_live) break;
+      const float4 a4 = *reinterpret_cast<const float4*>(Ar + l15 * LDA + 16 * q + 4 * lg);
+      const float4 c4 = *reinterpret_cast<const float4*>(Cr + l15 * LDA + 16 * q + 4 * lg);
+      const float av[4] = {a4.x, a4.y, a4.z, a4.w}, cv[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+          xa[cb] = mfma16(av[tt], ureg[cb][q][tt], xa[cb]);
+          xc[cb] = mfma16(cv[tt], ureg[cb][q][tt], xc[cb]);
+        }
+    }
+  } else {
+#pragma unroll
+    for (int q2 = 0; q2 < NQ2; ++q2) {
+      const float* pa8 = Ar + l15 * LDA + 32 * q2 + 8 * lg;
+      const float* pc8 = Cr + l15 * LDA + 32 * q2 + 8 * lg;
+      const float4 a0 = *reinterpret_cast<const float4*>(pa8), a1 = *reinterpret_cast<const float4*>(pa8 + 4);
+      const float4 c0 = *reinterpret_cast<const float4*>(pc8), c1 = *reinterpret_cast<const float4*>(pc8 + 4);
+      u16x8 ab, cbv;   // the widened 16-bit values narrow back exactly
+      ab[0] = nar16<DT>(a0.x); ab[1] = nar16<DT>(a0.y); ab[2] = nar16<DT>(a0.z); ab[3] = nar16<DT>(a0.w);
+      ab[4] = nar16<DT>(a1.x); ab[5] = nar16<DT>(a1.y); ab[6] = nar16<DT>(a1.z); ab[7] = nar16<DT>(a1.w);
+      cbv[0] = nar16<DT>(c0.x); cbv[1] = nar16<DT>(c0.y); cbv[2] = nar16<DT>(c0.z); cbv[3] = nar16<DT>(c0.w);
+      cbv[4] = nar16<DT>(c1.x); cbv[5] = nar16<DT>(c1.y); cbv[6] = nar16<DT>(c1.z); cbv[7] = nar16<DT>(c1.w);
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        if constexpr (DT == 1) {
+          xa[cb] = mfma16_bf16(ab, ubf[cb][q2], xa[cb]);
+          xc[cb] = mfma16_bf16(cbv, ubf[cb][q2], xc[cb]);
+        } else {
+          xa[cb] = mfma16_f16(ab, ubf[cb][q2], xa[cb]);
+          xc[cb] = mfma16_f16(cbv, ubf[cb][q2], xc[cb]);
+        }
+      }
+    }
+  }
+
+  // ---- s = sum over the concept block of XA (.) XC, r = relu(s); S partial ----
+  // lane holds rows 4 lg + r, column 16 (cg NCB + cb) + l15
+  float rr[NCB][4];
+  if constexpr (DKP >= 16) {   // the whole column group is one concept
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = 0.f;
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) v += xa[cb][r] * xc[cb][r];
+      v += shfl_xor(v, 1); v += shfl_xor(v, 2); v += shfl_xor(v, 4); v += shfl_xor(v, 8);
+      const float rv = v > 0.f ? v : 0.f;
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) rr[cb][r] = rv;
+    }
+    if (l15 == 0) {
+      float acc = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc += rr[0][r] * rr[0][r];
+      sacc[0] += acc;
+    }
+  } else {
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = xa[cb][r] * xc[cb][r];
+        if constexpr (DKP >= 2) v += shfl_xor(v, 1);
+        if constexpr (DKP >= 4) v += shfl_xor(v, 2);
+        if constexpr (DKP >= 8) v += shfl_xor(v, 4);
+        rr[cb][r] = v > 0.f ? v : 0.f;
+      }
+      if ((l15 % DKP) == 0) {
+        float acc = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc += rr[cb][r] * rr[cb][r];
+        sacc[cb] += acc;
+      }
+    }
+  }
+
+  // ---- GEMM2: Gt[i][j] += sum_n A[n][i] P[n][j] + C[n][i] Q[n][j]  (P = r XC, Q = r XA) ----
+  // k-step tt covers rows n = 4 lg + tt: the B operand is this lane's own MFMA output register.
+#pragma unroll
+  for (int ib = 0; ib < NIB; ++ib) {
+    if (ib >= nq_live) break;
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      const float av = Ar[(4 * lg + tt) * LDA + 16 * ib + l15];
+      const float cv = Cr[(4 * lg + tt) * LDA + 16 * ib + l15];
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        g[ib][cb] = mfma16(av, rr[cb][tt] * xc[cb][tt], g[ib][cb]);
+        g[ib][cb] = mfma16(cv, rr[cb][tt] * xa[cb][tt], g[ib][cb]);
+      }
+    }
+  }
+}
+
 template <int DP, int DKP, int DT, bool VEC, class Pre, class UVal, class Mid>
 __device__ __forceinline__ void partial_core(const void* __restrict__ A_, const void* __restrict__ C_, int64_t N,
                                              int d, int K, int dk, float* __restrict__ partials, int64_t rb_total,
@@ -307,108 +445,7 @@ __device__ __forceinline__ void partial_core(const void* __restrict__ A_, const 
     const int64_t rbt = rb0 + (int64_t)t * (RT / 16);
     const int nrb = (int)((rb1 - rbt) < (RT / 16) ? (rb1 - rbt) : (RT / 16));
     for (int rbl = w / CG; rbl < nrb; rbl += WPG) {
-      const float* Ar = As + 16 * rbl * LDA;
-      const float* Cr = Cs + 16 * rbl * LDA;
-      // ---- GEMM1: XA, XC for the 16 rows and this wave's NCB column blocks ----
-      f32x4 xa[NCB], xc[NCB];
-#pragma unroll
-      for (int cb = 0; cb < NCB; ++cb) { xa[cb] = f32x4{0.f, 0.f, 0.f, 0.f}; xc[cb] = xa[cb]; }
-      if constexpr (!BF) {
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          if (q >= nq_live) break;
-          const float4 a4 = *reinterpret_cast<const float4*>(Ar + l15 * LDA + 16 * q + 4 * lg);
-          const float4 c4 = *reinterpret_cast<const float4*>(Cr + l15 * LDA + 16 * q + 4 * lg);
-          const float av[4] = {a4.x, a4.y, a4.z, a4.w}, cv[4] = {c4.x, c4.y, c4.z, c4.w};
-#pragma unroll
-          for (int tt = 0; tt < 4; ++tt)
-#pragma unroll
-            for (int cb = 0; cb < NCB; ++cb) {
-              xa[cb] = mfma16(av[tt], ureg[cb][q][tt], xa[cb]);
-              xc[cb] = mfma16(cv[tt], ureg[cb][q][tt], xc[cb]);
-            }
-        }
-      } else {
-#pragma unroll
-        for (int q2 = 0; q2 < NQ2; ++q2) {
-          const float* pa8 = Ar + l15 * LDA + 32 * q2 + 8 * lg;
-          const float* pc8 = Cr + l15 * LDA + 32 * q2 + 8 * lg;
-          const float4 a0 = *reinterpret_cast<const float4*>(pa8), a1 = *reinterpret_cast<const float4*>(pa8 + 4);
-          const float4 c0 = *reinterpret_cast<const float4*>(pc8), c1 = *reinterpret_cast<const float4*>(pc8 + 4);
-          u16x8 ab, cbv;   // the widened 16-bit values narrow back exactly
-          ab[0] = nar16<DT>(a0.x); ab[1] = nar16<DT>(a0.y); ab[2] = nar16<DT>(a0.z); ab[3] = nar16<DT>(a0.w);
-          ab[4] = nar16<DT>(a1.x); ab[5] = nar16<DT>(a1.y); ab[6] = nar16<DT>(a1.z); ab[7] = nar16<DT>(a1.w);
-          cbv[0] = nar16<DT>(c0.x); cbv[1] = nar16<DT>(c0.y); cbv[2] = nar16<DT>(c0.z); cbv[3] = nar16<DT>(c0.w);
-          cbv[4] = nar16<DT>(c1.x); cbv[5] = nar16<DT>(c1.y); cbv[6] = nar16<DT>(c1.z); cbv[7] = nar16<DT>(c1.w);
-#pragma unroll
-          for (int cb = 0; cb < NCB; ++cb) {
-            if constexpr (DT == 1) {
-              xa[cb] = mfma16_bf16(ab, ubf[cb][q2], xa[cb]);
-              xc[cb] = mfma16_bf16(cbv, ubf[cb][q2], xc[cb]);
-            } else {
-              xa[cb] = mfma16_f16(ab, ubf[cb][q2], xa[cb]);
-              xc[cb] = mfma16_f16(cbv, ubf[cb][q2], xc[cb]);
-            }
-          }
-        }
-      }
-
-      // ---- s = sum over the concept block of XA (.) XC, r = relu(s); S partial ----
-      // lane holds rows 4 lg + r, column 16 (cg NCB + cb) + l15
-      float rr[NCB][4];
-      if constexpr (DKP >= 16) {   // the whole column group is one concept
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = 0.f;
-#pragma unroll
-          for (int cb = 0; cb < NCB; ++cb) v += xa[cb][r] * xc[cb][r];
-          v += shfl_xor(v, 1); v += shfl_xor(v, 2); v += shfl_xor(v, 4); v += shfl_xor(v, 8);
-          const float rv = v > 0.f ? v : 0.f;
-#pragma unroll
-          for (int cb = 0; cb < NCB; ++cb) rr[cb][r] = rv;
-        }
-        if (l15 == 0) {
-          float acc = 0.f;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc += rr[0][r] * rr[0][r];
-          sacc[0] += acc;
-        }
-      } else {
-#pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float v = xa[cb][r] * xc[cb][r];
-            if constexpr (DKP >= 2) v += shfl_xor(v, 1);
-            if constexpr (DKP >= 4) v += shfl_xor(v, 2);
-            if constexpr (DKP >= 8) v += shfl_xor(v, 4);
-            rr[cb][r] = v > 0.f ? v : 0.f;
-          }
-          if ((l15 % DKP) == 0) {
-            float acc = 0.f;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) acc += rr[cb][r] * rr[cb][r];
-            sacc[cb] += acc;
-          }
-        }
-      }
-
-      // ---- GEMM2: Gt[i][j] += sum_n A[n][i] P[n][j] + C[n][i] Q[n][j]  (P = r XC, Q = r XA) ----
-      // k-step tt covers rows n = 4 lg + tt: the B operand is this lane's own MFMA output register.
-#pragma unroll
-      for (int ib = 0; ib < NIB; ++ib) {
-        if (ib >= nq_live) break;
-#pragma unroll
-        for (int tt = 0; tt < 4; ++tt) {
-          const float av = Ar[(4 * lg + tt) * LDA + 16 * ib + l15];
-          const float cv = Cr[(4 * lg + tt) * LDA + 16 * ib + l15];
-#pragma unroll
-          for (int cb = 0; cb < NCB; ++cb) {
-            g[ib][cb] = mfma16(av, rr[cb][tt] * xc[cb][tt], g[ib][cb]);
-            g[ib][cb] = mfma16(cv, rr[cb][tt] * xa[cb][tt], g[ib][cb]);
-          }
-        }
-      }
+      rowblock_step<DP, DKP, DT>(As + 16 * rbl * LDA, Cs + 16 * rbl * LDA, ureg, ubf, g, sacc, nq_live, l15, lg);
     }
     if (t + 1 < ntile) {
       __syncthreads();
@@ -459,44 +496,279 @@ __global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_ker
 }
 
 // ---------------------------------------------------------------------------
-// reduce: out[e] = sum_p partials[p][e] over the P workgroup slabs (row stride ES); fixed order:
-// 4 interleaved chains p = g, g + 4, ... combined in order g = 0..3 (deterministic, no atomics).
-// (Measured against float4 / 64-group and slab-split variants in scripts/probe_reduce.hip: the
-// kernel boundary behind 4-17 MB of freshly written slabs dominates; this one is the fastest.)
+// batched problems: the descriptor of one problem (task-parallel DRSA grid, optsubspaces.py:17-23)
 // ---------------------------------------------------------------------------
-// One chain per (element, p mod 4): sum over p = grp, grp + 4, ... in ascending order.  The slabs
-// were just written by every CU of the partial (L2 of other XCDs / HBM), so the chain's loads are
-// all issued before its adds (RB of them per batch): one memory round trip per batch instead of
-// one per 8 loads -- the same additions in the same order, so the same bits.
-#ifndef DRSA_REDUCE_BATCH
-#define DRSA_REDUCE_BATCH 64
-#endif
-constexpr int kReduceBatch = DRSA_REDUCE_BATCH;
-__device__ __forceinline__ float reduce_chain(const float* __restrict__ partials, int P, int ES, int e, int grp) {
-  float acc = 0.f;
-  for (int p0 = grp; p0 < P; p0 += 4 * kReduceBatch) {
-    float v[kReduceBatch];
+struct BatchDesc {
+  const float* A;
+  const float* C;
+  int64_t N;
+  int64_t rb_total;
+  int d, K, dk, DKP;
+  int G;                // partial workgroups of this problem (<= gridDim.x)
+  int L;                // leaves (kLeaves partition)
+  int m;                // leaf groups per workgroup (0: one leaf per workgroup, per-leaf slabs)
+  float* U_io;
+  float* U_tmp;
+  float* f_traj;
+  int* counter;
+  float* partials;      // one slab per leaf group
+  float* gs;
+};
+
+// Workgroup b of problem p owns leaf groups [b m, (b + 1) m) and computes their leaves one after
+// another with the per-leaf kernel's arithmetic (rowblock_step, the same tile cut and wave order,
+// Gt reset per leaf), folding each leaf slab -- combined in the per-leaf kernel's wave order -- into
+// an LDS accumulator; a finished group's accumulator is its slab.  U is loaded once per workgroup
+// and the next tile (possibly the next leaf's) is prefetched under the current one's MFMAs.
+template <int DP, int DKP, bool VEC>
+__global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_grouped_kernel(
+    const BatchDesc* __restrict__ bd, int parity) {
+  using Cfg = PCfg<DP, DKP>;
+  constexpr int CW = Cfg::CW, CG = Cfg::CG, NCB = Cfg::NCB, NIB = Cfg::NIB, NW = Cfg::NW, NT = Cfg::NT;
+  constexpr int KP = Cfg::KP, RT = Cfg::RT, LDA = Cfg::LDA, NV = Cfg::NV, PFN = Cfg::PFN, SLD = Cfg::SLD;
+  constexpr int WPG = NW / CG, NQ = DP / 16, RB = RT / 16;
+  constexpr size_t ES = (DP * DP + KP + 3) / 4 * 4;
+  const BatchDesc& q = bd[blockIdx.y];
+  if ((int)blockIdx.x >= q.G) return;    // uniform per workgroup: before any barrier
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  // w uniform (readfirstlane): the per-wave roles of the leaf fold are scalar branches
+  const int tid = threadIdx.x, lane = lane_id(), w = __builtin_amdgcn_readfirstlane(wave_id());
+  const int l15 = lane & 15, lg = lane >> 4;
+  const int cg = w % CG;
+  float* As = smem;                        // [RT][LDA]
+  float* Cs = smem + RT * LDA;             // [RT][LDA]
+  float* red = smem;                       // [(NW - CG) x NIB x NCB x 4][64]   (aliases the tiles)
+  float* sred = smem + (size_t)(NW - CG) * DP * CW;   // [NW][64][NCB]
+  float* S = smem + Cfg::gtile_floats;     // [DP][SLD] + [KP]: the group accumulator
+  const float* U = parity ? q.U_tmp : q.U_io;
+  const int d = q.d, K = q.K, dk = q.dk, L = q.L;
+  const int64_t N = q.N, R = q.rb_total;
+  const int ngrp = (L + kLeafGroup - 1) / kLeafGroup;
+  const int gq0 = (int)blockIdx.x * q.m, gq1 = gq0 + q.m < ngrp ? gq0 + q.m : ngrp;
+  const int lf0 = gq0 * kLeafGroup, lf1 = gq1 * kLeafGroup < L ? gq1 * kLeafGroup : L;
+  const float* A = q.A;
+  const float* C = q.C;
+  // leaf bounds in row blocks (uniform), evaluated once per leaf
+  auto leaf_rb0 = [&](int lf) -> int64_t { return (int64_t)lf * R / L; };
+
+  float4 pa[PFN], pc[PFN];
+  uint32_t okm = 0;
+  auto load_tile = [&](int64_t rb0, int64_t rb1, int t) {   // = partial_core's load_tile (fp32)
+    const int64_t r0 = (rb0 + (int64_t)t * RB) * 16;
+    const int64_t rmax = rb1 * 16 < N ? rb1 * 16 : N;
+    const float* Ab = A + r0 * d;
+    const float* Cb = C + r0 * d;
 #pragma unroll
-    for (int j = 0; j < kReduceBatch; ++j) {
-      const int p = p0 + 4 * j;
-      v[j] = partials[(size_t)(p < P ? p : grp) * ES + e];
+    for (int p = 0; p < PFN; ++p) {
+      const int i = tid + p * NT;
+      const int row = (i / (DP / 4)) % RT, col = 4 * (i % (DP / 4));
+      const bool ok = i < NV && r0 + row < rmax && col < d;
+      const unsigned off = ok ? (unsigned)(row * d + col) : 0u;
+      float4 a, c;
+      if constexpr (VEC) {
+        a = *reinterpret_cast<const float4*>(Ab + off);
+        c = *reinterpret_cast<const float4*>(Cb + off);
+      } else {
+        float va[4], vc[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const unsigned o = (ok && col + u < d) ? off + u : 0u;
+          const float xa = Ab[o], xc = Cb[o];
+          va[u] = keep_or_zero(xa, col + u < d);
+          vc[u] = keep_or_zero(xc, col + u < d);
+        }
+        a = make_float4(va[0], va[1], va[2], va[3]);
+        c = make_float4(vc[0], vc[1], vc[2], vc[3]);
+      }
+      pa[p] = a;
+      pc[p] = c;
+      okm = (okm & ~(1u << p)) | ((ok ? 1u : 0u) << p);
     }
+  };
+  auto store_tile = [&]() {
 #pragma unroll
-    for (int j = 0; j < kReduceBatch; ++j)
-      if (p0 + 4 * j < P) acc += v[j];
+    for (int p = 0; p < PFN; ++p) {
+      const int i = tid + p * NT;
+      if (i < NV) {
+        const int row = i / (DP / 4), col = 4 * (i % (DP / 4));
+        const bool ok = (okm >> p) & 1u;
+        *reinterpret_cast<float4*>(As + row * LDA + col) = keep_or_zero4(pa[p], ok);
+        *reinterpret_cast<float4*>(Cs + row * LDA + col) = keep_or_zero4(pc[p], ok);
+      }
+    }
+  };
+  if (lf0 >= lf1) return;                 // (no such workgroup: G = ceil(groups / m))
+  int64_t c0 = leaf_rb0(lf0), c1 = leaf_rb0(lf0 + 1);           // current leaf
+  int64_t n1 = lf0 + 1 < lf1 ? leaf_rb0(lf0 + 2) : c1;            // end of the next leaf
+  load_tile(c0, c1, 0);
+  // group accumulator = +0
+  for (int e = tid; e < DP * SLD + KP; e += NT) S[e] = 0.f;
+
+  float ureg[NCB][NQ][4];
+  u16x8 ubf[1][1];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) {
+    const int jp = 16 * (cg * NCB + cb) + l15;
+    const int kc = jp / DKP, l = jp % DKP;
+    const bool real = kc < K && l < dk;
+    const int j = real ? kc * dk + l : 0;
+#pragma unroll
+    for (int qq = 0; qq < NQ; ++qq)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int k = 16 * qq + 4 * lg + t;
+        const float v = U[(size_t)(k < d ? k : 0) * d + j];
+        ureg[cb][qq][t] = keep_or_zero(v, real && k < d);
+      }
   }
-  return acc;
+  f32x4 g[NIB][NCB];
+  float sacc[NCB];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int ib = 0; ib < NIB; ++ib)
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) g[ib][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) sacc[cb] = 0.f;
+  };
+  zero_acc();
+  const int nq_live = (d + 15) / 16;
+  store_tile();
+  __syncthreads();
+  int lf = lf0, t = 0, nt = (int)((c1 - c0 + RB - 1) / RB);
+  for (;;) {
+    // the next tile: this leaf's next one, else the next leaf's first
+    const bool more_in_leaf = t + 1 < nt;
+    const bool has_next = more_in_leaf || lf + 1 < lf1;
+    if (has_next) {
+      const int64_t la = more_in_leaf ? c0 : c1, lb = more_in_leaf ? c1 : n1;
+      load_tile(la, lb, more_in_leaf ? t + 1 : 0);
+    }
+    const int64_t rbt = c0 + (int64_t)t * RB;
+    const int nrb = (int)((c1 - rbt) < RB ? (c1 - rbt) : RB);
+    for (int rbl = w / CG; rbl < nrb; rbl += WPG)
+      rowblock_step<DP, DKP, 0>(As + 16 * rbl * LDA, Cs + 16 * rbl * LDA, ureg, ubf, g, sacc, nq_live, l15, lg);
+    __syncthreads();                      // tile reads done
+    if (!more_in_leaf) {
+      // leaf slab = ((0 + Gt_cg) + Gt_{cg + CG}) + ... (drsa_partial_kernel's wave order), S += slab.
+      // LDS element offsets from one opaque per-lane base + compile-time constants (ds offset field):
+      // otherwise the 64 loop-invariant addresses are hoisted out of the leaf loop and spill.
+      constexpr int GE = NIB * NCB * 4;                  // Gt registers per lane
+      if (w >= CG) {
+        uint32_t ro = (uint32_t)((w - CG) * GE * 64 + lane);
+        asm volatile("" : "+v"(ro));
+#pragma unroll
+        for (int ib = 0; ib < NIB; ++ib)
+#pragma unroll
+          for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) red[ro + ((ib * NCB + cb) * 4 + r) * 64] = g[ib][cb][r];
+      }
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) sred[(w * 64 + lane) * NCB + cb] = sacc[cb];
+      __syncthreads();
+      if (w < CG) {
+        uint32_t ro = (uint32_t)(w * GE * 64 + lane);    // partner w + CG's element (ib, cb, r) = 0
+        uint32_t so = (uint32_t)(4 * lg * SLD + w * CW + l15);
+        asm volatile("" : "+v"(ro), "+v"(so));
+#pragma unroll
+        for (int ib = 0; ib < NIB; ++ib)
+#pragma unroll
+          for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float acc = 0.f + g[ib][cb][r];
+#pragma unroll
+              for (int k = 1; k < WPG; ++k)      // partners w + CG, w + 2 CG, ... in order
+                acc += red[ro + (k - 1) * CG * GE * 64 + ((ib * NCB + cb) * 4 + r) * 64];
+              float* sp = S + so + (16 * ib + r) * SLD + 16 * cb;
+              *sp = *sp + acc;
+            }
+      }
+      for (int k = tid; k < KP; k += NT) {
+        const int j0 = k * DKP, gcg = j0 / CW, cb = (j0 % CW) / 16, lo = DKP < 16 ? j0 % 16 : 0;
+        float acc = 0.f;
+        for (int ww = gcg; ww < NW; ww += CG)
+          for (int qq = 0; qq < 4; ++qq) acc += sred[(ww * 64 + 16 * qq + lo) * NCB + cb];
+        S[DP * SLD + k] = S[DP * SLD + k] + acc;
+      }
+      zero_acc();
+      __syncthreads();                    // red / sred reads and the S updates done
+      if ((lf + 1) % kLeafGroup == 0 || lf + 1 == lf1) {
+        // the group is complete: its slab, then a fresh accumulator
+        float* slab = q.partials + (size_t)(lf / kLeafGroup) * ES;
+        for (int e = tid; e < DP * DP; e += NT) {
+          const int i = e / DP, j = e % DP;
+          slab[e] = S[i * SLD + j];
+          S[i * SLD + j] = 0.f;
+        }
+        for (int k = tid; k < KP; k += NT) {
+          slab[DP * DP + k] = S[DP * SLD + k];
+          S[DP * SLD + k] = 0.f;
+        }
+        // (the next fold into S comes two barriers later)
+      }
+    }
+    if (!has_next) break;
+    if (more_in_leaf) {
+      ++t;
+    } else {
+      ++lf;
+      t = 0;
+      c0 = c1;
+      c1 = n1;
+      n1 = lf + 1 < lf1 ? leaf_rb0(lf + 2) : c1;
+      nt = (int)((c1 - c0 + RB - 1) / RB);
+    }
+    store_tile();
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// reduce: out[e] = the left fold over leaf groups q (ascending) of G_q[e], G_q[e] = the left fold
+// over the group's slabs (at most LG of them, ascending), both from +0 -- the kLeaves partition's
+// fixed order (deterministic, no atomics).  LG = kLeafGroup for per-leaf slabs (drsa_partial_kernel,
+// the fused step), 1 for the grouped kernel's per-group slabs: the same additions either way.
+// Thread group grp of a block computes G_q for q = grp, grp + 4, ... with every slab load of its
+// groups issued before the adds (the slabs were just written by every CU: one memory round trip per
+// batch of loads), then one thread per element folds the G_q in order.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void reduce_grouped(const float* __restrict__ partials, int P, int LG, int ES, int E,
+                                               float* __restrict__ out) {
+  __shared__ float part[kMaxGroups][64];
+  const int l = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + l;
+  const int ng = (P + LG - 1) / LG;
+  const int ec = e < E ? e : 0;
+#pragma unroll
+  for (int q0 = 0; q0 < kMaxGroups; q0 += 4) {
+    const int qq = q0 + grp;
+    if (q0 >= ng) break;                  // uniform
+    float v[kLeafGroup];
+#pragma unroll
+    for (int i = 0; i < kLeafGroup; ++i) {
+      const int p = qq * LG + i;
+      const bool ok = i < LG && qq < ng && p < P;
+      v[i] = partials[(size_t)(ok ? p : 0) * ES + ec];
+    }
+    float G = 0.f;
+#pragma unroll
+    for (int i = 0; i < kLeafGroup; ++i)
+      if (i < LG && qq * LG + i < P) G += v[i];
+    if (qq < ng) part[qq][l] = G;
+  }
+  __syncthreads();
+  if (grp == 0 && e < E) {
+    float T = 0.f;
+    for (int qq = 0; qq < ng; ++qq) T += part[qq][l];
+    out[e] = T;
+  }
 }
 
 __global__ __launch_bounds__(256) void drsa_reduce_kernel(const float* __restrict__ partials, int P, int E, int ES,
                                                           float* __restrict__ out) {
-  __shared__ float part[4][64];
-  const int l = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int e = blockIdx.x * 64 + l;
-  const float acc = e < E ? reduce_chain(partials, P, ES, e, grp) : 0.f;
-  part[grp][l] = acc;
-  __syncthreads();
-  if (grp == 0 && e < E) out[e] = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
+  reduce_grouped(partials, P, kLeafGroup, ES, E, out);
 }
 
 // the polar runs at PD = max(32, DP) (32x32 MFMA tiles; a d <= 16 problem is embedded once more)
@@ -596,46 +868,28 @@ __global__ __launch_bounds__(fin_threads<polar_dim<DP>()>()) void drsa_finish_ke
 // ---------------------------------------------------------------------------
 // batched independent problems (task-parallel DRSA grid, optsubspaces.py:17-23): one launch per
 // phase for every problem of a batch that shares the padded geometry.  Problem p's partial runs
-// on G workgroups (blockIdx.y = p, each a contiguous run of its row blocks), its reduce on
-// blockIdx.y = p, its finish on workgroup p.  U ping-pongs between U_io and U_tmp by step parity.
+// on G workgroups (blockIdx.y = p; drsa_partial_grouped_kernel, whole leaf groups each), its reduce
+// on blockIdx.y = p, its finish on workgroup p.  U ping-pongs between U_io and U_tmp by step parity.
 // ---------------------------------------------------------------------------
-struct BatchDesc {
-  const float* A;
-  const float* C;
-  int64_t N;
-  int64_t rb_total;
-  int d, K, dk, DKP;
-  int G;                // partial workgroups of this problem (<= gridDim.x)
-  float* U_io;
-  float* U_tmp;
-  float* f_traj;
-  int* counter;
-  float* partials;
-  float* gs;
-};
 
+// the per-leaf form for geometries whose grouped kernel does not fit the register file (concept
+// width 64): workgroup l of problem p computes leaf l exactly as drsa_partial_kernel does
 template <int DP, int DKP, bool VEC>
-__global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_batched_kernel(
+__global__ __launch_bounds__((partial_threads<DP, DKP>())) void drsa_partial_leaf_batched_kernel(
     const BatchDesc* __restrict__ bd, int parity) {
   const BatchDesc& q = bd[blockIdx.y];
-  if ((int)blockIdx.x >= q.G) return;    // uniform per workgroup: before any barrier
+  if ((int)blockIdx.x >= q.L) return;    // uniform per workgroup: before any barrier
   const float* U = parity ? q.U_tmp : q.U_io;
   const int d = q.d;
   partial_core<DP, DKP, 0, VEC>(
       q.A, q.C, q.N, d, q.K, q.dk, q.partials, q.rb_total, [] {},
-      [&](int k, int j, int) { return U[(size_t)k * d + j]; }, [] {}, q.G);
+      [&](int k, int j, int) { return U[(size_t)k * d + j]; }, [] {}, q.L);
 }
 
 __global__ __launch_bounds__(256) void drsa_reduce_batched_kernel(const BatchDesc* __restrict__ bd, int E, int ES) {
-  __shared__ float part[4][64];
   const BatchDesc& q = bd[blockIdx.y];
-  const int G = q.G;
-  const int l = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int e = blockIdx.x * 64 + l;
-  const float acc = e < E ? reduce_chain(q.partials, G, ES, e, grp) : 0.f;
-  part[grp][l] = acc;
-  __syncthreads();
-  if (grp == 0 && e < E) q.gs[e] = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
+  if (q.m > 0) reduce_grouped(q.partials, (q.L + kLeafGroup - 1) / kLeafGroup, 1, ES, E, q.gs);
+  else reduce_grouped(q.partials, q.L, kLeafGroup, ES, E, q.gs);
 }
 
 // mode 0: U_in -> U_out = polar(U_in + G c), f(U_in) -> f_traj[counter++]; mode 1: f only
@@ -730,10 +984,7 @@ struct PartialPlan {
 
 PartialPlan plan_partial(int64_t N) {
   const int64_t rbt = (N + 15) / 16;
-  int64_t grid = drsa::cu_count();   // one workgroup per CU; rows are split in 16-row blocks
-  // tuning knob (experiments): at most this many workgroups (fewer slabs for the reduce)
-  static const int gmax = getenv("DRSA_AMD_PARTIAL_GRID") ? atoi(getenv("DRSA_AMD_PARTIAL_GRID")) : 0;
-  if (gmax > 0 && grid > gmax) grid = gmax;
+  int64_t grid = kLeaves;            // one workgroup per leaf (= per CU on MI355X); 16-row blocks
   if (grid > rbt) grid = rbt;
   if (grid < 1) grid = 1;
   return {(int)grid, rbt};
@@ -1244,23 +1495,30 @@ int drsa_amd_drsa_run_batched(int P, const drsa_amd_problem_t* probs, int steps,
     DRSA_REQUIRE(!(hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone),
                  "drsa_run_batched: not capturable (allocates its descriptor table); use drsa_run_multi");
   }
+  // workgroups per problem: `blocks`, or about 16 waves of one-workgroup-per-CU launches over the
+  // chip (the 90-problem grid: one leaf group per workgroup, 36.4k problem-steps/s against 36.0k
+  // at two groups); each owns m = ceil(groups / G) whole leaf groups (the result does not depend on it)
   const int cu = drsa::cu_count();
-  int G = blocks > 0 ? blocks : (4 * cu + P - 1) / P;
-  if (G > cu) G = cu;                         // the workspace holds cu_count slabs per problem
-  if (G < 1) G = 1;
+  int Greq = blocks > 0 ? blocks : (16 * cu + P - 1) / P;
+  if (Greq < 1) Greq = 1;
   (void)min_rbt;
   const Geom& g = g0;
   const size_t E = slab_floats(g), ES = slab_stride(g);
+  int G = 1;
+  const bool leafwise = g0.DKp >= 64;          // see drsa_partial_leaf_batched_kernel
   // descriptor table on the device
   BatchDesc* hd = (BatchDesc*)malloc(sizeof(BatchDesc) * (size_t)P);
   DRSA_REQUIRE(hd, "drsa_run_batched: host allocation failed");
   for (int p = 0; p < P; ++p) {
     const drsa_amd_problem_t& q = probs[p];
     const Geom gq = geom(q.d, q.K);
-    const int64_t rbt = (q.N + 15) / 16;
-    const int Gp = (int)(G < rbt ? G : rbt);   // as plan_partial: never more workgroups than row blocks
-    hd[p] = BatchDesc{q.A, q.C, q.N, rbt, q.d, q.K, q.d / q.K, gq.DKp, Gp, q.U_io, q.U_tmp, q.f_traj, q.counter,
-                      (float*)q.ws, ws_gs(q.ws, q.N, gq)};
+    const PartialPlan pl = plan_partial(q.N);   // the leaves of drsa_run's partition
+    const int ngrp = (pl.grid + kLeafGroup - 1) / kLeafGroup;
+    const int m = leafwise ? 0 : (ngrp + Greq - 1) / Greq;
+    const int Gp = leafwise ? pl.grid : (ngrp + m - 1) / m;
+    if (Gp > G) G = Gp;
+    hd[p] = BatchDesc{q.A, q.C, q.N, pl.rb_total, q.d, q.K, q.d / q.K, gq.DKp, Gp, pl.grid, m, q.U_io, q.U_tmp,
+                      q.f_traj, q.counter, (float*)q.ws, ws_gs(q.ws, q.N, gq)};
   }
   BatchDesc* dd = nullptr;
   hipError_t e = hipMalloc((void**)&dd, sizeof(BatchDesc) * (size_t)P);
@@ -1281,9 +1539,15 @@ int drsa_amd_drsa_run_batched(int P, const drsa_amd_problem_t* probs, int steps,
       auto part = [&](auto dpt, auto dkt) -> int {
         constexpr int DP = decltype(dpt)::value, DKP = decltype(dkt)::value;
         using Cfg = PCfg<DP, DKP>;
-        auto kern = vec ? drsa_partial_batched_kernel<DP, DKP, true> : drsa_partial_batched_kernel<DP, DKP, false>;
-        DRSA_SMEM(kern, Cfg::lds_bytes);
-        hipLaunchKernelGGL(kern, dim3(G, P), dim3(Cfg::NT), Cfg::lds_bytes, s, dd, parity);
+        if constexpr (DKP >= 64) {     // = leafwise
+          auto kern = vec ? drsa_partial_leaf_batched_kernel<DP, DKP, true> : drsa_partial_leaf_batched_kernel<DP, DKP, false>;
+          DRSA_SMEM(kern, Cfg::lds_bytes);
+          hipLaunchKernelGGL(kern, dim3(G, P), dim3(Cfg::NT), Cfg::lds_bytes, s, dd, parity);
+        } else {
+          auto kern = vec ? drsa_partial_grouped_kernel<DP, DKP, true> : drsa_partial_grouped_kernel<DP, DKP, false>;
+          DRSA_SMEM(kern, Cfg::glds_bytes);
+          hipLaunchKernelGGL(kern, dim3(G, P), dim3(Cfg::NT), Cfg::glds_bytes, s, dd, parity);
+        }
         DRSA_LAUNCH_CHECK();
         return DRSA_OK;
       };

@@ -88,11 +88,11 @@ def hip_runner(problems, steps: int):
     fp32 = all(A.dtype == torch.float32 for A, _, _, _ in problems)
     with torch.cuda.stream(side):
         if len(geoms) == 1 and fp32:
-            # one partial workgroup per CU for every problem: the row partition (and so the fp32
-            # summation order) is drsa_run's, independent of how many tasks share the launch, the
-            # world size or the LPT plan -- grid results equal drsa.main's bit for bit
-            cu = torch.cuda.get_device_properties(dev).multi_processor_count
-            out = drsa_run_batched(problems, steps, blocks=cu)
+            # the batched partial folds whole groups of drsa_run's fixed 256-leaf row partition
+            # per workgroup, so the fp32 summation order is drsa_run's whatever the workgroup
+            # count, the tasks sharing the launch, the world size or the LPT plan: grid results
+            # equal drsa.main's bit for bit
+            out = drsa_run_batched(problems, steps)
         else:
             out = drsa_run_joint(problems, steps)
     torch.cuda.current_stream(dev).wait_stream(side)

@@ -175,8 +175,9 @@ def drsa_run_batched(problems, steps: int, blocks: int = 0, use_graph: bool = Tr
     """Many independent fp32 DRSA problems of one padded geometry (e.g. the reference's task grid:
     GTZAN classes x layers 19 / 26 / 33 x runs, d = 100 / 128 -> padded 128, concept width 32)
     advanced with one launch per phase for all of them (drsa_amd_drsa_run_batched).  ``blocks``:
-    partial workgroups per problem (0 = automatic); the row partition sets the fp32 summation
-    order.  Returns [(U_S, trajectory [S+1])]."""
+    about this many partial workgroups per problem (0 = automatic), each folding whole groups of
+    drsa_run's fixed 256-leaf row partition on chip: every result equals drsa_run's bit for bit,
+    for any ``blocks``.  Returns [(U_S, trajectory [S+1])]."""
     import ctypes
     if not problems:
         return []

@@ -341,11 +341,12 @@ int drsa_amd_drsa_run_multi(int P, const drsa_amd_problem_t* probs, int steps, i
 
 /* P independent fp32 problems sharing one padded geometry (same pow2(d) and concept width; N may
  * differ) advanced together with ONE launch per phase for all of them: every problem's partial
- * on `blocks` workgroups (0: about four waves of workgroups over the chip), the slab reduces, then
+ * on about `blocks` workgroups (0: about sixteen waves of workgroups over the chip), each owning whole
+ * groups of the fixed 256-leaf row partition that drsa_amd_drsa_run uses, the slab reduces, then
  * every problem's finish on its own workgroup.  The task-parallel DRSA grid of the reference's
  * cluster driver (optsubspaces.py:17-23: classes x layers x runs, each drsa.main(..., steps=5000)).
- * Fields of probs mean what they mean for drsa_amd_drsa_run_multi (dtype must be 0).  The
- * result depends on `blocks` through the fp32 summation order of the row partition.  Not stream-
+ * Fields of probs mean what they mean for drsa_amd_drsa_run_multi (dtype must be 0).  Every
+ * problem's trajectory and U equal drsa_amd_drsa_run's bit for bit, for any `blocks`.  Not stream-
  * capturable (it allocates its descriptor table); synchronises the stream before returning. */
 int drsa_amd_drsa_run_batched(int P, const drsa_amd_problem_t* probs, int steps, int blocks, int use_graph,
                               void* stream);

@@ -1,13 +1,14 @@
 """Task-parallel DRSA grid (xai/drsa/cluster/optsubspaces.py) on one GPU.
 
-* drsa_run_batched (one launch per phase for every problem of a padded geometry) with one
-  partial workgroup per CU per problem -- drsa_run's own row partition -- equals each problem run
-  alone with drsa_run (the path drsa.main takes) bit for bit;
-* with the automatic partition (fewer, longer workgroups per problem) the trajectories agree
-  with drsa_run to fp32 summation order (1e-5 relative), and with the reference's own run of
-  the d = 100 layer-19 shape over 500 steps to 1e-4 (tests/golden/drsa_long_fixture.npz);
+* drsa_run_batched (one launch per phase for every problem of a padded geometry; each partial
+  workgroup folds whole groups of drsa_run's fixed 256-leaf row partition on chip) equals each
+  problem run alone with drsa_run (the path drsa.main takes) bit for bit, for any number of
+  workgroups per problem (automatic, 1, 3, 32, 256) and for every concept width (the grouped
+  kernel; the per-leaf form at width 64);
+* the batched d = 100 layer-19 shape agrees with the reference's own 500-step run to 1e-4
+  (tests/golden/drsa_long_fixture.npz);
 * optimize_grid writes drsa.main's files for every (class, layer, run), with results equal to
-  drsa_run's bit for bit (it passes the per-CU partition, whatever the task count per launch)."""
+  drsa_run's bit for bit, whatever the task count per launch."""
 import os
 import pickle
 
@@ -30,9 +31,8 @@ def _data():
     return data
 
 
-def test_batched_equals_drsa_run_at_cu_partition():
+def test_batched_equals_drsa_run_any_partition():
     from drsa_audio_amd.xai.drsa.drsa import drsa_run, drsa_run_batched, initial_projections
-    cu = torch.cuda.get_device_properties(0).multi_processor_count
     data = _data()
     for geom_layers in ((19, 26), (7,)):
         probs = []
@@ -43,14 +43,36 @@ def test_batched_equals_drsa_run_at_cu_partition():
                                                                      device=DEV), 4))
         steps = 7
         s = torch.cuda.Stream(DEV)
+        runs = {}
         with torch.cuda.stream(s):
-            exact = drsa_run_batched(probs, steps, blocks=cu)
-            auto = drsa_run_batched(probs, steps)
+            for blocks in (0, 1, 3, 32, 256):
+                runs[blocks] = drsa_run_batched(probs, steps, blocks=blocks)
         torch.cuda.synchronize()
-        for (A, C, U0, K), (Ue, te), (Ua, ta) in zip(probs, exact, auto):
+        for i, (A, C, U0, K) in enumerate(probs):
             U, t = drsa_run(A, C, U0, K, steps)
-            assert np.array_equal(te.cpu().numpy(), t.cpu().numpy()) and torch.equal(Ue, U)
-            np.testing.assert_allclose(ta.cpu().numpy(), t.cpu().numpy(), rtol=1e-5, atol=0)
+            for blocks, out in runs.items():
+                Ub, tb = out[i]
+                assert np.array_equal(tb.cpu().numpy(), t.cpu().numpy()), (blocks, i)
+                assert torch.equal(Ub, U), (blocks, i)
+
+
+@pytest.mark.parametrize("d,K,N", [(128, 2, 5000), (64, 1, 3001), (128, 16, 4099), (100, 4, 100), (32, 4, 20000)])
+def test_batched_equals_drsa_run_geometries(d, K, N):
+    """Every padded geometry of the batched path: concept width 64 (the per-leaf form), 8, 32, a
+    problem with fewer row blocks than leaves, many rows per leaf."""
+    from drsa_audio_amd.xai.drsa.drsa import drsa_run, drsa_run_batched
+    probs = []
+    for j in range(3):
+        A, C = drsa_inputs(N + 17 * j, d, 500 + j)
+        U0 = np.linalg.qr(np.random.default_rng(j).standard_normal((d, d)))[0].astype(np.float32)
+        probs.append(tuple(torch.from_numpy(v).to(DEV) for v in (A, C, U0)) + (K,))
+    s = torch.cuda.Stream(DEV)
+    with torch.cuda.stream(s):
+        out = drsa_run_batched(probs, 5, blocks=2)
+    torch.cuda.synchronize()
+    for (A, C, U0, K_), (Ub, tb) in zip(probs, out):
+        U, t = drsa_run(A, C, U0, K_, 5)
+        assert np.array_equal(tb.cpu().numpy(), t.cpu().numpy()) and torch.equal(Ub, U)
 
 
 def test_batched_long_d100_vs_reference(golden_dir):
