@@ -484,6 +484,81 @@ def drsa_sharded_bench(device, world, rank, steps=100):
     return out
 
 
+def drsa_pipeline_bench(device, world, rank, model, samples_per_rank=1000, steps=100, num_locations=20, K=8):
+    """C4's rank-local chain (the reference: getdrsadata.py:119-137 preprocess_data
+    -> :47-59 load_and_normalize_data -> drsa.main): every rank extracts DRSA rows from ITS slice of a
+    seeded synthetic log-mel batch (drsa_training_data(group=): forward + LRP backward to j = 7, the
+    locations drawn from the global numpy stream, normalisation over all ranks' rows), then
+    main_sharded(local_rows=True) optimises K = 8 subspaces over the row shards (one all-reduce per
+    step).  No rank holds the whole set.  Weak scaling: samples_per_rank x num_locations rows per rank
+    (1000 x 20 = 20 000; 160 000 = C4's N at 8 ranks).  Rank 0 then rebuilds the whole batch, runs
+    the single-process chain (drsa_training_data + drsa_run) and reports the trajectory deviation."""
+    import tempfile
+    import pandas as pd
+    import torch.distributed as dist
+    from drsa_audio_amd.utils.constants import LRP_NAME_MAP_GTZAN
+    from drsa_audio_amd.zennit.composites import NameMapComposite
+    from drsa_audio_amd.xai.drsa.preprocessing import drsa_training_data
+    from drsa_audio_amd.xai.drsa.distributed import main_sharded
+    comp = NameMapComposite(LRP_NAME_MAP_GTZAN)
+    group = dist.group.WORLD if world > 1 else None
+    x = synthetic_logmel(samples_per_rank, seed=300 + rank, device=device)
+
+    def barrier():
+        torch.cuda.synchronize(device)
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(v):
+        if world == 1:
+            return v
+        t = torch.tensor([v], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t)
+
+    np.random.seed(7)
+    drsa_training_data(model, x[:8], comp, 7, 3, num_locations=num_locations, group=group)   # plan build / warm-up
+    barrier()
+    np.random.seed(7)
+    t0 = time.perf_counter()
+    A, C = drsa_training_data(model, x, comp, 7, 3, num_locations=num_locations, group=group)
+    barrier()
+    t_ext = max_over_ranks(time.perf_counter() - t0)
+    with tempfile.TemporaryDirectory() as root:
+        main_sharded(A, C, root, num_concepts=K, steps=3, runs=1, local_rows=True, group=group)   # warm-up
+        barrier()
+        t0 = time.perf_counter()
+        main_sharded(A, C, root, num_concepts=K, steps=steps, runs=1, local_rows=True, group=group)
+        barrier()
+        t_opt = max_over_ranks(time.perf_counter() - t0)
+        traj = None
+        if rank == 0:
+            traj = pd.read_csv(os.path.join(root, "run1", "train_stats.csv"))["loss"].to_numpy(np.float64)
+    rows = A.size(0) * world
+    out = {"config": f"rank-local C4 chain: {samples_per_rank} samples/rank x {world} rank(s), j=7 (d=64), "
+                     f"{num_locations} locations/sample, K={K}: drsa_training_data(group=) -> "
+                     f"main_sharded(local_rows=True), {steps} steps, 1 run",
+           "scaling": "weak", "rows_total": rows,
+           "extraction_rows_per_s": rows / t_ext, "extraction_s": t_ext,
+           "optimisation_steps_per_s": steps / t_opt, "optimisation_vector_steps_per_s": rows * steps / t_opt}
+    del A, C
+    if rank == 0:
+        from drsa_audio_amd.xai.drsa.drsa import drsa_run, initial_projections
+        xa = torch.cat([synthetic_logmel(samples_per_rank, seed=300 + r, device=device) for r in range(world)])
+        np.random.seed(7)
+        A1, C1 = drsa_training_data(model, xa, comp, 7, 3, num_locations=num_locations)
+        del xa
+        U0 = torch.tensor(np.ascontiguousarray(initial_projections(A1.size(1), 1, 42)[0]), dtype=torch.float32,
+                          device=device)
+        _, t1 = drsa_run(A1, C1, U0, K, steps)
+        t1 = t1.cpu().numpy().astype(np.float64)
+        out["traj_dev_vs_unsharded"] = float(np.max(np.abs(traj - t1) / np.abs(t1)))
+        del A1, C1
+    if world > 1:
+        dist.barrier()
+    return out
+
+
 def drsa_grid_bench(device, world, rank, steps=100, N=20000, classes=None):
     """Task-parallel DRSA over the reference's problem grid (optsubspaces.py:17-23): 10 classes x
     layers [19 (d=100), 26 (d=128), 33 (d=128)] x 3 runs = 90 independent problems, K=4, N rows
@@ -536,7 +611,7 @@ def drsa_grid_bench(device, world, rank, steps=100, N=20000, classes=None):
 
 
 # --------------------------------------------------------------------------- main
-LEGS = ("c2", "drsa", "frontend", "joint", "vggish", "sharded", "grid", "to_host", "clone")
+LEGS = ("c2", "drsa", "frontend", "joint", "vggish", "sharded", "pipeline", "grid", "to_host", "clone")
 
 
 def main():
@@ -551,6 +626,8 @@ def main():
                     help="write the per-step kernel tag order (JSON) for scripts/tag_profile.py")
     ap.add_argument("--grid-steps", type=int, default=100, help="steps of the task-parallel DRSA grid leg")
     ap.add_argument("--grid-classes", type=int, default=10, help="classes of the DRSA grid (10 = the reference's)")
+    ap.add_argument("--pipeline-samples", type=int, default=1000, help="samples per rank of the rank-local C4 leg")
+    ap.add_argument("--pipeline-steps", type=int, default=100, help="DRSA steps of the rank-local C4 leg")
     ap.add_argument("--legs", default="all",
                     help="secondary legs to run: all, or a comma list of " + ",".join(LEGS))
     args = ap.parse_args()
@@ -558,7 +635,7 @@ def main():
     if not legs <= set(LEGS):
         ap.error(f"--legs: unknown {sorted(legs - set(LEGS))}")
     if args.no_drsa:
-        legs -= {"drsa", "joint", "vggish", "sharded", "grid"}
+        legs -= {"drsa", "joint", "vggish", "sharded", "pipeline", "grid"}
 
     # rehearsal of the N > 1 path on a one-GPU box (tests only): every rank on cuda:0, usually gloo
     one_dev = os.environ.get("DRSA_BENCH_ONE_DEVICE") == "1"
@@ -687,9 +764,13 @@ def main():
     frontend = frontend_bench(device) if (rank == 0 and "frontend" in legs) else None
     joint = drsa_joint_bench(device) if (rank == 0 and "joint" in legs) else None
     vgg = vggish_lrp_bench(device) if (rank == 0 and "vggish" in legs) else None
-    drsa_sharded = grid = None
+    drsa_sharded = grid = pipeline = None
     if "sharded" in legs and world > 1:
         drsa_sharded = drsa_sharded_bench(device, world, rank)
+    if "pipeline" in legs:
+        log("[bench] rank-local DRSA pipeline (C4 chain)")
+        pipeline = drsa_pipeline_bench(device, world, rank, model, samples_per_rank=args.pipeline_samples,
+                                       steps=args.pipeline_steps)
     if "grid" in legs:
         log("[bench] task-parallel DRSA grid")
         from drsa_audio_amd.xai.drsa.cluster.optsubspaces import GTZAN_CLASSES
@@ -775,7 +856,8 @@ def main():
             "kernels": kernels,
             "secondary": {"standard_lrp_c2_bs64_samples_per_s": c2 and c2 * world,
                           "explained_samples_per_s_bs64": bs64 and bs64 * world, "drsa": drsa,
-                          "drsa_sharded": drsa_sharded, "drsa_joint_c5": joint, "vggish_lrp": vgg,
+                          "drsa_sharded": drsa_sharded, "drsa_rank_local_pipeline": pipeline,
+                          "drsa_joint_c5": joint, "vggish_lrp": vgg,
                           "drsa_grid_task_parallel": grid, "logmel_frontend": frontend, "to_host": to_host,
                           "clone_mode": clone_mode,
                           "cpu_baseline_drsa_c3": cpu_drsa},

@@ -28,6 +28,8 @@ namespace drsa_conv {
 static const Entry kTableBwdA_e[] = {
     BWD_SET64(128, 16),
     BWD_SET64(64, DRSA_CONV_CIC_BWD64_T8),
+    // the (2,4) pool backward folded into the staging (VGGish block 1 at W = 256: 8 x 16 tiles)
+    CONV_ENTRY_P4B(64, 64, 8, 16, 8, DRSA_CONV_CIC_BWD64),
 };
 extern const Table kTableBwdA = {kTableBwdA_e, (int)(sizeof(kTableBwdA_e) / sizeof(kTableBwdA_e[0]))};
 }  // namespace drsa_conv

@@ -47,8 +47,11 @@ const Entry* find(int cin_p, int cout_p, int W, int ng, int amode, int epi, int 
   // chunks spills 91-115 VGPRs at 3 waves/SIMD, the 8 x 16 one none
   static const int bwd64_t16 = env_int("DRSA_AMD_CONV_BWD64_T16", 1);
   static const int bwd32_t16 = env_int("DRSA_AMD_CONV_BWD32_T16", 0);   // (experiment) the same into 32 channels
+  // fp32 backward into 128 channels at W >= 32 (VGGish features.17, 100 -> 100 at 32 x 32): the 8 x 32
+  // tile holds 128 accumulators and spills 358-435 VGPRs at 3 waves/SIMD, the 8 x 16 one none
   const bool bwd_t16 = epi == EPI_BWD && et == 0 &&
-                       ((bwd64_t16 && cout_p == 64 && cin_p <= 128) || (bwd32_t16 && cout_p == 32 && !th16));
+                       ((bwd64_t16 && cout_p == 64 && cin_p <= 128) || cout_p == 128 ||
+                        (bwd32_t16 && cout_p == 32 && !th16));
   if (W >= 32 && (fwd_t16 || bwd_t16)) { tw = 16; mw = 8; th = 8; }
   else if (W >= 32) { tw = 32; mw = 8; th = (th16 && cout_p == 32 && ng <= 2) ? 16 : 8; }
   else if (W > 8 && !(w16_as8 & (epi == EPI_BWD ? 2 : 1))) { tw = 16; mw = 8; }
@@ -174,6 +177,11 @@ int drsa_amd_conv_bwd_has_kernel_bf16(int cin, int cout, int W, int ng, int spar
   return find(pad32(cin), pad32(cout), W, ng, sparse ? A_POOLSPARSE : A_DENSE, EPI_BWD, 1) != nullptr;
 }
 
+int drsa_amd_conv_bwd_has_kernel_pw(int cin, int cout, int W, int ng, int pool_w) {
+  if (cin < 2 || (pool_w != 2 && pool_w != 4) || (pool_w == 4 && (W / 4) % 4 != 0)) return 0;
+  return find(pad32(cin), pad32(cout), W, ng, A_POOLSPARSE, EPI_BWD, 0, pool_w) != nullptr;
+}
+
 int drsa_amd_conv_bwd_has_kernel_bf16_pw(int cin, int cout, int W, int pool_w) {
   if (cin < 16 || (pool_w != 2 && pool_w != 4)) return 0;
   return find(pad32(cin), pad32(cout), W, 1, A_POOLSPARSE, EPI_BWD, 1, pool_w) != nullptr;
@@ -211,8 +219,10 @@ int drsa_amd_conv_bwd_den_map(const float* g, const uint8_t* g_amax, int pool_w,
   const int et = wts_bf16 ? 1 : 0;
   DRSA_REQUIRE(!et || (ng == 1 && cin >= 16 && ((uintptr_t)wts & 15) == 0),
                "conv_bwd_den_map: bf16 weights need ng == 1, cin >= 16 and 16-byte alignment");
-  DRSA_REQUIRE(et || (ng >= 1 && ng <= 2 && (!g_amax || pool_w == 2)),
-               "conv_bwd_den_map: fp32 weights need ng 1..2 and a 2x2 pool");
+  DRSA_REQUIRE(et || (ng >= 1 && ng <= 2 && (!g_amax || pool_w == 2 || ng == 1)),
+               "conv_bwd_den_map: fp32 weights need ng 1..2 (ng 1 under a 2x4 pool)");
+  DRSA_REQUIRE(!g_amax || pool_w == 2 || (W / 4) % 4 == 0,
+               "conv_bwd_den_map: a 2x4 pool-sparse g needs W / 4 %% 4 == 0 (got W=%d)", W);
   const int pw = g_amax ? pool_w : 2;
   const Entry* e = find(pad32(cin), pad32(cout), W, ng, g_amax ? A_POOLSPARSE : A_DENSE, EPI_BWD, et, pw);
   if (!e) {

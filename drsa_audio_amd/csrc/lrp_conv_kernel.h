@@ -151,8 +151,10 @@ struct ConvCfg {
   static_assert(MT % WM == 0 && NT % WN == 0 && WM * WN <= 4, "wave split");
   static_assert(!BF || (CIC == 16 && (EPI < EPI_BWD ? AMODE == A_DENSE : EPI == EPI_BWD)),
                 "bf16: 16-channel chunks; dense forward, or the per-clone backward (dense or pool-sparse g)");
-  static_assert(PW == 2 || (PW == 4 && (EPI == EPI_FWD_POOL || (EPI == EPI_BWD && ET == 1 && AMODE == A_POOLSPARSE))),
-                "2x4 pool windows: the forward pool epilogue, or the bf16 backward's pool-sparse staging");
+  static_assert(PW == 2 || (PW == 4 && (EPI == EPI_FWD_POOL || (EPI == EPI_BWD && AMODE == A_POOLSPARSE &&
+                                                                  (ET == 1 || TW % 16 == 0)))),
+                "2x4 pool windows: the forward pool epilogue, or the backward's pool-sparse staging (fp32: "
+                "tiles of whole float4 cell groups)");
   // FF: the first layer's w^2 contraction fused into the epilogue.  The pass's R is re-laid as
   // the first layer's unpooled g (argmax pixel of each 2x2 cell) in FCH-channel slices of a pixel
   // image [FCH][2TH][FPS] (pixel column X at X + 4) over the dead staging tile T
@@ -179,7 +181,12 @@ struct Stager {
   // pool-sparse cells: interior rows of TW/8 float4 (4 cells) + the two halo cell columns
   static constexpr int CY = TH / 2 + 2, CX = TW / 2 + 2, Q8 = TW / 8 > 0 ? TW / 8 : 1, SROWS = CIC * CY;
   static constexpr int SI = (SROWS * Q8 + NT_ - 1) / NT_, SH = (SROWS * 2 + NT_ - 1) / NT_;
-  static constexpr int NI = DENSE ? DI : SI, NH = DENSE ? DH : SH;
+  // P4: 2 x 4 cells (VGGish's (2,4) pool folded into the staging): interior rows of TW/16 float4
+  // (4 cells = 16 pixels each) + the two halo cells, which reach 1 pixel into the halo each
+  static constexpr bool P4 = !DENSE && Cfg::PW_ == 4;
+  static constexpr int Q16 = TW / 16 > 0 ? TW / 16 : 1;
+  static constexpr int SI4 = (SROWS * Q16 + NT_ - 1) / NT_;
+  static constexpr int NI = DENSE ? DI : P4 ? SI4 : SI, NH = DENSE ? DH : SH;
   static constexpr int NWV = NG * KCP * (COUT / 4), WIT = (NWV + NT_ - 1) / NT_;
   float4 st_i[NI];
   uint32_t st_ia[DENSE ? 1 : NI];
@@ -194,9 +201,39 @@ struct Stager {
     const bool noload = (a.dbg & 1) != 0;
     // per-sample bases (uniform) + 32-bit per-lane offsets: saddr + voffset loads instead of a
     // 64-bit multiply-add per element (the host keeps one sample's cin x H x W below 2^31)
-    const float* __restrict__ inb = a.in + (size_t)bq * a.cin * (DENSE ? H * W : H2 * W2);
-    const uint8_t* __restrict__ amb = DENSE ? nullptr : a.in_amax + (size_t)bs * a.cin * H2 * W2;
-    if constexpr (DENSE) {
+    const int W4 = W >> 2;
+    const float* __restrict__ inb = a.in + (size_t)bq * a.cin * (DENSE ? H * W : H2 * (P4 ? W4 : W2));
+    const uint8_t* __restrict__ amb = DENSE ? nullptr : a.in_amax + (size_t)bs * a.cin * H2 * (P4 ? W4 : W2);
+    if constexpr (P4) {
+      // host contract: W / 4 % 4 == 0, so every 4-cell group is one aligned float4 / uint32
+      const int qy0 = (ty0 >> 1) - 1, cx0 = tx0 >> 2;
+#pragma unroll
+      for (int it = 0; it < SI4; ++it) {
+        const int i = tid + it * NT_;
+        const int row = i / Q16, q = i % Q16;
+        const int ci = row / CY, ry = row % CY;
+        const int cy = qy0 + ry, cx = cx0 + 4 * q, c = c0 + ci;
+        const bool ok = i < SROWS * Q16 && cy >= 0 && cy < H2 && c < a.cin && cx < W4 && !noload;
+        const int o = ok ? (c * H2 + cy) * W4 + cx : 0;
+        const float4 v = *reinterpret_cast<const float4*>(inb + o);
+        const uint32_t am = *reinterpret_cast<const uint32_t*>(amb + o);
+        st_i[it] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+        st_ia[it] = ok ? am : 0xffffffffu;   // 0xff names no pixel of a 2 x 4 window
+      }
+#pragma unroll
+      for (int it = 0; it < SH; ++it) {
+        const int i = tid + it * NT_;
+        const int row = i >> 1, side = i & 1;
+        const int ci = row / CY, ry = row % CY;
+        const int cy = qy0 + ry, cx = side ? cx0 + TW / 4 : cx0 - 1, c = c0 + ci;
+        const bool ok = i < SROWS * 2 && cy >= 0 && cy < H2 && cx >= 0 && cx < W4 && c < a.cin && !noload;
+        const int o = ok ? (c * H2 + cy) * W4 + cx : 0;
+        const float v = inb[o];
+        const int am = (int)amb[o];
+        st_h[it] = ok ? v : 0.f;
+        st_ha[it] = ok ? am : 0xff;
+      }
+    } else if constexpr (DENSE) {
       if ((W & 3) == 0) {
 #pragma unroll
         for (int it = 0; it < DI; ++it) {
@@ -311,8 +348,41 @@ struct Stager {
     if (ry < CY - 1) *reinterpret_cast<float2*>(d + RS) = make_float2(sb == 2 ? v : 0.f, sb == 3 ? v : 0.f);
   }
 
+  // one 2 x 4 cell -> its 8 pixels: halo rows 2ry-1, 2ry, LDS columns 4rx .. 4rx+3 (halo columns
+  // 4rx-3 .. 4rx; rx = 0 and TW/4 + 1 are the halo cells, whose other columns are row padding)
+  __device__ __forceinline__ static void put_cell4(float* halo, int ci, int ry, int rx, float v, int sb) {
+    float* d = halo + ci * PLANE + (2 * ry - 1) * RS + 4 * rx;
+    if (ry > 0)
+      *reinterpret_cast<float4*>(d) = make_float4(sb == 0 ? v : 0.f, sb == 1 ? v : 0.f, sb == 2 ? v : 0.f, sb == 3 ? v : 0.f);
+    if (ry < CY - 1)
+      *reinterpret_cast<float4*>(d + RS) =
+          make_float4(sb == 4 ? v : 0.f, sb == 5 ? v : 0.f, sb == 6 ? v : 0.f, sb == 7 ? v : 0.f);
+  }
+
   __device__ __forceinline__ void store(float* halo, float* wl, int tid) const {
-    if constexpr (DENSE) {
+    if constexpr (P4) {
+      static_assert(XO == 3, "P4 cells land on 16-byte aligned columns 4 rx");
+#pragma unroll
+      for (int it = 0; it < SI4; ++it) {
+        const int i = tid + it * NT_;
+        if (i < SROWS * Q16) {
+          const int row = i / Q16, q = i % Q16;
+          const int ci = row / CY, ry = row % CY;
+          const float vv[4] = {st_i[it].x, st_i[it].y, st_i[it].z, st_i[it].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            put_cell4(halo, ci, ry, 1 + 4 * q + e, vv[e], (int)((st_ia[it] >> (8 * e)) & 0xffu));
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < SH; ++it) {
+        const int i = tid + it * NT_;
+        if (i < SROWS * 2) {
+          const int row = i >> 1, side = i & 1;
+          put_cell4(halo, row / CY, row % CY, side ? TW / 4 + 1 : 0, st_h[it], st_ha[it]);
+        }
+      }
+    } else if constexpr (DENSE) {
 #pragma unroll
       for (int it = 0; it < DI; ++it) {
         const int i = tid + it * NT_;
@@ -1284,6 +1354,12 @@ struct Entry {
   drsa_conv::Entry{CIN, COUT, TH, TW, MW, CIC, NG, AM, EP,                                                 \
                    drsa_conv::conv3x3_kernel<CIN, COUT, TH, TW, MW, CIC, NG, AM, EP>,                      \
                    drsa_conv::ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AM, EP>::lds_floats * sizeof(float)}
+
+// fp32 per-clone backward with g at (2,4)-pool resolution (VGGish block 1, create_model.py:61)
+#define CONV_ENTRY_P4B(CIN, COUT, TH, TW, MW, CIC)                                                          \
+  drsa_conv::Entry{CIN, COUT, TH, TW, MW, CIC, 1, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD,              \
+                   drsa_conv::conv3x3_kernel<CIN, COUT, TH, TW, MW, CIC, 1, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD, 0, 4>, \
+                   drsa_conv::ConvCfg<CIN, COUT, TH, TW, MW, CIC, 1, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD, 0, 4>::lds_floats * sizeof(float), 0, 4}
 
 #define CONV_ENTRY_BFA(CIN, COUT, TH, TW, MW, NG, AM, EP)                                                 \
   drsa_conv::Entry{CIN, COUT, TH, TW, MW, 16, NG, AM, EP,                                                 \

@@ -712,6 +712,12 @@ class LRPEngine:
                   and _capi.lib().drsa_amd_conv_bwd_has_kernel_bf16_pw(st.cout, st.cin, w, 4)):
                 # the (2,4) pool backward folded into the bf16 backward's staging (no unpooled g)
                 amax_in, pool_w = rec["amax"], 4
+            elif (st.pool and st.pool_k == (2, 4) and st.wts_bwd_bf is None and st.den_kind != "ab" and li > 0
+                  and stop_after != li - 1 and self._post_for(li - 1)[0] == POST_DIV_MAP
+                  and _capi.lib().drsa_amd_conv_bwd_has_kernel_pw(st.cout, st.cin, w, st.ng_bwd, 4)):
+                # the same fold in the fp32 backward (VGGish block 1 above the WSquare layer: the den-map
+                # backward takes the pooled g and its argmax bytes)
+                amax_in, pool_w = rec["amax"], 4
             elif st.pool:
                 ph, pw = st.pool_k
                 gf = self._buf((li, "g_unpool"), (Bq, st.cout, h, w))

@@ -185,6 +185,11 @@ int drsa_amd_conv_bwd_bf16(const float* g, const uint8_t* g_amax, const uint16_t
  * backward is folded into the staging (each halo pixel takes its cell's g where the cell's argmax
  * byte, row * pool_w + col, names it), so no unpooled g is written or read.  ng = 1. */
 int drsa_amd_conv_bwd_has_kernel_bf16_pw(int cin, int cout, int W, int pool_w);
+/* 1 when the fp32 backward (drsa_amd_conv_bwd_den_map with g_amax) has a kernel for g at 2 x pool_w
+ * pool resolution: the (2,4) pool backward folded into the fp32 staging (VGGish block 1; 2 x 4 cells
+ * expanded to their 8 pixels at the LDS store; needs W / 4 % 4 == 0), bit-identical to the unpool
+ * followed by the dense-g backward (the same MFMA operands). */
+int drsa_amd_conv_bwd_has_kernel_pw(int cin, int cout, int W, int ng, int pool_w);
 int drsa_amd_conv_bwd_bf16_pw(const float* g, const uint8_t* g_amax, int pool_w, const uint16_t* wts, const float* x,
                               const float* den, float* out, int Bq, int clones, int cin, int cout, int H, int W,
                               int xmode, int post, float eps, void* stream);

@@ -1,6 +1,7 @@
 """bench.py --gpus N through its own launcher (utils/launch.py) on a one-GPU box: two ranks on
-cuda:0 over gloo run the explanation headline, the row-sharded DRSA leg and the task-parallel
-DRSA grid, and rank 0 reports n_gpus = 2 (VERDICT r02 'next' 1)."""
+cuda:0 over gloo run the explanation headline, the row-sharded DRSA leg, the rank-local C4 chain
+(extraction + sharded optimisation) and the task-parallel DRSA grid, and rank 0 reports n_gpus = 2
+(VERDICT r02 'next' 1, r04 item 7)."""
 import json
 import os
 import subprocess
@@ -16,7 +17,8 @@ def test_bench_gpus2_own_launcher_one_device():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env.update(DRSA_BENCH_ONE_DEVICE="1", DRSA_BENCH_BACKEND="gloo")
     cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--batch", "16", "--steps", "2",
-           "--warmup", "1", "--no-cpu-baseline", "--legs", "sharded,grid", "--grid-steps", "4", "--grid-classes", "2"]
+           "--warmup", "1", "--no-cpu-baseline", "--legs", "sharded,pipeline,grid", "--grid-steps", "4",
+           "--grid-classes", "2", "--pipeline-samples", "24", "--pipeline-steps", "30"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-4000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
@@ -29,6 +31,11 @@ def test_bench_gpus2_own_launcher_one_device():
     # the N > 1 line checks itself against the unsharded run of every rank's rows
     assert sec["drsa_sharded"]["traj_dev_vs_unsharded"] < 1e-5
     assert sec["drsa_sharded"]["c5_joint"]["traj_dev_vs_unsharded"] < 1e-5
+    # the rank-local C4 chain (drsa_training_data(group=) -> main_sharded(local_rows=True)) against
+    # the single-process chain on the whole batch
+    pl = sec["drsa_rank_local_pipeline"]
+    assert pl["rows_total"] == 2 * 24 * 20 and pl["extraction_rows_per_s"] > 0 and pl["optimisation_steps_per_s"] > 0
+    assert pl["traj_dev_vs_unsharded"] < 1e-5
     g = sec["drsa_grid_task_parallel"]
     assert g["problems"] == 18 and g["problems_per_rank"] == [9, 9] and g["scaling"] == "strong"
     lo, hi = g["objective_final_min_max"]
