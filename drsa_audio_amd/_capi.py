@@ -57,9 +57,7 @@ SIGNATURES = {
                                           _i32, _i32, _f32, _vp]),
     "drsa_amd_conv_bwd_den_map": (_i32, [_fp, _vp, _i32, _vp, _i32, _fp, _fp, _fp, _i32, _i32, _i32, _i32, _i32, _i32,
                                          _i32, _i32, _f32, _vp]),
-    "drsa_amd_conv_bwd_first_fused": (_i32, [_fp, _vp, _fp, _fp, _fp, _fp, _vp, _fp, _fp, _fp, _i32, _i32, _i32,
-                                             _i32, _i32, _i32, _f32, _vp]),
-    "drsa_amd_conv_bwd_has_kernel_first_fused": (_i32, [_i32, _i32, _i32, _i32]),
+    "drsa_amd_conv_bwd_has_kernel_pw": (_i32, [_i32, _i32, _i32, _i32, _i32]),
     "drsa_amd_conv_bwd_has_kernel_bf16_pw": (_i32, [_i32, _i32, _i32, _i32]),
     "drsa_amd_conv_bwd_bf16_pw": (_i32, [_fp, _vp, _i32, _vp, _fp, _fp, _fp, _i32, _i32, _i32, _i32, _i32, _i32,
                                          _i32, _i32, _f32, _vp]),

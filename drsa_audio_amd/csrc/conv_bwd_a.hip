@@ -13,7 +13,6 @@
 #endif
 
 #define CONV_FAMILY_BWD64(CIN, NG, AM, C8)                                              \
-  CONV_ENTRY(CIN, 64, 16, 32, 8, DRSA_CONV_CIC_BWD64, NG, AM, drsa_conv::EPI_BWD),      \
   CONV_ENTRY(CIN, 64, 8, 32, 8, DRSA_CONV_CIC_BWD64, NG, AM, drsa_conv::EPI_BWD),       \
   CONV_ENTRY(CIN, 64, 8, 16, 8, DRSA_CONV_CIC_BWD64, NG, AM, drsa_conv::EPI_BWD),       \
   CONV_ENTRY(CIN, 64, 8, 8, 4, C8, NG, AM, drsa_conv::EPI_BWD)

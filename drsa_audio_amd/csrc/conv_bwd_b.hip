@@ -13,8 +13,6 @@ namespace drsa_conv {
 static const Entry kTableBwdB_e[] = {
     BWD_SET(64, 32, DRSA_CONV_CIC_BWD64_32),
     BWD_SET(32, 32, DRSA_CONV_CIC_BWD32),
-    CONV_ENTRY_FF(32, 32, DRSA_CONV_CIC_BWD32),
-    CONV_ENTRY_FF(64, 32, DRSA_CONV_CIC_BWD64_32),
 };
 extern const Table kTableBwdB = {kTableBwdB_e, (int)(sizeof(kTableBwdB_e) / sizeof(kTableBwdB_e[0]))};
 }  // namespace drsa_conv

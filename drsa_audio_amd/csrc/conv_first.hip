@@ -155,10 +155,9 @@ __global__ __launch_bounds__(kThreads) void first_conv_pool_kernel(ConvArgs a, i
 template <int NG>
 int launch_ng(const ConvArgs& a, int cout_p, int B, hipStream_t s) {
   const int total = B * (a.H / 2) * (a.W / 8);
-  const char* cs_v = getenv("DRSA_AMD_FIRST_FWD_CSPLIT");   // tuning knob (0 = heuristic)
-  const int cs_env = cs_v ? atoi(cs_v) : 0;
-  // splitting the channels over more waves measured no gain at the bench shape (store-bound)
-  const int cs = cs_env > 0 ? cs_env : 1;
+  // the kernel can split the channels over grid.y; more waves measured no gain at the bench shape
+  // (store-bound), so one split
+  const int cs = 1;
   const dim3 grid((total + kThreads - 1) / kThreads, cs);
   if (!a.out_den) hipLaunchKernelGGL((first_conv_pool_kernel<NG, 0>), grid, dim3(kThreads), 0, s, a, cout_p, total);
   else if (a.den_map) hipLaunchKernelGGL((first_conv_pool_kernel<NG, 1>), grid, dim3(kThreads), 0, s, a, cout_p, total);

@@ -1074,11 +1074,9 @@ int launch_reduce(const float* partials, const PartialPlan& pl, const Geom& g, f
 }
 
 // the fused step (drsa_fused_step_kernel) covers DP = 64 with concept blocks <= 16 wide (one
-// 1024-thread workgroup shape for the partial and the polar): C3 and C4.  DRSA_AMD_DRSA_FUSED=0
-// selects the three-launch step.
+// 1024-thread workgroup shape for the partial and the polar): C3 and C4.
 bool fused_ok(const Geom& g) {
-  static const int on = getenv("DRSA_AMD_DRSA_FUSED") ? atoi(getenv("DRSA_AMD_DRSA_FUSED")) : 1;
-  return on && g.DP == 64 && g.DKp <= 16;
+  return g.DP == 64 && g.DKp <= 16;
 }
 
 template <int DKP>

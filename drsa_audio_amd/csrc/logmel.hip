@@ -668,7 +668,6 @@ extern "C" int drsa_amd_logmel(const float* wav, int64_t n_songs, int64_t song_s
   a.log_eps = log_eps;
   a.out = out;
   const int M = n_fft / 2;
-  static const int no_fast = getenv("DRSA_AMD_LOGMEL_GENERIC") ? atoi(getenv("DRSA_AMD_LOGMEL_GENERIC")) : 0;
   auto carve = [&](bool fast) {
     int off = 0;
     auto take = [&](int n) { int o = off; off += (n + 3) & ~3; return o; };
@@ -688,7 +687,7 @@ extern "C" int drsa_amd_logmel(const float* wav, int64_t n_songs, int64_t song_s
     return (size_t)off * 4;
   };
   // the 16-wave n_fft = 800 kernel when its tables + mel tile fit in LDS, else the generic kernel
-  bool fast = n_fft == 800 && !no_fast && carve(true) <= 160 * 1024;
+  bool fast = n_fft == 800 && carve(true) <= 160 * 1024;
   const size_t smem = carve(fast);
   DRSA_REQUIRE(smem <= 160 * 1024, "logmel: LDS footprint %zu B exceeds 160 KB (n_mels*width too large)", smem);
   const void* fn = fast ? (const void*)logmel800_kernel : (const void*)logmel_kernel;

@@ -27,19 +27,9 @@ struct ConvArgs {
   float eps;
   int den_ring_only;        // forward (first layer, map den): write out_den on the ring groups only
   int den_shared;           // backward POST_DIV: den is one [cout][H][W] plane for every sample
-  int dbg;                  // ablation only (DRSA_AMD_CONV_DBG): 1 no staging loads, 2 no epilogue I/O, 4 no MFMA
-  // backward with the first-layer contraction fused (template FF = 1; drsa_amd_conv_bwd_first_fused):
-  // out holds R on the tile border ring only, ff_out the first layer's input relevance [Bq][2H][2W]
-  // off the tile footprints' border (drsa_amd_first_layer_bwd_border completes it)
-  const uint8_t* ff_amax;   // first layer's 2x2 pool argmax [B][cout][H][W]
-  const float* ff_w2;       // first layer's squared weights [cout][9]
-  float* ff_out;
 };
 
 // conv_first.hip: Cin = 1 forward with fused ReLU + 2x2 pool + argmax + den (VALU; W % 8 == 0)
 #include <hip/hip_runtime.h>
 int drsa_first_conv_pool(const ConvArgs& a, int cout_p, int ng, int B, hipStream_t s);
-// lrp_misc.hip: the first layer's w^2 contraction at the border pixels of the FY x FX footprints of
-// drsa_amd_conv_bwd_first_fused (g holds R on the footprints' cell rings; H, W at pixel resolution)
-int drsa_first_layer_border(const float* g, const uint8_t* amax, const float* w2, float* out, int Bq, int clones,
-                            int C, int H, int W, int FY, int FX, hipStream_t s);
+

@@ -25,42 +25,37 @@ const drsa_conv::Table* kTables[] = {&drsa_conv::kTableFwdA,  &drsa_conv::kTable
 
 int pad32(int c) { return (c + 31) / 32 * 32; }
 
-int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
-}
 
-const Entry* find(int cin_p, int cout_p, int W, int ng, int amode, int epi, int et = 0, int pw = 2, int ff = 0) {
+// Tile shape per direction, channel width and map width (measured choices; variant builds change
+// them with -D, scripts/build_variant.py):
+// * W >= 32: 8 x 32 tiles, except 8 x 16 for the fp32 forward into 64 channels (half the
+//   accumulators: 2 waves/SIMD instead of 1; GTZAN conv_fwd:features.6 0.391 -> 0.356 ms, VGGish
+//   features.3 1.43 -> 1.36 ms), the fp32 backward into 64 channels (the 8 x 32 tile with 16-channel
+//   chunks spills 91-115 VGPRs) and into 128 channels (VGGish features.17: the 8 x 32 tile spills
+//   358-435 VGPRs; 0.291 -> 0.101 ms); the fp32 forward into 128 channels on 8 x 8 tiles (4 times the
+//   workgroups at 3 waves/SIMD instead of 1: VGGish conv_fwd:features.17 0.318 -> 0.175 ms, .14 0.168
+//   -> 0.100 ms, fp32 standard LRP 7.6k -> 8.0k samples/s; 8 x 16: 0.189 / 0.101 ms);
+// * 8 < W < 32: 8 x 8 tiles (more workgroups for the small layers: conv_fwd:features.9 0.287 -> 0.266
+//   ms, conv_bwd 0.218 -> 0.214 at B = 512);  W <= 8: 8 x 8.
+// Measured slower and dropped: 16-row tiles, 32-channel fp32 forwards / backwards on 8 x 16 tiles.
+#ifndef DRSA_CONV_FWD128_TW
+#define DRSA_CONV_FWD128_TW 8    // fp32 forward into 128 channels at W >= 32: tile width (32, 16 or 8)
+#endif
+const Entry* find(int cin_p, int cout_p, int W, int ng, int amode, int epi, int et = 0, int pw = 2) {
   int th = 8, tw, mw;
-  static const int th16 = env_int("DRSA_AMD_CONV_TH16", 0);
-  // 8x8 tiles at 8 < W < 32 (bits: 1 forward, 2 backward; measured faster than 8x16 at 16x16: conv_fwd
-  // features.9 0.287 -> 0.266 ms, conv_bwd 0.218 -> 0.214 at B = 512); DRSA_AMD_CONV_W16_TILE8=0 restores 8x16
-  static const int w16_as8 = env_int("DRSA_AMD_CONV_W16_TILE8", 3);
-  // forward into 64 channels at W >= 32 with 8 x 16 tiles (half the accumulators: 2 waves/SIMD
-  // instead of 1; GTZAN conv_fwd:features.6 0.391 -> 0.356 ms, VGGish features.3 fp32 1.43 -> 1.36 ms)
-  static const int fwd64_t16 = env_int("DRSA_AMD_CONV_FWD64_T16", 1);
-  // (measured slower, off) 32-channel fp32 forwards on 8 x 16 tiles (123 VGPRs: 4 waves/SIMD instead
-  // of 3): conv_fwd:features.3 0.632 -> 0.659 ms
-  static const int fwd32_t16 = env_int("DRSA_AMD_CONV_FWD32_T16", 0);
-  const bool fwd_t16 = epi != EPI_BWD && et == 0 && ((fwd64_t16 && cout_p == 64) || (fwd32_t16 && cout_p == 32 && !th16));
-  // fp32 backward into 64 channels at W >= 32 (VGGish) on 8 x 16 tiles: the 8 x 32 tile with 16-channel
-  // chunks spills 91-115 VGPRs at 3 waves/SIMD, the 8 x 16 one none
-  static const int bwd64_t16 = env_int("DRSA_AMD_CONV_BWD64_T16", 1);
-  static const int bwd32_t16 = env_int("DRSA_AMD_CONV_BWD32_T16", 0);   // (experiment) the same into 32 channels
-  // fp32 backward into 128 channels at W >= 32 (VGGish features.17, 100 -> 100 at 32 x 32): the 8 x 32
-  // tile holds 128 accumulators and spills 358-435 VGPRs at 3 waves/SIMD, the 8 x 16 one none
-  const bool bwd_t16 = epi == EPI_BWD && et == 0 &&
-                       ((bwd64_t16 && cout_p == 64 && cin_p <= 128) || cout_p == 128 ||
-                        (bwd32_t16 && cout_p == 32 && !th16));
-  if (W >= 32 && (fwd_t16 || bwd_t16)) { tw = 16; mw = 8; th = 8; }
-  else if (W >= 32) { tw = 32; mw = 8; th = (th16 && cout_p == 32 && ng <= 2) ? 16 : 8; }
-  else if (W > 8 && !(w16_as8 & (epi == EPI_BWD ? 2 : 1))) { tw = 16; mw = 8; }
+  const bool fwd_t16 = epi != EPI_BWD && et == 0 && cout_p == 64;
+  const bool bwd_t16 = epi == EPI_BWD && et == 0 && ((cout_p == 64 && cin_p <= 128) || cout_p == 128);
+  if (W >= 32 && epi != EPI_BWD && et == 0 && cout_p == 128 && DRSA_CONV_FWD128_TW != 32) {
+    tw = DRSA_CONV_FWD128_TW;
+    mw = tw == 8 ? 4 : 8;
+  } else if (W >= 32 && (fwd_t16 || bwd_t16)) { tw = 16; mw = 8; }
+  else if (W >= 32) { tw = 32; mw = 8; }
   else { tw = 8; mw = 4; }
   for (const drsa_conv::Table* t : kTables)
     for (int i = 0; i < t->n; ++i) {
       const Entry& e = t->entries[i];
       if (e.cin_p == cin_p && e.cout_p == cout_p && e.th == th && e.tw == tw && e.mw == mw && e.ng == ng &&
-          e.amode == amode && e.epi == epi && e.et == et && e.pw == pw && e.ff == ff)
+          e.amode == amode && e.epi == epi && e.et == et && e.pw == pw)
         return &e;
     }
   return nullptr;
@@ -98,8 +93,7 @@ int drsa_amd_conv_fwd(const float* in, const float* wts, const float* bias, cons
   DRSA_REQUIRE(pool || W % 4 == 0, "conv_fwd: an unpooled output needs W %% 4 == 0 (float4 epilogue; got W=%d)", W);
   DRSA_REQUIRE(pool != 2 || W % 4 == 0, "conv_fwd: a 2x4 pool needs W %% 4 == 0 (got W=%d)", W);
   const int cin_p = cin_pad(cin), cout_p = pad32(cout);
-  const int first_generic = env_int("DRSA_AMD_CONV_FIRST_GENERIC", 0);   // per call: tests compare both paths
-  if (cin == 1 && pool == 1 && W % 8 == 0 && !first_generic) {
+  if (cin == 1 && pool == 1 && W % 8 == 0) {   // the Cin = 1 VALU kernel (conv_first.hip)
     ConvArgs a{};
     a.in = in; a.wts = wts; a.bias = bias; a.den_map = den_map; a.out = out; a.out_amax = out_amax;
     a.out_den = out_den; a.H = H; a.W = W; a.cin = cin; a.cout = cout; a.clones = 1;
@@ -162,8 +156,6 @@ int drsa_amd_conv_bwd(const float* g, const uint8_t* g_amax, const float* wts, c
   ConvArgs a{};
   a.in = g; a.in_amax = g_amax; a.wts = wts; a.x = x; a.den = den; a.out = out; a.H = H; a.W = W;
   a.cin = cin; a.cout = cout; a.clones = clones; a.xmode = xmode; a.post = post; a.eps = eps;
-  static const int dbg = env_int("DRSA_AMD_CONV_DBG", 0);
-  a.dbg = dbg;
   const Entry* e = find(cin_p, cout_p, W, ng, g_amax ? A_POOLSPARSE : A_DENSE, EPI_BWD);
   if (!e) {
     drsa::set_error("conv_bwd: no kernel for cin=%d cout=%d W=%d ng=%d sparse=%d", cin, cout, W, ng, g_amax != nullptr);
@@ -297,42 +289,6 @@ int drsa_amd_conv_bwd_den_ring(const float* g, const uint8_t* g_amax, const void
   a.den_const4 = den_const4; a.out = out; a.H = H; a.W = W; a.cin = cin; a.cout = cout;
   a.clones = clones; a.xmode = xmode; a.post = POST_DIV_RING; a.eps = eps;
   return launch(e, a, Bq, (hipStream_t)stream);
-}
-
-int drsa_amd_conv_bwd_has_kernel_first_fused(int cin, int cout, int H, int W) {
-  // the border kernel runs one band (2W pixels) + 14 rows of strip pairs per workgroup of 256
-  if (cout != 32 || H % 8 != 0 || W % 32 != 0 || 2 * W + 14 * (W / 32 + 1) > 256) return 0;
-  return find(pad32(cin), 32, W, 1, A_POOLSPARSE, EPI_BWD, 0, 2, 1) != nullptr;
-}
-
-int drsa_amd_conv_bwd_first_fused(const float* g, const uint8_t* g_amax, const float* wts, const float* x,
-                                  const float* den, const float* den_const4, const uint8_t* first_amax,
-                                  const float* first_w2, float* out, float* first_out, int Bq, int clones, int cin,
-                                  int cout, int H, int W, float eps, void* stream) {
-  DRSA_REQUIRE(g && g_amax && wts && x && den && first_amax && first_w2 && out && first_out,
-               "conv_bwd_first_fused: null pointer");
-  DRSA_REQUIRE(Bq > 0 && clones > 0 && Bq % clones == 0, "conv_bwd_first_fused: bad batch/clones");
-  DRSA_REQUIRE(cout == 32 && H % 8 == 0 && W % 32 == 0 && 2 * W + 14 * (W / 32 + 1) <= 256,
-               "conv_bwd_first_fused: needs cout == 32, H %% 8 == 0, W %% 32 == 0 and W <= 96 (got cout=%d %dx%d)",
-               cout, H, W);
-  DRSA_REQUIRE(!den_const4 || ((uintptr_t)den_const4 & 15) == 0, "conv_bwd_first_fused: den_const4 must be 16-byte aligned");
-  const Entry* e = find(pad32(cin), 32, W, 1, A_POOLSPARSE, EPI_BWD, 0, 2, 1);
-  if (!e) {
-    drsa::set_error("conv_bwd_first_fused: no kernel for cin=%d W=%d", cin, W);
-    return DRSA_EUNSUPPORTED;
-  }
-  ConvArgs a{};
-  a.in = g; a.in_amax = g_amax; a.wts = wts; a.x = x; a.den = den; a.den_const4 = den_const4; a.out = out;
-  a.H = H; a.W = W; a.cin = cin; a.cout = cout; a.clones = clones; a.xmode = XM_MUL;
-  a.post = den_const4 ? POST_DIV_RING : POST_DIV; a.eps = eps;
-  a.ff_amax = first_amax; a.ff_w2 = first_w2; a.ff_out = first_out;
-  static const int ff_dbg0 = env_int("DRSA_AMD_FF_DBG", 0);
-  const int rc = (ff_dbg0 & 2) ? DRSA_OK : launch(e, a, Bq, (hipStream_t)stream);
-  if (rc != DRSA_OK) return rc;
-  static const int ff_dbg = env_int("DRSA_AMD_FF_DBG", 0);   // ablation only: 1 = no border kernel, 2 = border only
-  if (ff_dbg & 1) return DRSA_OK;
-  return drsa_first_layer_border(out, first_amax, first_w2, first_out, Bq, clones, cout, 2 * H, 2 * W, 2 * e->th,
-                                 2 * e->tw, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -95,8 +95,7 @@ constexpr int bf_stride(int hx) {
 // chain), 1 = bf16 (v_mfma_f32_32x32x16_bf16, forward only: conv inputs and weights rounded to
 // bf16 when staged, fp32 accumulation, fp32 outputs).  The bf16 chunk is 16 input channels = one
 // tap per MFMA (k = tap * 16 + ci); its halo is pixel-major, 8 channels per 16-byte pixel slot.
-template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI, int ET = 0, int PW = 2,
-          int FF = 0>
+template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI, int ET = 0, int PW = 2>
 struct ConvCfg {
   static constexpr int CIN_ = CIN, COUT_ = COUT, TH_ = TH, TW_ = TW, MW_ = MW, CIC_ = CIC, NG_ = NG;
   static constexpr int AMODE_ = AMODE, EPI_ = EPI;
@@ -133,10 +132,7 @@ struct ConvCfg {
   static constexpr size_t staging_floats =
       BF ? bf_halo_floats + bf_w_floats : (size_t)CIC * PLANE + (size_t)NG * KCP * COUT;
   static constexpr size_t epi_floats = (size_t)TCH * TH * TWP;
-  // FF: + the first layer's w^2 [COUT][12] (9 used) behind the staging / epilogue area
-  static constexpr size_t ff_w_floats = FF ? (size_t)COUT * 12 : 0;
-  static constexpr size_t lds_floats =
-      (staging_floats > epi_floats ? staging_floats : epi_floats) + ff_w_floats;
+  static constexpr size_t lds_floats = staging_floats > epi_floats ? staging_floats : epi_floats;
   // minimum waves per SIMD the register allocation must allow (1 block = 1 wave per SIMD)
   static constexpr int WPE = BF ? (COUT <= 64 ? DRSA_CONV_BF_WPE : 1)
                              : (EPI == EPI_BWD && NG == 1) ? (SMALL_BWD ? 4 : DRSA_CONV_BWD_WPE)
@@ -155,14 +151,6 @@ struct ConvCfg {
                                                                   (ET == 1 || TW % 16 == 0)))),
                 "2x4 pool windows: the forward pool epilogue, or the backward's pool-sparse staging (fp32: "
                 "tiles of whole float4 cell groups)");
-  // FF: the first layer's w^2 contraction fused into the epilogue.  The pass's R is re-laid as
-  // the first layer's unpooled g (argmax pixel of each 2x2 cell) in FCH-channel slices of a pixel
-  // image [FCH][2TH][FPS] (pixel column X at X + 4) over the dead staging tile T
-  static constexpr int FCH = kThreads / (TH * TW / 4);
-  static constexpr int FPS = 2 * TW + 8;
-  static_assert(!FF || (EPI == EPI_BWD && NG == 1 && ET == 0 && ES == 2 && COUT == 32 && TH == 8 && TW == 32 &&
-                        (size_t)FCH * 2 * TH * FPS <= epi_floats),
-                "first-layer fusion: the fp32 8x32-tile backward into 32 channels");
   static constexpr int PW_ = PW;
 };
 
@@ -198,7 +186,6 @@ struct Stager {
   // the compiler issues them back to back without exec branches or per-load waits.
   __device__ __forceinline__ void load(const ConvArgs& a, int c0, int tid, int ty0, int tx0, int bq, int bs) {
     const int H = a.H, W = a.W, H2 = H >> 1, W2 = W >> 1;
-    const bool noload = (a.dbg & 1) != 0;
     // per-sample bases (uniform) + 32-bit per-lane offsets: saddr + voffset loads instead of a
     // 64-bit multiply-add per element (the host keeps one sample's cin x H x W below 2^31)
     const int W4 = W >> 2;
@@ -213,7 +200,7 @@ struct Stager {
         const int row = i / Q16, q = i % Q16;
         const int ci = row / CY, ry = row % CY;
         const int cy = qy0 + ry, cx = cx0 + 4 * q, c = c0 + ci;
-        const bool ok = i < SROWS * Q16 && cy >= 0 && cy < H2 && c < a.cin && cx < W4 && !noload;
+        const bool ok = i < SROWS * Q16 && cy >= 0 && cy < H2 && c < a.cin && cx < W4;
         const int o = ok ? (c * H2 + cy) * W4 + cx : 0;
         const float4 v = *reinterpret_cast<const float4*>(inb + o);
         const uint32_t am = *reinterpret_cast<const uint32_t*>(amb + o);
@@ -226,7 +213,7 @@ struct Stager {
         const int row = i >> 1, side = i & 1;
         const int ci = row / CY, ry = row % CY;
         const int cy = qy0 + ry, cx = side ? cx0 + TW / 4 : cx0 - 1, c = c0 + ci;
-        const bool ok = i < SROWS * 2 && cy >= 0 && cy < H2 && cx >= 0 && cx < W4 && c < a.cin && !noload;
+        const bool ok = i < SROWS * 2 && cy >= 0 && cy < H2 && cx >= 0 && cx < W4 && c < a.cin;
         const int o = ok ? (c * H2 + cy) * W4 + cx : 0;
         const float v = inb[o];
         const int am = (int)amb[o];
@@ -241,7 +228,7 @@ struct Stager {
           const int row = i / Q4, q = i % Q4;
           const int ci = row / HY, hy = row % HY;
           const int gy = ty0 - 1 + hy, gx = tx0 + 4 * q, c = c0 + ci;
-          const bool ok = i < DROWS * Q4 && gy >= 0 && gy < H && c < a.cin && gx < W && !noload;
+          const bool ok = i < DROWS * Q4 && gy >= 0 && gy < H && c < a.cin && gx < W;
           const int o = ok ? (c * H + gy) * W + gx : 0;
           const float4 v = *reinterpret_cast<const float4*>(inb + o);
           st_i[it] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -253,7 +240,7 @@ struct Stager {
           const int row = i / Q4, q = i % Q4;
           const int ci = row / HY, hy = row % HY;
           const int gy = ty0 - 1 + hy, gx = tx0 + 4 * q, c = c0 + ci;
-          const bool rok = i < DROWS * Q4 && gy >= 0 && gy < H && c < a.cin && !noload;
+          const bool rok = i < DROWS * Q4 && gy >= 0 && gy < H && c < a.cin;
           float vv[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -271,7 +258,7 @@ struct Stager {
         const int row = i >> 1, side = i & 1;
         const int ci = row / HY, hy = row % HY;
         const int gy = ty0 - 1 + hy, gx = side ? tx0 + TW : tx0 - 1, c = c0 + ci;
-        const bool ok = i < DROWS * 2 && gy >= 0 && gy < H && gx >= 0 && gx < W && c < a.cin && !noload;
+        const bool ok = i < DROWS * 2 && gy >= 0 && gy < H && gx >= 0 && gx < W && c < a.cin;
         const int o = ok ? (c * H + gy) * W + gx : 0;
         const float v = inb[o];
         st_h[it] = ok ? v : 0.f;
@@ -285,7 +272,7 @@ struct Stager {
           const int row = i / Q8, q = i % Q8;
           const int ci = row / CY, ry = row % CY;
           const int cy = qy0 + ry, cx = qx0 + 1 + 4 * q, c = c0 + ci;
-          const bool ok = i < SROWS * Q8 && 4 * q < TW / 2 && cy >= 0 && cy < H2 && c < a.cin && cx < W2 && !noload;
+          const bool ok = i < SROWS * Q8 && 4 * q < TW / 2 && cy >= 0 && cy < H2 && c < a.cin && cx < W2;
           const int o = ok ? (c * H2 + cy) * W2 + cx : 0;
           const float4 v = *reinterpret_cast<const float4*>(inb + o);
           const uint32_t am = *reinterpret_cast<const uint32_t*>(amb + o);
@@ -299,7 +286,7 @@ struct Stager {
           const int row = i / Q8, q = i % Q8;
           const int ci = row / CY, ry = row % CY;
           const int cy = qy0 + ry, cx = qx0 + 1 + 4 * q, c = c0 + ci;
-          const bool rok = i < SROWS * Q8 && 4 * q < TW / 2 && cy >= 0 && cy < H2 && c < a.cin && !noload;
+          const bool rok = i < SROWS * Q8 && 4 * q < TW / 2 && cy >= 0 && cy < H2 && c < a.cin;
           float vv[4];
           uint32_t aa = 0;
 #pragma unroll
@@ -321,7 +308,7 @@ struct Stager {
         const int row = i >> 1, side = i & 1;
         const int ci = row / CY, ry = row % CY;
         const int cy = qy0 + ry, cx = side ? qx0 + CX - 1 : qx0, c = c0 + ci;
-        const bool ok = i < SROWS * 2 && cy >= 0 && cy < H2 && cx >= 0 && cx < W2 && c < a.cin && !noload;
+        const bool ok = i < SROWS * 2 && cy >= 0 && cy < H2 && cx >= 0 && cx < W2 && c < a.cin;
         const int o = ok ? (c * H2 + cy) * W2 + cx : 0;
         const float v = inb[o];
         const int am = (int)amb[o];
@@ -693,29 +680,10 @@ __device__ __forceinline__ void mfma_chunk_bf(const uint4* hb, const uint4* wb, 
   }
 }
 
-// backward: XCD-aware (sample, tile, clone) order of the workgroups (1) or the launch order (0)
-#ifndef DRSA_CONV_BWD_REMAP
-#define DRSA_CONV_BWD_REMAP 0   // measured: no change at 4 clones
-#endif
-// first-layer fusion ablation (experiments only): 1 = no contraction, 2 = no pixel image either
-#ifndef DRSA_FF_DBG
-#define DRSA_FF_DBG 0
-#endif
-// first-layer fusion: 1 = a pixel row's neighbour columns from the adjacent lanes (DPP) instead of
-// two more LDS reads
-#ifndef DRSA_FF_DPP
-#define DRSA_FF_DPP 1
-#endif
-// first-layer fusion: unroll of the contraction's channel loop (4 = all, spills)
-#ifndef DRSA_FF_UNROLL
-#define DRSA_FF_UNROLL 1
-#endif
-
 // PW: pool window width of EPI_FWD_POOL (2 x PW windows; 4 = VGGish's (2,4) pool)
-template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI, int ET = 0, int PW = 2,
-          int FF = 0>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AMODE, EPI, ET, PW, FF>::WPE))) void conv3x3_kernel(ConvArgs a) {
-  using Cfg = ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AMODE, EPI, ET, PW, FF>;
+template <int CIN, int COUT, int TH, int TW, int MW, int CIC, int NG, int AMODE, int EPI, int ET = 0, int PW = 2>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AMODE, EPI, ET, PW>::WPE))) void conv3x3_kernel(ConvArgs a) {
+  using Cfg = ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, AMODE, EPI, ET, PW>;
   constexpr int HY = Cfg::HY, HX = Cfg::HX, RS = Cfg::RS, PLANE = Cfg::PLANE;
   constexpr int MTH = Cfg::MTH, MTW = Cfg::MTW, MTX = Cfg::MTX;
   constexpr int WM = Cfg::WM, MPW = Cfg::MPW, NPW = Cfg::NPW;
@@ -728,20 +696,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
   const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
   const int H = a.H, W = a.W;
   const int tiles_x = (W + TW - 1) / TW;
-  int tile_id = blockIdx.x, bq = blockIdx.y;  // bq: batch index (incl. clones)
-  if constexpr (EPI == EPI_BWD && DRSA_CONV_BWD_REMAP) {
-    // XCD-aware order: dispatch id d runs on XCD d % 8; give each XCD a contiguous run of
-    // (sample, tile, clone) items, clones fastest, so the clones of a tile (which read the same
-    // x / den tile) and the neighbouring tiles (which share g halo rows) meet in one L2
-    const int ntile = gridDim.x, total = ntile * gridDim.y;
-    if (total % 8 == 0) {
-      const int id = blockIdx.x + blockIdx.y * ntile;
-      const int L = (id & 7) * (total >> 3) + (id >> 3);
-      const int q = L % a.clones, rest = L / a.clones;
-      tile_id = rest % ntile;
-      bq = (rest / ntile) * a.clones + q;
-    }
-  }
+  const int tile_id = blockIdx.x, bq = blockIdx.y;  // bq: batch index (incl. clones)
   const int ty0 = (tile_id / tiles_x) * TH;
   const int tx0 = (tile_id % tiles_x) * TW;
   const int bs = bq / a.clones;               // sample index (shared forward state)
@@ -810,12 +765,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
   auto gchs = [&](int cl, int v, int sub) { return ES == 1 ? gch(cl, v) : v * 32 + sub * TCH + cl; };
   typename std::conditional<Cfg::BF, StagerBF<Cfg>, Stager<Cfg>>::type stg;
   stg.load(a, 0, tid, ty0, tx0, bq, bs);
-  float* const WL = smem + (Cfg::lds_floats - Cfg::ff_w_floats);
-  if constexpr (FF) {
-    // read in the epilogue with uniform addresses (LDS broadcasts; the scalar cache cannot be used
-    // for a buffer the compiler cannot prove unaliased with the kernel's stores)
-    for (int i = tid; i < COUT * 9; i += kThreads) WL[(i / 9) * 12 + i % 9] = a.ff_w2[i];
-  }
   // backward: all chunks but the last here, the last one peeled below (after the epilogue
   // addressing is set up, so that none of it is live across the loop)
   for (int chunk = 0; chunk + (EPI == EPI_BWD ? 1 : 0) < Cfg::NCHUNK; ++chunk) {
@@ -824,7 +773,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
     else stg.store(halo, wl, tid);
     __syncthreads();
     if (chunk + 1 < Cfg::NCHUNK) stg.load(a, (chunk + 1) * CIC, tid, ty0, tx0, bq, bs);
-    if (!active || (a.dbg & 4)) continue;
+    if (!active) continue;
     if constexpr (Cfg::BF)
       mfma_chunk_bf<Cfg>(reinterpret_cast<const uint4*>(halo), reinterpret_cast<const uint4*>(wl), pix_off, lane, wn, acc);
     else
@@ -846,8 +795,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
   // mode does not use it) and are ALL issued before any arithmetic; the rule / post modes are
   // uniform selects, not branches (a branch around the division would put each den load in
   // its own basic block, one full memory round trip after another)
-  const bool need_x = (a.xmode != XM_NONE || a.post != POST_NONE) && !(a.dbg & 2);
-  const bool mul_x = a.xmode != XM_NONE && !(a.dbg & 2), split_x = a.xmode == XM_SPLIT && !(a.dbg & 2);
+  const bool need_x = a.xmode != XM_NONE || a.post != POST_NONE;
+  const bool mul_x = a.xmode != XM_NONE, split_x = a.xmode == XM_SPLIT;
   // POST_DIV_RING: float4 groups off the image's border ring read the map's per-channel value
   // (den_const4, one 16-byte line per channel: an L1 broadcast) instead of the per-sample copy,
   // which the forward writes on the ring only; the pointer is a per-lane select, no branch
@@ -869,15 +818,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
   const unsigned upix = (unsigned)pix;
   float* const obase = a.out + (size_t)bq * a.cout * HW;
   const float* const xbase = a.x ? a.x + (size_t)bs * a.cout * HW : obase;
-  // FF: float4 groups on the tile's border ring still store R (the border pixels' contraction
-  // needs the neighbour tiles' cells: drsa_amd_first_layer_bwd_border); the first layer's argmax
-  // of the group's 4 cells is one 32-bit load; contraction thread (fr, fj) owns footprint pixels
-  // (fr, 4fj .. 4fj + 3) of the 2TH x 2TW footprint
-  const bool tile_ring = py == 0 || py == TH - 1 || px == 0 || px == TW - 4;
-  const uint8_t* ffa = FF ? a.ff_amax + (size_t)bs * a.cout * HW + pix : nullptr;
-  const int fr = tid / (TW / 2), fj = tid % (TW / 2);
-  typedef float ff2 __attribute__((ext_vector_type(2)));
-  ff2 ffacc[2] = {ff2{0.f, 0.f}, ff2{0.f, 0.f}};
   // epilogue x/den loads of (n-tile v, pass sub); (0, 0) is issued before the last chunk's MFMAs
   auto epi_loads = [&](int v, int sub, float4 (&xk)[V4T], float4 (&dk)[V4T], bool lx = true, bool ld = true,
                        int i0 = 0, int i1 = -1) {
@@ -904,7 +844,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
     __syncthreads();
     epi_loads(0, 0, pre_x, pre_d, true, DRSA_CONV_PRE_D, 0, kPreN);
 
-    if (active && !(a.dbg & 4)) {
+    if (active) {
       if constexpr (Cfg::BF)
         mfma_chunk_bf<Cfg>(reinterpret_cast<const uint4*>(halo), reinterpret_cast<const uint4*>(wl), pix_off, lane, wn,
                            acc);
@@ -1151,108 +1091,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
       } else {
         epi_loads(v, sub, xk, dk);
       }
-      uint32_t ak[V4T];
-      if constexpr (FF) {
-#pragma unroll
-        for (int it = 0; it < V4T; ++it) {
-          const int co = gchs(cl0 + it * CS, v, sub);
-          ak[it] = *reinterpret_cast<const uint32_t*>(ffa + (size_t)co * HW);
-        }
-      }
       stage(v, [&](int u, int r) { return acc[0][u][v][r]; }, sub);
-      if constexpr (FF) {
-        // R (the Epsilon-type rule and the division; the host requires XM_MUL and POST_DIV[_RING])
-        float4 Rf[V4T];
-#pragma unroll
-        for (int it = 0; it < V4T; ++it) {
-          const int cl = cl0 + it * CS;
-          const int co = gchs(cl, v, sub);
-          const float4 t = *reinterpret_cast<const float4*>(T + (cl * TH + py) * TWP + px);
-          const float4 x = xk[it], d = dk[it];
-          auto f = [&](float tt, float xx, float dd) {
-            const float q = div_nb(xx * tt, stab(dd, eps));
-            return (xx > 0.f) ? q : 0.f;
-          };
-          Rf[it] = make_float4(f(t.x, x.x, d.x), f(t.y, x.y, d.y), f(t.z, x.z, d.z), f(t.w, x.w, d.w));
-          if (tile_ring) *reinterpret_cast<float4*>(oqp + (size_t)co * HW) = Rf[it];
-        }
-        constexpr int FPS = Cfg::FPS, FH = 2 * TH;
-        float* P = T;
-#pragma unroll
-        for (int it = 0; it < ((DRSA_FF_DBG & 2) ? 0 : V4T); ++it) {
-          // slice it = channels sub*TCH + it*CS + (0..CS-1); this thread's group is slot cl0:
-          // cell (py, px + i) -> pixels (2py + s/2, 2px + 2i + s%2), s = its argmax, zeros elsewhere
-          __syncthreads();
-          {
-            const uint32_t am = ak[it];
-            const float rv[4] = {Rf[it].x, Rf[it].y, Rf[it].z, Rf[it].w};
-            float o0[8], o1[8];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const uint32_t s = (am >> (8 * i)) & 0xffu;
-              o0[2 * i] = s == 0u ? rv[i] : 0.f;
-              o0[2 * i + 1] = s == 1u ? rv[i] : 0.f;
-              o1[2 * i] = s == 2u ? rv[i] : 0.f;
-              o1[2 * i + 1] = s == 3u ? rv[i] : 0.f;
-            }
-            float* pw = P + (cl0 * FH + 2 * py) * FPS + 2 * px + 4;
-            reinterpret_cast<float4*>(pw)[0] = make_float4(o0[0], o0[1], o0[2], o0[3]);
-            reinterpret_cast<float4*>(pw)[1] = make_float4(o0[4], o0[5], o0[6], o0[7]);
-            reinterpret_cast<float4*>(pw + FPS)[0] = make_float4(o1[0], o1[1], o1[2], o1[3]);
-            reinterpret_cast<float4*>(pw + FPS)[1] = make_float4(o1[4], o1[5], o1[6], o1[7]);
-          }
-          __syncthreads();
-          // the dense first-layer chain (first_layer_bwd_pooled_kernel): channel ascending, then
-          // dy, dx; rows / columns outside the footprint are clamped (only border pixels read them,
-          // and those are recomputed by the border kernel)
-#pragma unroll DRSA_FF_UNROLL
-          for (int k = 0; k < ((DRSA_FF_DBG & 1) ? 0 : CS); ++k) {
-            const int c = v * 32 + sub * TCH + it * CS + k;
-            const float4 w03 = *reinterpret_cast<const float4*>(WL + c * 12);
-            const float4 w47 = *reinterpret_cast<const float4*>(WL + c * 12 + 4);
-            const float wv[9] = {w03.x, w03.y, w03.z, w03.w, w47.x, w47.y, w47.z, w47.w, WL[c * 12 + 8]};
-            ff2 pr[3][5];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-              int rr = fr - 1 + i;
-              rr = rr < 0 ? 0 : rr > FH - 1 ? FH - 1 : rr;
-              const float* q = P + (k * FH + rr) * FPS + 4 * fj + 3;
-#if DRSA_FF_DPP
-              // the row's 4 pixels as one ds_read_b128 (8 lanes cover all banks), the neighbours'
-              // edge pixels from the adjacent lanes of the same 16-lane row (DPP row shifts; the
-              // footprint's outer columns only feed border pixels, recomputed elsewhere)
-              const float4 p4 = *reinterpret_cast<const float4*>(q + 1);
-              const float p0 = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-                                   0, __builtin_bit_cast(int, p4.w), 0x111, 0xf, 0xf, true));
-              const float p5 = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-                                   0, __builtin_bit_cast(int, p4.x), 0x101, 0xf, 0xf, true));
-#else
-              const float p0 = q[0];
-              const float4 p4 = *reinterpret_cast<const float4*>(q + 1);
-              const float p5 = q[5];
-#endif
-              pr[i][0] = ff2{p0, p4.x};
-              pr[i][1] = ff2{p4.x, p4.y};
-              pr[i][2] = ff2{p4.y, p4.z};
-              pr[i][3] = ff2{p4.z, p4.w};
-              pr[i][4] = ff2{p4.w, p5};
-            }
-#pragma unroll
-            for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-              for (int dx = -1; dx <= 1; ++dx) {
-                const float w = wv[(1 - dy) * 3 + (1 - dx)];
-                const ff2 ww = ff2{w, w};
-                ffacc[0] = __builtin_elementwise_fma(pr[1 + dy][1 + dx], ww, ffacc[0]);
-                ffacc[1] = __builtin_elementwise_fma(pr[1 + dy][3 + dx], ww, ffacc[1]);
-              }
-          }
-        }
-        continue;
-      }
       // the common mode (Epsilon-type rule: R = x * J^T g, then the next layer's division)
       // specialised: the loads above are already in flight, this branch is uniform
-      if (NG == 1 && a.xmode == XM_MUL && post_div && !(a.dbg & 2)) {
+      if (NG == 1 && a.xmode == XM_MUL && post_div) {
 #pragma unroll
         for (int it = 0; it < V4T; ++it) {
           const int cl = cl0 + it * CS;
@@ -1306,10 +1148,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
         const bool ok = cl < TCH && co < a.cout;
         const int coc = ok ? co : 0;
         float4 R = Rk[it];
-        if (a.dbg & 2) {
-          if (ok && pix_ok && R.x == 12345.f) oqp[(size_t)coc * HW] = 1.f;
-          continue;
-        }
         // POST_DIV: x > 0 ? R / stab(den) : 0;  POST_MASK: x > 0 ? R : 0 (quotients evaluated for
         // every lane and mode, then selected)
         const float4 x = xk[it], d = dk[it];
@@ -1322,12 +1160,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
         if (ok && pix_ok) *reinterpret_cast<float4*>(obase + (upix + (unsigned)coc * (unsigned)HW)) = R;
       }
      }
-      if constexpr (FF) {
-        // every footprint pixel is written; the border ones are overwritten by the border kernel
-        const int W2 = 2 * W;
-        *reinterpret_cast<float4*>(a.ff_out + ((size_t)bq * 2 * H + 2 * ty0 + fr) * W2 + 2 * tx0 + 4 * fj) =
-            make_float4(ffacc[0].x, ffacc[0].y, ffacc[1].x, ffacc[1].y);
-      }
     }
   }
 }
@@ -1339,16 +1171,8 @@ struct Entry {
   KernFn fn;
   size_t lds;
   int et = 0;   // operand type (ConvCfg ET)
-  int pw = 2;   // forward pool window width (ConvCfg PW)
-  int ff = 0;   // first-layer contraction fused into the backward epilogue (ConvCfg FF)
+  int pw = 2;   // pool window width (ConvCfg PW)
 };
-
-// fp32 pool-sparse backward of the layer above a WSquare first layer, with that layer's
-// contraction fused (drsa_amd_conv_bwd_first_fused)
-#define CONV_ENTRY_FF(CIN, COUT, CIC)                                                                       \
-  drsa_conv::Entry{CIN, COUT, 8, 32, 8, CIC, 1, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD,                \
-                   drsa_conv::conv3x3_kernel<CIN, COUT, 8, 32, 8, CIC, 1, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD, 0, 2, 1>, \
-                   drsa_conv::ConvCfg<CIN, COUT, 8, 32, 8, CIC, 1, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD, 0, 2, 1>::lds_floats * sizeof(float), 0, 2, 1}
 
 #define CONV_ENTRY(CIN, COUT, TH, TW, MW, CIC, NG, AM, EP)                                                 \
   drsa_conv::Entry{CIN, COUT, TH, TW, MW, CIC, NG, AM, EP,                                                 \
@@ -1395,17 +1219,14 @@ struct Entry {
                    drsa_conv::conv3x3_kernel<CIN, COUT, TH, TW, MW, CIC, NG, drsa_conv::A_DENSE, drsa_conv::EPI_FWD_POOL, ET, 4>, \
                    drsa_conv::ConvCfg<CIN, COUT, TH, TW, MW, CIC, NG, drsa_conv::A_DENSE, drsa_conv::EPI_FWD_POOL, ET, 4>::lds_floats * sizeof(float), ET, 4}
 #define CONV_FAMILY_P4(CIN, COUT, CIC, NG, ET)                    \
-  CONV_ENTRY_P4(CIN, COUT, 16, 32, 8, CIC, NG, ET),                \
   CONV_ENTRY_P4(CIN, COUT, 8, 32, 8, CIC, NG, ET),                 \
   CONV_ENTRY_P4(CIN, COUT, 8, 16, 8, CIC, NG, ET),                 \
   CONV_ENTRY_P4(CIN, COUT, 8, 8, 4, CIC, NG, ET)
 #define FWD_SET_P4(CIN, COUT, CIC, ET)                                                  \
   CONV_FAMILY_P4(CIN, COUT, CIC, 1, ET), CONV_FAMILY_P4(CIN, COUT, CIC, 2, ET), CONV_FAMILY_P4(CIN, COUT, CIC, 3, ET)
 
-// tile by output width: W >= 32 -> 16x32 (32 output channels) or 8x32 (MW 8); 8 < W < 32 -> 8x16
-// (MW 8); W <= 8 -> 8x8 (MW 4)
+// tile families (the choice: lrp_conv.hip find): 8x32 / 8x16 (MW 8), 8x8 (MW 4)
 #define CONV_FAMILY(CIN, COUT, CIC, NG, AM, EP)                      \
-  CONV_ENTRY(CIN, COUT, 16, 32, 8, CIC, NG, AM, EP),                 \
   CONV_ENTRY(CIN, COUT, 8, 32, 8, CIC, NG, AM, EP),                  \
   CONV_ENTRY(CIN, COUT, 8, 16, 8, CIC, NG, AM, EP),                  \
   CONV_ENTRY(CIN, COUT, 8, 8, 4, CIC, NG, AM, EP)
@@ -1425,7 +1246,6 @@ struct Entry {
   CONV_FAMILY(CIN, COUT, CIC, 2, drsa_conv::A_POOLSPARSE, drsa_conv::EPI_BWD)
 
 #define CONV_FAMILY_BF(CIN, COUT, NG, EP)                      \
-  CONV_ENTRY_BF(CIN, COUT, 16, 32, 8, NG, EP),                 \
   CONV_ENTRY_BF(CIN, COUT, 8, 32, 8, NG, EP),                  \
   CONV_ENTRY_BF(CIN, COUT, 8, 16, 8, NG, EP),                  \
   CONV_ENTRY_BF(CIN, COUT, 8, 8, 4, NG, EP)

@@ -1060,111 +1060,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRSA_FQ_WPE
   }
 }
 
-// The border pixels of drsa_amd_conv_bwd_first_fused's FY x FX footprints (FY = 2 TH2, FX = 2 TW2):
-// workgroup (k, bq) takes the horizontal band of pixel rows FY k - 1, FY k and, for k < H / FY,
-// the vertical strips of footprint row k (pixel rows FY k + 1 .. FY k + FY - 2 at pixel columns
-// FX m - 1, FX m).  The cells under them (on the footprints' rings, where the fused kernel stored
-// g) are expanded once into pixel images in LDS (value at the argmax pixel, zeros elsewhere and
-// outside the image): the band image holds pixel rows FY k - 2 .. FY k + 1 (column X at X + 4),
-// the strip image pixel rows FY k .. FY k + FY - 1 x columns FX m - 2 .. FX m + 1.  Each thread
-// then runs one pixel pair through the chain of first_layer_bwd_pooled_kernel (channel
-// ascending, then dy, dx; zero terms included) with packed fmas.
-constexpr int FLB_CG = 8;   // channels per staged group of the border kernel
-
-__global__ __launch_bounds__(256) void first_layer_bwd_border_kernel(const float* __restrict__ g,
-                                                                     const uint8_t* __restrict__ amax,
-                                                                     const float* __restrict__ w2,
-                                                                     float* __restrict__ out, int C, int H, int W,
-                                                                     int clones, int TH2, int TW2) {
-  extern __shared__ __attribute__((aligned(16))) float bsm[];
-  typedef float bf2 __attribute__((ext_vector_type(2)));
-  const int tid = threadIdx.x;
-  const int H2 = H >> 1, W2 = W >> 1, FY = 2 * TH2, FX = 2 * TW2;
-  const int WB = W + 8, NM = W / FX + 1, WS = 4 * NM;
-  float* BI = bsm;                                   // [CG][4][WB]
-  float* SI = BI + (size_t)FLB_CG * 4 * WB;          // [CG][FY][WS]
-  const int k = blockIdx.x, bq = blockIdx.y, bs = bq / clones;
-  const bool vert = k < H / FY;
-  const size_t plane = (size_t)H2 * W2;
-  const float* gb = g + (size_t)bq * C * plane;
-  const uint8_t* ab = amax + (size_t)bs * C * plane;
-  // expand cell (cy, cx) of channel c into the 2 x 2 pixels at image row r0, column x0 of slot cl
-  auto cell = [&](float* img, int ws, int rows, int cl, int c, int cy, int cx, int r0, int x0) {
-    const bool ok = c < C && cy >= 0 && cy < H2 && cx >= 0 && cx < W2;
-    const size_t o = ok ? c * plane + (size_t)cy * W2 + cx : 0;
-    const float v = gb[o];
-    const int s = ok ? (int)ab[o] : 4;
-    float* d = img + ((size_t)cl * rows + r0) * ws + x0;
-    d[0] = s == 0 ? v : 0.f;
-    d[1] = s == 1 ? v : 0.f;
-    d[ws] = s == 2 ? v : 0.f;
-    d[ws + 1] = s == 3 ? v : 0.f;
-  };
-  // pair p: band pairs first (row FY k - 1 + p / (W / 2), columns 2 (p % (W / 2)) + 0, 1), then the
-  // strip pairs (row FY k + 1 + q / NM, columns FX m - 1, FX m with m = q % NM); one per thread
-  const int nband = W, nstrip = vert ? (FY - 2) * NM : 0;
-  const int p = tid;
-  int Y = -1, X0 = 0, ws = WB, cstride = 4 * WB;
-  const float* rowp = BI;   // image row of pixel row Y - 1, at the column of pixel X0 - 1
-  if (p < nband) {
-    const int r = p / (W / 2);
-    Y = k * FY - 1 + r;
-    X0 = 2 * (p % (W / 2));
-    rowp = BI + r * WB + X0 + 3;
-  } else if (p < nband + nstrip) {
-    const int q = p - nband, m = q % NM;
-    Y = k * FY + 1 + q / NM;
-    X0 = FX * m - 1;
-    rowp = SI + (Y - 1 - k * FY) * WS + 4 * m;
-    ws = WS;
-    cstride = FY * WS;
-  }
-  const bool act = p < nband + nstrip;
-  bf2 acc = bf2{0.f, 0.f};
-  for (int c0 = 0; c0 < C; c0 += FLB_CG) {
-    if (c0) __syncthreads();
-    // band: cell rows TH2 k - 1 (image rows 0, 1) and TH2 k (rows 2, 3); cell columns -2 .. W2 + 1
-    for (int i = tid; i < FLB_CG * 2 * (W2 + 4); i += 256) {
-      const int cl = i / (2 * (W2 + 4)), rem = i % (2 * (W2 + 4));
-      const int rr = rem / (W2 + 4), cx = rem % (W2 + 4) - 2;
-      cell(BI, WB, 4, cl, c0 + cl, k * TH2 - 1 + rr, cx, 2 * rr, 2 * cx + 4);
-    }
-    if (vert) {
-      // strips: cell rows TH2 k .. TH2 k + TH2 - 1, cell columns TW2 m - 1, TW2 m
-      for (int i = tid; i < FLB_CG * TH2 * 2 * NM; i += 256) {
-        const int cl = i / (TH2 * 2 * NM), rem = i % (TH2 * 2 * NM);
-        const int ry = rem / (2 * NM), j = rem % (2 * NM), m = j >> 1;
-        cell(SI, WS, FY, cl, c0 + cl, k * TH2 + ry, TW2 * m - 1 + (j & 1), 2 * ry, 4 * m + 2 * (j & 1));
-      }
-    }
-    __syncthreads();
-    if (act) {
-#pragma unroll 2
-      for (int cl = 0; cl < FLB_CG; ++cl) {
-        const int c = c0 + cl;
-        if (c >= C) break;
-        float wv[9];
-#pragma unroll
-        for (int t = 0; t < 9; ++t) wv[t] = w2[c * 9 + t];
-        const float* rp = rowp + (size_t)cl * cstride;
-#pragma unroll
-        for (int dy = -1; dy <= 1; ++dy) {
-          const float* r = rp + (dy + 1) * ws;
-          const float e0 = r[0], e1 = r[1], e2 = r[2], e3 = r[3];
-          const bf2 q0 = bf2{e0, e1}, q1 = bf2{e1, e2}, q2 = bf2{e2, e3};
-          acc = __builtin_elementwise_fma(q0, bf2{wv[(1 - dy) * 3 + 2], wv[(1 - dy) * 3 + 2]}, acc);
-          acc = __builtin_elementwise_fma(q1, bf2{wv[(1 - dy) * 3 + 1], wv[(1 - dy) * 3 + 1]}, acc);
-          acc = __builtin_elementwise_fma(q2, bf2{wv[(1 - dy) * 3], wv[(1 - dy) * 3]}, acc);
-        }
-      }
-    }
-  }
-  if (act) {
-    if (Y >= 0 && Y < H && X0 >= 0) out[((size_t)bq * H + Y) * W + X0] = acc.x;
-    if (Y >= 0 && Y < H && X0 + 1 < W) out[((size_t)bq * H + Y) * W + X0 + 1] = acc.y;
-  }
-}
-
 // den[co][y][x] = sum_ci sum_{in-bounds taps} w2[co][ci][ky][kx] * 1 + b2[co]
 __global__ void first_layer_den_kernel(const float* __restrict__ w2, const float* __restrict__ b2, float* __restrict__ den,
                                        int C, int CI, int H, int W) {
@@ -1499,33 +1394,15 @@ size_t proj_bwd_lds() { return ((size_t)D * (D + 1) + 2 * (size_t)D * 68) * size
 template <int D, bool PL>
 size_t proj_bwd_rc_lds() { return ((size_t)D * (D + 1) + 4 * 2 * (size_t)D * 16 + p_lds_floats<D, PL>()) * sizeof(float); }
 
-// Where the projection kernels keep the residual P: in LDS (DRSA_AMD_PROJ_PLDS=1, DP <= 64), else
-// the forward holds its MFMA operands in registers (unpadded DP <= 64; 0.139 ms at B = 512, d = 64,
-// vs 0.161 from LDS, which costs a workgroup per CU) and the backward reads them through L1
-// (0.524 vs 0.537 ms from LDS; registers would cost it a wave per SIMD).
-int proj_p_lds_env() {
-  static const int v = getenv("DRSA_AMD_PROJ_PLDS") ? atoi(getenv("DRSA_AMD_PROJ_PLDS")) : -1;
-  return v;
-}
-bool proj_p_lds_fwd() { return proj_p_lds_env() == 1; }
+// Where the projection kernels keep the residual P: the forward holds its MFMA operands in
+// registers (unpadded DP <= 64; 0.139 ms at B = 512, d = 64, vs 0.161 with P in LDS, which costs a
+// workgroup per CU) and the backward reads them through L1 (0.524 vs 0.537 ms from LDS; registers
+// would cost it a wave per SIMD).  The LDS form stays compiled for padded problems' fallbacks.
+bool proj_p_lds_fwd() { return false; }
 
-bool proj_p_lds_bwd() { return proj_p_lds_env() == 1; }
+bool proj_p_lds_bwd() { return false; }
 
 }  // namespace
-
-int drsa_first_layer_border(const float* g, const uint8_t* amax, const float* w2, float* out, int Bq, int clones,
-                            int C, int H, int W, int FY, int FX, hipStream_t s) {
-  DRSA_REQUIRE(FY >= 4 && FX >= 4 && FY % 2 == 0 && FX % 2 == 0 && H % FY == 0 && W % FX == 0,
-               "first_layer_border: bad footprint");
-  const size_t lds = sizeof(float) * ((size_t)FLB_CG * 4 * (W + 8) + (size_t)FLB_CG * FY * 4 * (W / FX + 1));
-  DRSA_REQUIRE(lds <= 64 * 1024 && W + (H / FY > 0 ? (FY - 2) * (W / FX + 1) : 0) <= 256,
-               "first_layer_border: %d x %d pixels do not fit one workgroup", H, W);
-  DRSA_SMEM(first_layer_bwd_border_kernel, lds);
-  hipLaunchKernelGGL(first_layer_bwd_border_kernel, dim3(H / FY + 1, Bq), dim3(256), lds, s, g, amax, w2, out, C, H,
-                     W, clones, FY / 2, FX / 2);
-  DRSA_LAUNCH_CHECK();
-  return DRSA_OK;
-}
 
 extern "C" {
 
@@ -1695,8 +1572,7 @@ int drsa_amd_heatmap_sort(const float* hm, int B, int K, int HW, int std_from_su
                           float* sub_out, float* rel, int64_t* mask, void* stream) {
   DRSA_REQUIRE(K >= 1 && K <= 64, "heatmap_sort: K must be in [1, 64]");
   DRSA_REQUIRE(HW % 4 == 0, "heatmap_sort: H*W must be a multiple of 4");
-  static const int no_cache = getenv("DRSA_AMD_SORT_GENERIC") ? atoi(getenv("DRSA_AMD_SORT_GENERIC")) : 0;
-  if (K == 4 && HW == 16384 && !no_cache) {
+  if (K == 4 && HW == 16384) {
     auto kern = std_from_sum ? heatmap_sort_cached_kernel<4, 16, true> : heatmap_sort_cached_kernel<4, 16, false>;
     hipLaunchKernelGGL(kern, dim3(B), dim3(256), 0, (hipStream_t)stream, hm, std_out, std_rel, sub_out, rel, mask);
   } else {

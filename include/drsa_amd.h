@@ -231,24 +231,6 @@ int drsa_amd_conv_bwd_den_ring(const float* g, const uint8_t* g_amax, const void
 /* 1 if drsa_amd_conv_bwd_bf16 has a kernel for this shape (sparse: g at 2x2-pool resolution). */
 int drsa_amd_conv_bwd_has_kernel_bf16(int cin, int cout, int W, int ng, int sparse);
 
-/* The backward of the layer above a WSquare first layer under a 2x2 max-pool, with that first
- * layer's w^2 contraction (drsa_amd_first_layer_bwd, pooled; lrp.py's input-layer rule via
- * attribute.py:98-107) fused into its epilogue: fp32 conv_bwd (pool-sparse g, xmode = XM_MUL,
- * post = POST_DIV with den, or POST_DIV_RING with den = den_ring and den_const4 when den_const4 is
- * not NULL) whose R never makes the round trip through HBM.  Each 8 x 32-cell tile re-lays its R
- * as the first layer's unpooled g (the argmax pixel of each cell, first_amax [B][cout][H][W]) in
- * LDS and contracts it with first_w2 [cout][9] into first_out [Bq][2H][2W] in the dense chain's
- * order (channel ascending, then dy, dx); `out` receives R only on the tiles' border cell rings,
- * from which a second kernel computes the footprints' border pixels.  first_out is bit-identical
- * to drsa_amd_conv_bwd (or _den_ring) + drsa_amd_first_layer_bwd; `out` is NOT the full R.
- * Needs cout == 32 (the first layer's channels), H % 8 == 0, W % 32 == 0, W <= 96; H, W at pooled
- * resolution.  drsa_amd_conv_bwd_has_kernel_first_fused reports support for (cin, cout, H, W). */
-int drsa_amd_conv_bwd_first_fused(const float* g, const uint8_t* g_amax, const float* wts, const float* x,
-                                  const float* den, const float* den_const4, const uint8_t* first_amax,
-                                  const float* first_w2, float* out, float* first_out, int Bq, int clones, int cin,
-                                  int cout, int H, int W, float eps, void* stream);
-int drsa_amd_conv_bwd_has_kernel_first_fused(int cin, int cout, int H, int W);
-
 /* Dense layer forward: z = x W^T + b [, relu(z)]  (classifier Linear layers). */
 int drsa_amd_linear_fwd(const float* x, const float* W, const float* bias, float* z_out, float* relu_out, int M,
                         int N, int K, void* stream);

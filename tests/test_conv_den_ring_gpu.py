@@ -7,7 +7,7 @@ Parity: bit-identical to drsa_amd_conv_fwd (map den, 2x2 pool) + drsa_amd_conv_b
 the full copy, for fp32 and bf16 backward weights, dense and pool-sparse g, Epsilon-type (XM_MUL)
 and plain (XM_NONE) rules, clones > 1 -- with the copy's interior filled with NaN, so a read of a
 value the ring forward did not store would show; plus the engine at plan level (GTZAN standard
-LRP and HeatmapGenerator) against DRSA_AMD_DEN_COPY=1."""
+LRP and HeatmapGenerator) against the per-sample copy (plan._DEN_COPY)."""
 import numpy as np
 import pytest
 import torch
@@ -127,7 +127,7 @@ def test_ring_entries_reject_missing_operands():
 
 @pytest.mark.parametrize("hg", [False, True])
 def test_plan_ring_equals_den_copy(monkeypatch, hg):
-    """The engine with the ring form (default) and with the full copy (DRSA_AMD_DEN_COPY=1) gives
+    """The engine with the ring form (default) and with the full copy (plan._DEN_COPY) gives
     identical relevances / heatmaps (GTZAN: WSquare first layer, 2x2 pool)."""
     import copy
     import drsa_audio_amd.engine.plan as plan
@@ -201,7 +201,7 @@ def test_conv_bwd_den_map_equals_post_div_on_copy(cin, H, W, sparse, bf16, pool_
 @pytest.mark.parametrize("bf16_bwd", [False, True])
 def test_vggish_plan_den_map_equals_den_copy(monkeypatch, bf16_bwd):
     """VGGish-BN (WSquare conv0 -> conv3, no pool between): the plan reading the map itself equals
-    the plan with the per-sample copy (DRSA_AMD_DEN_COPY=1), fp32 and bf16-backward plans."""
+    the plan with the per-sample copy (plan._DEN_COPY), fp32 and bf16-backward plans."""
     import drsa_audio_amd.engine.plan as plan
     from drsa_audio_amd.engine import clear_cache
     from drsa_audio_amd.utils.constants import LRP_NAME_MAP_VGGISH
