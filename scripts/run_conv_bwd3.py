@@ -4,7 +4,7 @@ import os, sys, torch, json
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from drsa_audio_amd import _capi
 dev = torch.device("cuda")
-Bs, clones = 512, 5
+Bs, clones = 512, 4
 Bq = Bs * clones
 g = torch.randn(Bq, 32, 32, 32, device=dev)
 amax = torch.randint(0, 4, (Bs, 32, 32, 32), device=dev, dtype=torch.uint8)
