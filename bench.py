@@ -625,9 +625,9 @@ def main():
     ap.add_argument("--pipeline-samples", type=int, default=1000, help="samples per rank of the rank-local C4 leg")
     ap.add_argument("--pipeline-steps", type=int, default=100, help="DRSA steps of the rank-local C4 leg")
     ap.add_argument("--legs", default="all",
-                    help="secondary legs to run: all, or a comma list of " + ",".join(LEGS))
+                    help="secondary legs to run: all, none, or a comma list of " + ",".join(LEGS))
     args = ap.parse_args()
-    legs = set(LEGS) if args.legs == "all" else set(args.legs.split(","))
+    legs = set(LEGS) if args.legs == "all" else set() if args.legs == "none" else set(args.legs.split(","))
     if not legs <= set(LEGS):
         ap.error(f"--legs: unknown {sorted(legs - set(LEGS))}")
     if args.no_drsa:

@@ -231,7 +231,9 @@ __device__ __forceinline__ void stage_u_padded(float* Us, const float* __restric
   }
 }
 
-template <int DP, bool PAD, bool PLDS>
+// HOUT = false (the plan's default: projection_bwd recomputes h): only the residual GEMM
+// delta = a P runs and U is not staged -- h = a U is needed by nobody (a' = a + delta).
+template <int DP, bool PAD, bool PLDS, bool HOUT>
 __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __restrict__ a, const float* __restrict__ U,
                                                             const float* __restrict__ Pm,
                                                             float* __restrict__ h, float* __restrict__ ap,
@@ -240,8 +242,8 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
   const int d = PAD ? d_in : DP;   // PAD = false: d == DP at compile time (no padding code)
   constexpr int P = 64, LD = DP + 1, PL = P + 4;
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* Us = sm;               // [DP][LD]   U[c][j]
-  float* as = Us + DP * LD;     // [DP][PL]   a tile, then a' tile
+  float* Us = sm;               // [DP][LD]   U[c][j] (HOUT only)
+  float* as = Us + (HOUT ? DP * LD : 0);   // [DP][PL]   a tile, then a' tile
   float* Ps = as + DP * PL;     // [DP][DP + 16] P (when PLDS)
   const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
   const int b = blockIdx.y;
@@ -250,9 +252,9 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
   const int d4 = (d + 3) & ~3;
   // per-sample bases + 32-bit per-lane offsets (saddr + voffset addressing; d * H * W < 2^31)
   const float* __restrict__ a_b = a + (size_t)b * d * HW;
-  float* __restrict__ h_b = h ? h + (size_t)b * d * HW : nullptr;
+  float* __restrict__ h_b = HOUT ? h + (size_t)b * d * HW : nullptr;
   float* __restrict__ ap_b = ap ? ap + (size_t)b * d * HW : nullptr;
-  stage_u_padded<DP>(Us, U, d, tid);
+  if constexpr (HOUT) stage_u_padded<DP>(Us, U, d, tid);
   if constexpr (PLDS) stage_p<DP>(Ps, Pm, d, tid);
   constexpr int NB = DP / 16;
   // unpadded DP <= 64: the residual's MFMA A operands (P[c][k], read as the symmetric P[k][c]) live
@@ -321,7 +323,7 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
           const float bv = as[c * PL + w * 16 + (lane & 15)];
 #pragma unroll
           for (int jb = 0; jb < NB; ++jb) {
-            acc[jb] = mfma16(Us[c * LD + jb * 16 + (lane & 15)], bv, acc[jb]);
+            if constexpr (HOUT) acc[jb] = mfma16(Us[c * LD + jb * 16 + (lane & 15)], bv, acc[jb]);
             dl[jb] = mfma16(preg[jb * (DP / 4) + k0 / 4], bv, dl[jb]);
           }
         }
@@ -332,7 +334,7 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
           const float bv = as[c * PL + w * 16 + (lane & 15)];
 #pragma unroll
           for (int jb = 0; jb < NB; ++jb) {
-            acc[jb] = mfma16(Us[c * LD + jb * 16 + (lane & 15)], bv, acc[jb]);
+            if constexpr (HOUT) acc[jb] = mfma16(Us[c * LD + jb * 16 + (lane & 15)], bv, acc[jb]);
             dl[jb] = mfma16(p_op<DP, PLDS>(Ps, Pm, d, jb * 16 + (lane & 15), c), bv, dl[jb]);
           }
         }
@@ -344,7 +346,7 @@ __global__ __launch_bounds__(256) void projection_fwd_kernel(const float* __rest
         for (int r = 0; r < 4; ++r) {
           const int j = jb * 16 + (lane >> 4) * 4 + r, p = w * 16 + (lane & 15);
           const int og = j * HW + (y0 + p / TW) * W + x0 + p % TW;
-          if (h_b && j < d) h_b[og] = acc[jb][r];
+          if (HOUT && j < d) h_b[og] = acc[jb][r];
           const float v = as[j * PL + p] + dl[jb][r];
           as[j * PL + p] = v;   // a tile no longer needed: holds a' now
           if (ap_b && j < d) ap_b[og] = v;
@@ -874,33 +876,28 @@ __global__ __launch_bounds__(256) void first_layer_bwd_kernel(const float* __res
 #ifndef DRSA_FQ_WPE
 #define DRSA_FQ_WPE 8
 #endif
+// 1: the 6 x 6 patch streamed row by row (one row of pairs live: fewer VGPRs, more waves)
+#ifndef DRSA_FQ_STREAM
+#define DRSA_FQ_STREAM 1
+#endif
 constexpr int FQ_Y = 16, FQ_X = 64, FQ_C = DRSA_FQ_C;
 constexpr int FQ_RY = FQ_Y + 2, FQ_RX = FQ_X + 2;            // cells incl. halo
 constexpr int FQ_PY = 2 * FQ_RY, FQ_PX = 2 * FQ_RX + 4;      // pixel image (row pad 4)
 constexpr int FQ_KR = (FQ_RY + 3) / 4;                       // row passes of 4 waves
-// image column of the halo origin: 2 puts every cell's pixel pair on an 8-byte boundary (one
-// ds_write_b64 per cell row, consecutive lanes: conflict-free) and a thread's own 4 pixels of a patch
-// row (columns 4tx + 4 .. 4tx + 7) on a 16-byte boundary (one ds_read_b128); the window's outer two
-// pixels are the neighbour lanes' (DPP wave shifts), or the halo columns for the tile's edge threads.
-// (Origin 3 -- one ds_read_b128 + one 2-way-conflicted ds_read_b64 per row, and two ds_write2_b32 per
-// cell -- kept the LDS busy 70 % of the kernel, 44 % of it bank conflicts: 0.37 ms at the bench shape.)
-constexpr int FQ_C0 = 2;
+// image column of the halo origin: 3 puts every thread's 6-pixel window (starting at 4tx + 4) on
+// a 16-byte boundary, so a row of it is one ds_read_b128 + one ds_read_b64 over consecutive lanes
+// (bank-conflict free; the former origin 1 gave 8-byte reads at a 16-byte lane stride)
+constexpr int FQ_C0 = 3;
+constexpr int FQ_NS = FQ_C * FQ_KR + 1;                      // staged cells per thread
 
 typedef float fq2 __attribute__((ext_vector_type(2)));
-constexpr int FQ_NS = FQ_C * FQ_KR + 1;                      // staged cells per thread
 
 __device__ __forceinline__ void fq_put(float* img, int ci, int ry, int rx, float v, int sb) {
   float* d = img + (ci * FQ_PY + 2 * ry) * FQ_PX + 2 * rx + FQ_C0;
-  *reinterpret_cast<fq2*>(d) = fq2{sb == 0 ? v : 0.f, sb == 1 ? v : 0.f};
-  *reinterpret_cast<fq2*>(d + FQ_PX) = fq2{sb == 2 ? v : 0.f, sb == 3 ? v : 0.f};
-}
-
-// the value of lane l - 1 (wave_shr:1) / l + 1 (wave_shl:1) of the wave
-__device__ __forceinline__ float fq_from_left(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xf, 0xf, false));
-}
-__device__ __forceinline__ float fq_from_right(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, false));
+  d[0] = sb == 0 ? v : 0.f;
+  d[1] = sb == 1 ? v : 0.f;
+  d[FQ_PX] = sb == 2 ? v : 0.f;
+  d[FQ_PX + 1] = sb == 3 ? v : 0.f;
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRSA_FQ_WPE))) void first_layer_bwd_pooled_kernel(const float* __restrict__ g,
@@ -976,21 +973,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRSA_FQ_WPE
 #pragma unroll
       for (int t = 0; t < 9; ++t) wv[t] = (c < C) ? w2[c * 9 + t] : 0.f;
       // patch P[i][j] = pixel (2qy0 + 4ty - 1 + i, 2qx0 + 4tx - 1 + j) = img[4ty + 1 + i][4tx + FQ_C0 + 1 + j];
-      // pair q (q = 0..4) = (P[i][q], P[i][q + 1]).  P[i][1..4] is this thread's aligned float4;
-      // P[i][0] / P[i][5] are lane tx - 1's .w / lane tx + 1's .x (the wave holds tile rows ty and
-      // ty + 1 as lanes 0-31 and 32-63), or the halo columns at tx = 0 / 31
-      const float* base = img + (ci * FQ_PY + 4 * ty + 1) * FQ_PX + 4 * tx + FQ_C0 + 2;
-      const int ecol = (tx == 0 ? FQ_C0 + 1 : 4 * (FQ_X / 2) + FQ_C0 + 2) - (4 * tx + FQ_C0 + 2);
+      // pair q (q = 0..4) = (P[i][q], P[i][q + 1])
+      const float* base = img + (ci * FQ_PY + 4 * ty + 1) * FQ_PX + 4 * tx + FQ_C0 + 1;
+#if DRSA_FQ_STREAM
       // patch rows streamed: row i feeds output rows py = i - 1 - dy, i.e. each output row takes
       // its taps in dy order (then dx) -- the chain order -- with only one patch row live
 #pragma unroll
       for (int i = 0; i < 6; ++i) {
         const float* r = base + i * FQ_PX;
         const float4 q4 = *reinterpret_cast<const float4*>(r);
-        const float e = r[ecol];
-        const float pl = fq_from_left(q4.w), pr5 = fq_from_right(q4.x);
-        const float p0 = tx == 0 ? e : pl, p5 = tx == FQ_X / 2 - 1 ? e : pr5;
-        const fq2 rp[5] = {fq2{p0, q4.x}, fq2{q4.x, q4.y}, fq2{q4.y, q4.z}, fq2{q4.z, q4.w}, fq2{q4.w, p5}};
+        const fq2 q2 = *reinterpret_cast<const fq2*>(r + 4);
+        const fq2 rp[5] = {fq2{q4.x, q4.y}, fq2{q4.y, q4.z}, fq2{q4.z, q4.w}, fq2{q4.w, q2.x}, q2};
 #pragma unroll
         for (int py = 0; py < 4; ++py) {
           const int dy = i - py - 1;
@@ -1004,6 +997,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRSA_FQ_WPE
           }
         }
       }
+#else
+      fq2 pr[6][5];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const float* r = base + i * FQ_PX;
+        const float4 q4 = *reinterpret_cast<const float4*>(r);
+        const fq2 q2 = *reinterpret_cast<const fq2*>(r + 4);
+        pr[i][0] = fq2{q4.x, q4.y};
+        pr[i][1] = fq2{q4.y, q4.z};
+        pr[i][2] = fq2{q4.z, q4.w};
+        pr[i][3] = fq2{q4.w, q2.x};
+        pr[i][4] = q2;
+      }
+#pragma unroll
+      for (int py = 0; py < 4; ++py)
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+          for (int dx = -1; dx <= 1; ++dx) {
+            const float w = wv[(1 - dy) * 3 + (1 - dx)];
+            const fq2 ww = fq2{w, w};
+            acc[py][0] = __builtin_elementwise_fma(pr[py + 1 + dy][1 + dx], ww, acc[py][0]);
+            acc[py][1] = __builtin_elementwise_fma(pr[py + 1 + dy][3 + dx], ww, acc[py][1]);
+          }
+#endif
     }
   };
 #if FQ_DEPTH2
@@ -1372,7 +1390,9 @@ int with_lds(F* fn, size_t lds) {
 int proj_dp(int d) { return d < 1 ? 0 : d <= 16 ? 16 : d <= 32 ? 32 : d <= 64 ? 64 : d <= 128 ? 128 : 0; }
 
 template <int D, bool PL>
-size_t proj_fwd_lds() { return ((size_t)D * (D + 1) + (size_t)D * 68 + p_lds_floats<D, PL>()) * sizeof(float); }
+size_t proj_fwd_lds(bool hout) {
+  return ((hout ? (size_t)D * (D + 1) : 0) + (size_t)D * 68 + p_lds_floats<D, PL>()) * sizeof(float);
+}
 template <int D>
 size_t proj_bwd_lds() { return ((size_t)D * (D + 1) + 2 * (size_t)D * 68) * sizeof(float); }
 template <int D, bool PL>
@@ -1445,9 +1465,11 @@ int drsa_amd_projection_fwd(const float* a, const float* U, const float* P, floa
   case DD: {                                                                                          \
     constexpr bool PLC = DD <= 64;                                                                  \
     const bool pl = PLC && proj_p_lds_fwd();                                                        \
-    auto kf = D == DD ? (pl ? projection_fwd_kernel<DD, false, PLC> : projection_fwd_kernel<DD, false, false>)  \
-                      : (pl ? projection_fwd_kernel<DD, true, PLC> : projection_fwd_kernel<DD, true, false>);   \
-    const size_t lds = pl ? proj_fwd_lds<DD, PLC>() : proj_fwd_lds<DD, false>();                    \
+    auto kf = h ? (D == DD ? (pl ? projection_fwd_kernel<DD, false, PLC, true> : projection_fwd_kernel<DD, false, false, true>)   \
+                           : (pl ? projection_fwd_kernel<DD, true, PLC, true> : projection_fwd_kernel<DD, true, false, true>))   \
+                : (D == DD ? (pl ? projection_fwd_kernel<DD, false, PLC, false> : projection_fwd_kernel<DD, false, false, false>) \
+                           : (pl ? projection_fwd_kernel<DD, true, PLC, false> : projection_fwd_kernel<DD, true, false, false>)); \
+    const size_t lds = pl ? proj_fwd_lds<DD, PLC>(h != nullptr) : proj_fwd_lds<DD, false>(h != nullptr);  \
     { int rc = with_lds(kf, lds); if (rc) return rc; }                                              \
     hipLaunchKernelGGL(kf, grid, dim3(256), lds, s, a, U, P, h, ap, pooled, amax,                    \
                        D, H, W, pool);                                                                \
