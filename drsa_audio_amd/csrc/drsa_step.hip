@@ -790,8 +790,22 @@ __device__ __forceinline__ double finish_prologue(const float* __restrict__ gs, 
                                                   const float* __restrict__ U, float* X, bool build_x,
                                                   double* dterm, float* cvec, double* fsh) {
   constexpr int PD = polar_dim<DP>(), NT = fin_threads<PD>(), LD = ns_ld<PD>();
+  constexpr int NQ = (PD * PD + NT - 1) / NT;
   const int tid = threadIdx.x;
   const int dk = d / K;
+  // X's U and G entries are loaded first, so their memory latency overlaps the f / c stages
+  // (loads from clamped addresses, pinned, so all of them are in flight at once: no exec branches)
+  float uq[NQ], gq[NQ];
+  if (build_x) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int e = tid + q * NT;
+      const int ip = e / PD, jp = e % PD, kc = jp / DKP, l = jp % DKP;
+      const bool real = e < PD * PD && ip < d && jp < DP && kc < K && l < dk;
+      uq[q] = U[real ? (size_t)ip * d + kc * dk + l : 0];
+      gq[q] = gs[real ? ip * DP + jp : 0];
+    }
+  }
   if (tid < K) dterm[tid] = sqrt(sqrt((double)gs[DP * DP + tid] / n_total));
   __syncthreads();
   if (tid == 0) {
@@ -808,14 +822,12 @@ __device__ __forceinline__ double finish_prologue(const float* __restrict__ gs, 
   }
   if (!build_x) return f;
   __syncthreads();
-  // (loads from clamped addresses, pinned, so all of them are in flight at once: no exec branches)
 #pragma unroll
-  for (int q = 0; q < (PD * PD + NT - 1) / NT; ++q) {
+  for (int q = 0; q < NQ; ++q) {
     const int e = tid + q * NT;
     const int ip = e / PD, jp = e % PD, kc = jp / DKP, l = jp % DKP;
     const bool real = e < PD * PD && ip < d && jp < DP && kc < K && l < dk;
-    const float u = U[real ? (size_t)ip * d + kc * dk + l : 0];
-    const float gv = gs[real ? ip * DP + jp : 0];
+    const float u = uq[q], gv = gq[q];
     const float rv = keep_or_zero(u + gv * cvec[kc < K ? kc : 0], real);
     const float v = ip < d ? rv : ((jp == pad_col(ip - d, K, dk, DKP)) ? 1.f : 0.f);
     if (e < PD * PD) X[ip * LD + jp] = v;
@@ -863,6 +875,269 @@ __global__ __launch_bounds__(fin_threads<polar_dim<DP>()>()) void drsa_finish_ke
     int mode, float tol, int max_iter, int* __restrict__ iters_out) {
   finish_body<DP>(gs, n_total, d, K, DKP, U, U_out, f_out, step_counter, f_stride_by_counter, mode, tol, max_iter,
                   iters_out);
+}
+
+// ---------------------------------------------------------------------------
+// Cooperative finish at DP = 128 (drsa_run / run_multi, the C5 shapes): the polar's two 128^3
+// products per Newton-Schulz iteration split over kCoopWG workgroups on as many CUs, workgroup j
+// owning the 32 columns [32 j, 32 j + 32) of X.  Per iteration workgroup j forms P_j = X^T X[:, j]
+// (4 tiles), T_j = 1.5 I - 0.5 P_j with its max |P_j - I|, and X'[:, j] = X T_j (4 tiles); the new
+// column blocks and the error maxima are exchanged through the workspace (one hand-off per
+// iteration: agent-scope stores, a ticket counter, agent-scope loads), so every workgroup holds
+// the whole X' for the next P.  Bit-identical to drsa_finish_kernel's single-workgroup polar_ns:
+//   * every P / X T entry is the same full-k fp32 MFMA chain (P's lower tiles there are mirrored
+//     from the upper ones, here computed directly: x_k y_k = y_k x_k exactly);
+//   * tr(P) from P's diagonal (each workgroup hands its diagonal tile's 32 entries over), folded in
+//     the same order; the inf-norm row sums as column sums of workgroup j's block (P is exactly
+//     symmetric), in the same order; maxima are order-free;
+//   * the X T of an iteration whose error stops the loop is computed speculatively (the error is
+//     exchanged with its result) and dropped, so the returned X is the one polar_ns returns.
+// The workgroups spin on each other: the launch needs kCoopWG co-resident workgroups (one per CU,
+// 150 KB of LDS each), which the callers guarantee by launching nothing else that waits on them; a
+// spin that outlives kCoopSpinTicks (100 ms) gives up and poisons U_out with NaN instead of hanging.
+// ---------------------------------------------------------------------------
+constexpr int kCoopWG = 4;
+constexpr long long kCoopSpinTicks = 10000000;   // s_memrealtime runs at 100 MHz
+
+// diagnostic build (-DDRSA_COOP_STAMP, scripts/probe_coop.py): phase times of the last launch's
+// workgroups, read back by drsa_amd_debug_coop_stamps; nothing in the kernel reads them
+#ifdef DRSA_COOP_STAMP
+__device__ unsigned long long g_coop_stamps[kCoopWG][64];
+#define COOP_STAMP(slot) do { if (threadIdx.x == 0 && (slot) < 64) g_coop_stamps[blockIdx.x][(slot)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define COOP_STAMP(slot)
+#endif
+
+struct CoopXchg {
+  float xb[2][128 * 128];        // X' by iteration parity (column block j written by workgroup j)
+  float sc[2][kCoopWG][4];       // per parity and workgroup: error max, inf-norm partial
+  unsigned ticket;               // hand-off counter: kCoopWG arrivals per exchange, never reset
+  unsigned pad[63];
+};
+
+__device__ __forceinline__ void coop_st(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float coop_ld(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// every thread calls after its agent-scope stores; returns false if the other workgroups did not
+// arrive within kCoopSpinTicks
+__device__ bool coop_exchange(unsigned* ticket, int* ok_sh) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = (old / kCoopWG + 1) * kCoopWG;
+    const long long t0 = wall_clock64();
+    int ok = 1;
+    for (;;) {
+      const unsigned v = __hip_atomic_load(ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((int)(v - target) >= 0) break;
+      if (wall_clock64() - t0 > kCoopSpinTicks) { ok = 0; break; }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    *ok_sh = ok;
+  }
+  __syncthreads();
+  return *ok_sh != 0;
+}
+
+constexpr int kCoopTLD = 32;   // T_j row stride (one 32-column block)
+constexpr size_t coop_lds_bytes() {
+  return ((size_t)2 * 128 * ns_ld<128>() + (size_t)128 * kCoopTLD + 64) * sizeof(float);
+}
+
+__global__ __launch_bounds__(1024) void drsa_finish_coop_kernel(
+    const float* __restrict__ gs, double n_total, int d, int K, int DKP, const float* __restrict__ U,
+    float* __restrict__ U_out, float* __restrict__ f_out, int* __restrict__ step_counter, int f_stride_by_counter,
+    float tol, int max_iter, CoopXchg* __restrict__ xc) {
+  constexpr int DP = 128, LD = ns_ld<DP>(), NT = 1024, TLD = kCoopTLD, TPR = NT / DP;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* X = smem;                 // current X (full)
+  float* Xn = X + DP * LD;         // X' being assembled
+  float* Tj = Xn + DP * LD;        // T_j = 1.5 I - 0.5 P[:, j-block]
+  float* red = Tj + DP * TLD;      // 64 floats
+  __shared__ double dterm[128];
+  __shared__ float cvec[128];
+  __shared__ double fsh;
+  __shared__ float diag[128];
+  __shared__ int ok_sh;
+  const int tid = threadIdx.x, lane = lane_id(), w = wave_id(), j = blockIdx.x;
+  const int lo = lane & 31, hi = lane >> 5;
+  const int dk = d / K;
+  COOP_STAMP(0);
+  const double f = finish_prologue<DP>(gs, n_total, d, K, DKP, U, X, true, dterm, cvec, &fsh);
+  bool ok = true;
+  COOP_STAMP(1);
+
+  // P_j tile (ib = w) of X^T X[:, j-block] for waves 0..3: Tj[row][col - 32 j] = raw P (it == 0) or
+  // 1.5 I - 0.5 P with err (it > 0)
+  auto gram_block = [&](int it, float& err) {
+    __syncthreads();   // X complete
+    if (w < 4) {
+      f32x16 acc = {};
+#pragma unroll 8
+      for (int k0 = 0; k0 < DP; k0 += 2) {
+        const int kk = k0 + hi;
+        acc = mfma32(X[kk * LD + 32 * w + lo], X[kk * LD + 32 * j + lo], acc);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = 32 * w + t32_row(r, hi);
+        float v = acc[r];
+        if (it > 0) {
+          const bool dg = row == 32 * j + lo;
+          err = fmaxf(err, fabsf(v - (dg ? 1.f : 0.f)));
+          v = (dg ? 1.5f : 0.f) - 0.5f * v;
+        }
+        Tj[row * TLD + lo] = v;
+      }
+    }
+  };
+  // X'[:, j-block] = X T_j for waves 0..3 (tile ib = w): into Xn and the exchange buffer
+  auto xt_block = [&](int par) {
+    __syncthreads();   // T_j complete
+    if (w < 4) {
+      f32x16 acc = {};
+#pragma unroll 8
+      for (int kr = 0; kr < DP; kr += 2) {
+        const int kk = kr + hi;
+        acc = mfma32(X[(32 * w + lo) * LD + kk], Tj[kk * TLD + lo], acc);
+      }
+      float* xg = xc->xb[par];
+      int l = lane;
+      asm volatile("" : "+v"(l));
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = 32 * w + t32_row(r, l >> 5), col = 32 * j + (l & 31);
+        Xn[row * LD + col] = acc[r];
+        coop_st(&xg[row * DP + col], acc[r]);
+      }
+    }
+  };
+  // the other workgroups' column blocks of X' (after the exchange)
+  // (all loads issued before the first LDS store: one memory round trip, not 12)
+  auto gather_blocks = [&](int par) {
+    constexpr int NQ = (kCoopWG - 1) * 32 * DP / NT;
+    const float* xg = xc->xb[par];
+    unsigned t = (unsigned)tid;
+    asm volatile("" : "+v"(t));   // addresses per call: hoisted out of the iteration loop they spill
+    float v[NQ];
+    unsigned lds[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const unsigned e = t + (unsigned)q * NT;  // over the 3 foreign blocks, 32-float runs
+      const unsigned bi = e >> 12, rem = e & 4095u;
+      const unsigned blk = bi < (unsigned)j ? bi : bi + 1;
+      const unsigned row = rem >> 5, col = 32 * blk + (rem & 31u);
+      v[q] = coop_ld(&xg[row * DP + col]);
+      lds[q] = row * LD + col;
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) Xn[lds[q]] = v[q];
+  };
+
+  // ---- iteration 0: raw P_j, scaling a^2 = DP / tr(P) unless a^2 ||P||_inf >= 2.9 ----
+  float err = 0.f, rowmax_all;
+  gram_block(0, err);
+  __syncthreads();   // Tj (raw P) complete
+  COOP_STAMP(2);
+  // row sums of |P| for the rows of block j, as column sums of P[:, j-block] (polar_ns's order)
+  float rs = 0.f;
+  if (tid < 32 * TPR) {
+    const int cl = tid / TPR, part = tid % TPR;
+#pragma unroll
+    for (int c = part; c < DP; c += TPR) rs += fabsf(Tj[c * TLD + cl]);
+  }
+  for (int m = 1; m < TPR; m <<= 1) rs += shfl_xor(rs, m);
+  const float rmax_j = block_max<NT>(tid < 32 * TPR ? rs : 0.f, red);
+  // hand-off 0: block j's diagonal of P (its own diagonal tile) and its inf-norm partial
+  if (tid < 32) {
+    const int i = 32 * j + tid;
+    coop_st(&xc->xb[0][i * DP + i], Tj[i * TLD + tid]);
+  }
+  if (tid == 0) coop_st(&xc->sc[0][j][1], rmax_j);
+  COOP_STAMP(3);
+  ok = coop_exchange(&xc->ticket, &ok_sh);
+  COOP_STAMP(4);
+  {
+    const float dv = coop_ld(&xc->xb[0][(tid & (DP - 1)) * (DP + 1)]);
+    float rm[kCoopWG];
+#pragma unroll
+    for (int i = 0; i < kCoopWG; ++i) rm[i] = coop_ld(&xc->sc[0][i][1]);
+    if (tid < DP) diag[tid] = dv;
+    rowmax_all = rm[0];
+#pragma unroll
+    for (int i = 1; i < kCoopWG; ++i) rowmax_all = fmaxf(rowmax_all, rm[i]);
+  }
+  const float rowmax = rowmax_all;
+  __syncthreads();   // diag complete
+  float tr = 0.f;
+  for (int i = lane; i < DP; i += 64) tr += diag[i];
+  for (int m = 32; m >= 1; m >>= 1) tr += shfl_xor(tr, m);
+  float a2 = (float)DP / tr;
+  if (a2 * rowmax >= 2.9f) a2 = 1.f / rowmax;
+  const float a = sqrtf(a2);
+  for (int e = tid; e < DP * DP; e += NT) {
+    const int r = e / DP, c = e % DP;
+    X[r * LD + c] *= a;
+  }
+  for (int e = tid; e < DP * 32; e += NT) {
+    const int r = e / 32, cl = e % 32;
+    const float pv = Tj[r * TLD + cl] * a2;
+    const bool dg = r == 32 * j + cl;
+    err = fmaxf(err, fabsf(pv - (dg ? 1.f : 0.f)));
+    Tj[r * TLD + cl] = (dg ? 1.5f : 0.f) - 0.5f * pv;
+  }
+  err = block_max<NT>(err, red);
+  COOP_STAMP(5);
+
+  int it = 0;
+  float err_prev = 1.f;
+  for (; ok; ++it) {
+    const int par = (it + 1) & 1;   // parity 0 carried iteration 0's scalars
+    xt_block(par);                   // speculative: dropped below if err stops the loop
+    if (tid == 0) coop_st(&xc->sc[par][j][0], err);
+    COOP_STAMP(6 + 5 * it);
+    ok = coop_exchange(&xc->ticket, &ok_sh);
+    COOP_STAMP(7 + 5 * it);
+    if (!ok) break;
+    float ev[kCoopWG];
+#pragma unroll
+    for (int i = 0; i < kCoopWG; ++i) ev[i] = coop_ld(&xc->sc[par][i][0]);
+    gather_blocks(par);
+    float e_all = ev[0];
+#pragma unroll
+    for (int i = 1; i < kCoopWG; ++i) e_all = fmaxf(e_all, ev[i]);
+    if (e_all < tol || it >= max_iter) break;   // X stays (polar_ns breaks before the update)
+    const bool last = (float)DP * e_all < DRSA_NS_LAST || (it > 0 && err_prev < 1e-4f && e_all > 0.25f * err_prev);
+    err_prev = e_all;
+    float* t = X; X = Xn; Xn = t;
+    if (last) { ++it; break; }
+    COOP_STAMP(8 + 5 * it);
+    err = 0.f;
+    gram_block(it + 1, err);
+    COOP_STAMP(9 + 5 * it);
+    err = block_max<NT>(err, red);
+    COOP_STAMP(10 + 5 * it);
+  }
+  __syncthreads();
+  COOP_STAMP(60);
+  // U_out: workgroup j writes the real entries of its padded column block
+#pragma unroll
+  for (int q = 0; q < DP * 32 / NT; ++q) {
+    const int e = tid + q * NT, i = e >> 5, pc = 32 * j + (e & 31);
+    const int kc = pc / DKP, l = pc % DKP;
+    if (i < d && kc < K && l < dk) U_out[i * d + kc * dk + l] = ok ? X[i * LD + pc] : __builtin_nanf("");
+  }
+  if (j == 0 && tid == 0) {
+    const int slot = f_stride_by_counter ? *step_counter : 0;
+    f_out[slot] = (float)f;
+    if (f_stride_by_counter) *step_counter = slot + 1;
+  }
+  COOP_STAMP(61);
 }
 
 // ---------------------------------------------------------------------------
@@ -1112,10 +1387,12 @@ int fused_step(const float* A, const float* C, int64_t N, double n_total, const 
   return launch_reduce(partials, pl, g, gs_out, s);
 }
 
-// workspace layout: [partials grid*E] [gs E] [16 B pad]
+// workspace layout: [partials grid*E] [gs E] [16 B pad]; DP = 128 adds the cooperative finish's
+// exchange area (CoopXchg) at the next 256-B boundary after gs
 size_t ws_bytes(int64_t N, const Geom& g) {
   const PartialPlan pl = plan_partial(N);
-  return ((size_t)pl.grid * slab_stride(g) + slab_floats(g)) * sizeof(float) + 64;
+  const size_t base = ((size_t)pl.grid * slab_stride(g) + slab_floats(g)) * sizeof(float) + 64;
+  return g.DP == 128 ? base + 256 + sizeof(CoopXchg) : base;
 }
 
 int partial_impl(const void* A, const void* C, int64_t N, int d, int K, const float* U, float* gs_out, void* ws,
@@ -1146,12 +1423,49 @@ float* ws_gs(void* ws, int64_t N, const Geom& g) {
   return (float*)ws + (size_t)plan_partial(N).grid * slab_stride(g);
 }
 
+CoopXchg* ws_xchg(void* ws, int64_t N, const Geom& g) {
+  if (g.DP != 128) return nullptr;
+  const uintptr_t e = (uintptr_t)(ws_gs(ws, N, g) + slab_floats(g));
+  return (CoopXchg*)((e + 255) / 256 * 256);
+}
+
+// the exchange counter starts at 0 (kCoopWG arrivals per hand-off from there)
+int coop_reset(CoopXchg* xc, hipStream_t s) {
+  if (xc) DRSA_HIP(hipMemsetAsync(&xc->ticket, 0, sizeof(unsigned), s));
+  return DRSA_OK;
+}
+
+// a full finish step at DP = 128 on kCoopWG cooperating workgroups (bit-identical to dispatch_finish)
+int launch_finish_coop(const float* gs, double n_total, const Geom& g, const float* U, float* U_out, float* f_out,
+                       int* counter, int by_counter, CoopXchg* xc, hipStream_t s) {
+  const size_t lds = coop_lds_bytes();
+  DRSA_SMEM(drsa_finish_coop_kernel, lds);
+  hipLaunchKernelGGL(drsa_finish_coop_kernel, dim3(kCoopWG), dim3(1024), lds, s, gs, n_total, g.d, g.K, g.DKp, U, U_out,
+                     f_out, counter, by_counter, kPolarTol, kPolarMaxIter, xc);
+  DRSA_LAUNCH_CHECK();
+  return DRSA_OK;
+}
+
+// finish of one step of drsa_run / run_multi: cooperative at DP = 128, else the one-workgroup kernel
+int step_finish(const float* gs, double n_total, const Geom& g, const float* U, float* U_out, float* f_out,
+                int* counter, CoopXchg* xc, hipStream_t s) {
+  if (U_out && xc && g.DP == 128) return launch_finish_coop(gs, n_total, g, U, U_out, f_out, counter, 1, xc, s);
+  return dispatch_finish(gs, n_total, g, U, U_out, f_out, counter, 1, U_out ? 0 : 1, kPolarTol, kPolarMaxIter, nullptr,
+                         s);
+}
+
 }  // namespace
 
 // ===========================================================================
 // C ABI
 // ===========================================================================
 extern "C" {
+
+#ifdef DRSA_COOP_STAMP
+int drsa_amd_debug_coop_stamps(unsigned long long* host_out) {
+  return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_coop_stamps), sizeof(g_coop_stamps));
+}
+#endif
 
 size_t drsa_amd_drsa_workspace_bytes(int64_t N, int d, int K) {
   const Geom g = geom(d, K);
@@ -1273,6 +1587,8 @@ int drsa_amd_drsa_run(const float* A, const float* C, int64_t N, int d, int K, f
     if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) use_graph = 0;
   }
   DRSA_HIP(hipMemsetAsync(counter, 0, sizeof(int), s));
+  CoopXchg* xc = ws_xchg(ws, N, g);
+  if (int rc = coop_reset(xc, s)) return rc;
   // fused: the gradient at U_0 first, then per step one fused launch (finish of the previous step
   // + partial at the new U) and the slab reduce; the final objective reads the last gs
   const bool fused = fused_ok(g);
@@ -1284,7 +1600,7 @@ int drsa_amd_drsa_run(const float* A, const float* C, int64_t N, int d, int K, f
     if (fused) return fused_step(A, C, N, (double)N, g, gs, gs, Uin, Uout, f_traj, counter, ws, s);
     int rc = drsa_amd_drsa_partial(A, C, N, d, K, Uin, gs, ws, ws_size, stream);
     if (rc) return rc;
-    return dispatch_finish(gs, (double)N, g, Uin, Uout, f_traj, counter, 1, 0, kPolarTol, kPolarMaxIter, nullptr, s);
+    return step_finish(gs, (double)N, g, Uin, Uout, f_traj, counter, xc, s);
   };
   int done = 0;
   if (use_graph && steps >= 2) {
@@ -1381,6 +1697,7 @@ int drsa_amd_drsa_run_multi(int P, const drsa_amd_problem_t* probs, int steps, i
     }
     const drsa_amd_problem_t& q = probs[p];
     if (!hip_ok(hipMemsetAsync(q.counter, 0, sizeof(int), s), "memset")) { cleanup(); return rc; }
+    if (int r = coop_reset(ws_xchg(q.ws, q.N, geom(q.d, q.K)), s)) { cleanup(); return r; }
   }
   // one step of problem p on stream st: U_in -> U_out, f -> f_traj[counter++]
   auto one = [&](int p, hipStream_t st, const float* Uin, float* Uout) -> int {
@@ -1389,8 +1706,7 @@ int drsa_amd_drsa_run_multi(int P, const drsa_amd_problem_t* probs, int steps, i
     float* gs = ws_gs(q.ws, q.N, g);
     int r = partial_impl(q.A, q.C, q.N, q.d, q.K, Uin, gs, q.ws, q.ws_size, st, q.dtype);
     if (r) return r;
-    return dispatch_finish(gs, (double)q.N, g, Uin, Uout, q.f_traj, q.counter, 1, Uout ? 0 : 1, kPolarTol,
-                           kPolarMaxIter, nullptr, st);
+    return step_finish(gs, (double)q.N, g, Uin, Uout, q.f_traj, q.counter, ws_xchg(q.ws, q.N, g), st);
   };
   // fork -> per-problem body -> join, captured from stream s
   auto forked = [&](int nsteps_body, bool final_objective) -> int {
