@@ -879,24 +879,27 @@ __global__ __launch_bounds__(fin_threads<polar_dim<DP>()>()) void drsa_finish_ke
 
 // ---------------------------------------------------------------------------
 // Cooperative finish at DP = 128 (drsa_run / run_multi, the C5 shapes): the polar's two 128^3
-// products per Newton-Schulz iteration split over kCoopWG workgroups on as many CUs, workgroup j
-// owning the 32 columns [32 j, 32 j + 32) of X.  Per iteration workgroup j forms P_j = X^T X[:, j]
-// (4 tiles), T_j = 1.5 I - 0.5 P_j with its max |P_j - I|, and X'[:, j] = X T_j (4 tiles); the new
+// products per Newton-Schulz iteration split over kCoopWG = 8 workgroups on as many CUs, workgroup j
+// owning the 16 columns [16 j, 16 j + 16) of X.  Per iteration workgroup j forms P_j = X^T X[:, j]
+// (8 16x16 tiles, one wave each, two per SIMD), T_j = 1.5 I - 0.5 P_j with its max |P_j - I|, and
+// X'[:, j] = X T_j (8 tiles); the new
 // column blocks and the error maxima are exchanged through the workspace (one hand-off per
 // iteration: agent-scope stores, a ticket counter, agent-scope loads), so every workgroup holds
 // the whole X' for the next P.  Bit-identical to drsa_finish_kernel's single-workgroup polar_ns:
-//   * every P / X T entry is the same full-k fp32 MFMA chain (P's lower tiles there are mirrored
-//     from the upper ones, here computed directly: x_k y_k = y_k x_k exactly);
+//   * every P / X T entry is the same full-k fp32 fma chain (k ascending from +0: the 32x32x2 MFMA
+//     there, 16x16x4 here, both exact chains; P's lower tiles there are mirrored from the upper
+//     ones, here computed directly: x_k y_k = y_k x_k exactly);
 //   * tr(P) from P's diagonal (each workgroup hands its diagonal tile's 32 entries over), folded in
 //     the same order; the inf-norm row sums as column sums of workgroup j's block (P is exactly
 //     symmetric), in the same order; maxima are order-free;
 //   * the X T of an iteration whose error stops the loop is computed speculatively (the error is
 //     exchanged with its result) and dropped, so the returned X is the one polar_ns returns.
 // The workgroups spin on each other: the launch needs kCoopWG co-resident workgroups (one per CU,
-// 150 KB of LDS each), which the callers guarantee by launching nothing else that waits on them; a
+// 141 KB of LDS each), which the callers guarantee by launching nothing else that waits on them; a
 // spin that outlives kCoopSpinTicks (100 ms) gives up and poisons U_out with NaN instead of hanging.
 // ---------------------------------------------------------------------------
-constexpr int kCoopWG = 4;
+constexpr int kCoopWG = 8;
+constexpr int kCoopBW = 128 / kCoopWG;   // columns per workgroup (16x16x4 MFMA tiles)
 constexpr long long kCoopSpinTicks = 10000000;   // s_memrealtime runs at 100 MHz
 
 // diagnostic build (-DDRSA_COOP_STAMP, scripts/probe_coop.py): phase times of the last launch's
@@ -944,7 +947,7 @@ __device__ bool coop_exchange(unsigned* ticket, int* ok_sh) {
   return *ok_sh != 0;
 }
 
-constexpr int kCoopTLD = 32;   // T_j row stride (one 32-column block)
+constexpr int kCoopTLD = kCoopBW;   // T_j row stride (one column block)
 constexpr size_t coop_lds_bytes() {
   return ((size_t)2 * 128 * ns_ld<128>() + (size_t)128 * kCoopTLD + 64) * sizeof(float);
 }
@@ -964,31 +967,32 @@ __global__ __launch_bounds__(1024) void drsa_finish_coop_kernel(
   __shared__ double fsh;
   __shared__ float diag[128];
   __shared__ int ok_sh;
+  constexpr int BW = kCoopBW, NB = DP / BW;   // 16-row / 16-column tiles, NB = 8 per column block
   const int tid = threadIdx.x, lane = lane_id(), w = wave_id(), j = blockIdx.x;
-  const int lo = lane & 31, hi = lane >> 5;
+  const int lo = lane & 15, hi = lane >> 4;   // 16x16x4: A/B lane l -> index l & 15 at k = k0 + (l >> 4)
   const int dk = d / K;
   COOP_STAMP(0);
   const double f = finish_prologue<DP>(gs, n_total, d, K, DKP, U, X, true, dterm, cvec, &fsh);
   bool ok = true;
   COOP_STAMP(1);
 
-  // P_j tile (ib = w) of X^T X[:, j-block] for waves 0..3: Tj[row][col - 32 j] = raw P (it == 0) or
-  // 1.5 I - 0.5 P with err (it > 0)
+  // P_j tile (ib = w) of X^T X[:, j-block] for waves 0..7: Tj[row][col - BW j] = raw P (it == 0) or
+  // 1.5 I - 0.5 P with err (it > 0).  16x16 D layout: lane l, reg r -> row 4 (l >> 4) + r, col l & 15.
   auto gram_block = [&](int it, float& err) {
     __syncthreads();   // X complete
-    if (w < 4) {
-      f32x16 acc = {};
+    if (w < NB) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 8
-      for (int k0 = 0; k0 < DP; k0 += 2) {
+      for (int k0 = 0; k0 < DP; k0 += 4) {
         const int kk = k0 + hi;
-        acc = mfma32(X[kk * LD + 32 * w + lo], X[kk * LD + 32 * j + lo], acc);
+        acc = mfma16(X[kk * LD + BW * w + lo], X[kk * LD + BW * j + lo], acc);
       }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = 32 * w + t32_row(r, hi);
+      for (int r = 0; r < 4; ++r) {
+        const int row = BW * w + 4 * hi + r;
         float v = acc[r];
         if (it > 0) {
-          const bool dg = row == 32 * j + lo;
+          const bool dg = row == BW * j + lo;
           err = fmaxf(err, fabsf(v - (dg ? 1.f : 0.f)));
           v = (dg ? 1.5f : 0.f) - 0.5f * v;
         }
@@ -996,22 +1000,22 @@ __global__ __launch_bounds__(1024) void drsa_finish_coop_kernel(
       }
     }
   };
-  // X'[:, j-block] = X T_j for waves 0..3 (tile ib = w): into Xn and the exchange buffer
+  // X'[:, j-block] = X T_j for waves 0..7 (tile ib = w): into Xn and the exchange buffer
   auto xt_block = [&](int par) {
     __syncthreads();   // T_j complete
-    if (w < 4) {
-      f32x16 acc = {};
+    if (w < NB) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 8
-      for (int kr = 0; kr < DP; kr += 2) {
-        const int kk = kr + hi;
-        acc = mfma32(X[(32 * w + lo) * LD + kk], Tj[kk * TLD + lo], acc);
+      for (int k0 = 0; k0 < DP; k0 += 4) {
+        const int kk = k0 + hi;
+        acc = mfma16(X[(BW * w + lo) * LD + kk], Tj[kk * TLD + lo], acc);
       }
       float* xg = xc->xb[par];
       int l = lane;
       asm volatile("" : "+v"(l));
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = 32 * w + t32_row(r, l >> 5), col = 32 * j + (l & 31);
+      for (int r = 0; r < 4; ++r) {
+        const int row = BW * w + 4 * (l >> 4) + r, col = BW * j + (l & 15);
         Xn[row * LD + col] = acc[r];
         coop_st(&xg[row * DP + col], acc[r]);
       }
@@ -1020,7 +1024,7 @@ __global__ __launch_bounds__(1024) void drsa_finish_coop_kernel(
   // the other workgroups' column blocks of X' (after the exchange)
   // (all loads issued before the first LDS store: one memory round trip, not 12)
   auto gather_blocks = [&](int par) {
-    constexpr int NQ = (kCoopWG - 1) * 32 * DP / NT;
+    constexpr int NQ = (kCoopWG - 1) * BW * DP / NT;
     const float* xg = xc->xb[par];
     unsigned t = (unsigned)tid;
     asm volatile("" : "+v"(t));   // addresses per call: hoisted out of the iteration loop they spill
@@ -1028,10 +1032,10 @@ __global__ __launch_bounds__(1024) void drsa_finish_coop_kernel(
     unsigned lds[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      const unsigned e = t + (unsigned)q * NT;  // over the 3 foreign blocks, 32-float runs
-      const unsigned bi = e >> 12, rem = e & 4095u;
+      const unsigned e = t + (unsigned)q * NT;  // over the foreign blocks, BW-float runs
+      const unsigned bi = e / (BW * DP), rem = e % (BW * DP);
       const unsigned blk = bi < (unsigned)j ? bi : bi + 1;
-      const unsigned row = rem >> 5, col = 32 * blk + (rem & 31u);
+      const unsigned row = rem / BW, col = BW * blk + rem % BW;
       v[q] = coop_ld(&xg[row * DP + col]);
       lds[q] = row * LD + col;
     }
@@ -1046,16 +1050,16 @@ __global__ __launch_bounds__(1024) void drsa_finish_coop_kernel(
   COOP_STAMP(2);
   // row sums of |P| for the rows of block j, as column sums of P[:, j-block] (polar_ns's order)
   float rs = 0.f;
-  if (tid < 32 * TPR) {
+  if (tid < BW * TPR) {
     const int cl = tid / TPR, part = tid % TPR;
 #pragma unroll
     for (int c = part; c < DP; c += TPR) rs += fabsf(Tj[c * TLD + cl]);
   }
   for (int m = 1; m < TPR; m <<= 1) rs += shfl_xor(rs, m);
-  const float rmax_j = block_max<NT>(tid < 32 * TPR ? rs : 0.f, red);
+  const float rmax_j = block_max<NT>(tid < BW * TPR ? rs : 0.f, red);
   // hand-off 0: block j's diagonal of P (its own diagonal tile) and its inf-norm partial
-  if (tid < 32) {
-    const int i = 32 * j + tid;
+  if (tid < BW) {
+    const int i = BW * j + tid;
     coop_st(&xc->xb[0][i * DP + i], Tj[i * TLD + tid]);
   }
   if (tid == 0) coop_st(&xc->sc[0][j][1], rmax_j);
@@ -1084,10 +1088,10 @@ __global__ __launch_bounds__(1024) void drsa_finish_coop_kernel(
     const int r = e / DP, c = e % DP;
     X[r * LD + c] *= a;
   }
-  for (int e = tid; e < DP * 32; e += NT) {
-    const int r = e / 32, cl = e % 32;
+  for (int e = tid; e < DP * BW; e += NT) {
+    const int r = e / BW, cl = e % BW;
     const float pv = Tj[r * TLD + cl] * a2;
-    const bool dg = r == 32 * j + cl;
+    const bool dg = r == BW * j + cl;
     err = fmaxf(err, fabsf(pv - (dg ? 1.f : 0.f)));
     Tj[r * TLD + cl] = (dg ? 1.5f : 0.f) - 0.5f * pv;
   }
@@ -1127,8 +1131,8 @@ __global__ __launch_bounds__(1024) void drsa_finish_coop_kernel(
   COOP_STAMP(60);
   // U_out: workgroup j writes the real entries of its padded column block
 #pragma unroll
-  for (int q = 0; q < DP * 32 / NT; ++q) {
-    const int e = tid + q * NT, i = e >> 5, pc = 32 * j + (e & 31);
+  for (int q = 0; q < DP * BW / NT; ++q) {
+    const int e = tid + q * NT, i = e / BW, pc = BW * j + e % BW;
     const int kc = pc / DKP, l = pc % DKP;
     if (i < d && kc < K && l < dk) U_out[i * d + kc * dk + l] = ok ? X[i * LD + pc] : __builtin_nanf("");
   }

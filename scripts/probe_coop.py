@@ -23,12 +23,12 @@ out = {}
 for steps in (1, 7):
     drsa_run(Ag, Cg, Ug, 16, steps, use_graph=False)
     torch.cuda.synchronize()
-    st = (ctypes.c_ulonglong * (4 * 64))()
+    st = (ctypes.c_ulonglong * (8 * 64))()
     _capi.lib().drsa_amd_debug_coop_stamps(st)
-    a = np.array(st, dtype=np.float64).reshape(4, 64)
+    a = np.array(st, dtype=np.float64).reshape(8, 64)
     t0 = a[:, 0].min()
     rows = {}
-    for j in range(4):
+    for j in range(8):
         rows[j] = {k: round((a[j, k] - t0) / 1e3, 2) for k in range(64) if a[j, k] >= t0 and a[j, k] > 0}
     out[f"steps{steps}"] = rows   # kilocycles since the first workgroup's start
 print(json.dumps(out))
