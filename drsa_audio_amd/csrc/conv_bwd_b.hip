@@ -16,3 +16,9 @@ static const Entry kTableBwdB_e[] = {
 };
 extern const Table kTableBwdB = {kTableBwdB_e, (int)(sizeof(kTableBwdB_e) / sizeof(kTableBwdB_e[0]))};
 }  // namespace drsa_conv
+
+#ifdef DRSA_CONV_STAMP
+extern "C" int drsa_amd_debug_conv_stamps(void* buf) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(drsa_conv::g_conv_stamps), &buf, sizeof(buf));
+}
+#endif

@@ -60,6 +60,13 @@ namespace drsa_conv {
 
 constexpr int kThreads = 256;
 
+// diagnostic build only (-DDRSA_CONV_STAMP, scripts/probe_conv_phases.py): phase times of every
+// workgroup of the 32 -> 32 pool-sparse backward (GTZAN conv_bwd:features.3) into a buffer of their
+// own, set by drsa_amd_debug_conv_stamps; nothing in the kernel reads them
+#ifdef DRSA_CONV_STAMP
+static __device__ unsigned long long* g_conv_stamps;
+#endif
+
 // bias3 of a forward call without bias ([3][COUT], COUT <= 128)
 __device__ const float g_zero_bias3[3 * 128] = {};
 
@@ -690,6 +697,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
   constexpr int KC = Cfg::KC, KCP = Cfg::KCP;
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
+#ifdef DRSA_CONV_STAMP
+  constexpr bool kStamp = EPI == EPI_BWD && CIN == 32 && COUT == 32 && AMODE == A_POOLSPARSE && ET == 0;
+  unsigned long long* const stp = kStamp && g_conv_stamps && threadIdx.x == 0
+                                      ? g_conv_stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 : nullptr;
+#define CONV_STAMP(slot) do { if (stp) stp[(slot)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define CONV_STAMP(slot) do {} while (0)
+#endif
+  CONV_STAMP(0);
   float* halo = smem;                          // [CIC][PLANE]   (bf16: [2][HY][HXB] x 16 B)
   float* wl = smem + (Cfg::BF ? Cfg::bf_halo_floats : (size_t)CIC * PLANE);   // [NG][KCP][COUT]
 
@@ -772,12 +788,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
     if constexpr (Cfg::BF) stg.store(halo, wl, tid, ty0, tx0);
     else stg.store(halo, wl, tid);
     __syncthreads();
+    CONV_STAMP(1 + 2 * chunk);
     if (chunk + 1 < Cfg::NCHUNK) stg.load(a, (chunk + 1) * CIC, tid, ty0, tx0, bq, bs);
     if (!active) continue;
     if constexpr (Cfg::BF)
       mfma_chunk_bf<Cfg>(reinterpret_cast<const uint4*>(halo), reinterpret_cast<const uint4*>(wl), pix_off, lane, wn, acc);
     else
       mfma_chunk<Cfg, Cfg::PD>(halo, wl, pix_off, lane, wn, acc);
+    CONV_STAMP(2 + 2 * chunk);
   }
   constexpr int Q = TH * TW / 4, CS = kThreads / Q;
   static_assert(kThreads % Q == 0, "float4 groups per tile must divide the block");
@@ -842,6 +860,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
     if constexpr (Cfg::BF) stg.store(halo, wl, tid, ty0, tx0);
     else stg.store(halo, wl, tid);
     __syncthreads();
+    CONV_STAMP(2 * Cfg::NCHUNK - 1);
     epi_loads(0, 0, pre_x, pre_d, true, DRSA_CONV_PRE_D, 0, kPreN);
 
     if (active) {
@@ -851,6 +870,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
       else
         mfma_chunk<Cfg, Cfg::PD>(halo, wl, pix_off, lane, wn, acc);
     }
+    CONV_STAMP(2 * Cfg::NCHUNK);
   }
 
   // the pool cells of the staged tile T (2 x PWc windows), one per thread and iteration `it`
@@ -1162,6 +1182,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
      }
     }
   }
+#ifdef DRSA_CONV_STAMP
+  if (stp) {
+    stp[13] = __builtin_amdgcn_s_memtime();
+    stp[14] = (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_ID
+    stp[15] = (unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11));   // XCC_ID
+  }
+#endif
+#undef CONV_STAMP
 }
 
 typedef void (*KernFn)(ConvArgs);
