@@ -23,12 +23,29 @@ constexpr int fin_threads() { return DP >= 64 ? 1024 : 256; }
 template <int DP>
 constexpr int ns_ld() { return DP + 2; }
 
+// wave max in lane 63 by DPP row shifts and row broadcasts (a max is order-free, so this equals the
+// xor-shuffle tree it replaces bit for bit; 6 dependent VALU ops instead of 6 ds_bpermute round trips)
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_max_step(float v) {
+  const int o = __builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, ROW_MASK, 0xf, false);
+  return fmaxf(v, __int_as_float(o));
+}
+__device__ __forceinline__ float wave_max63(float v) {
+  v = dpp_max_step<0x111, 0xf>(v);   // row_shr:1
+  v = dpp_max_step<0x112, 0xf>(v);   // row_shr:2
+  v = dpp_max_step<0x114, 0xf>(v);   // row_shr:4
+  v = dpp_max_step<0x118, 0xf>(v);   // row_shr:8   -> lane 15 of each row: the row's max
+  v = dpp_max_step<0x142, 0xa>(v);   // row_bcast:15 (rows 1, 3)
+  v = dpp_max_step<0x143, 0xc>(v);   // row_bcast:31 (rows 2, 3) -> lane 63: the wave's max
+  return v;
+}
+
 // single-barrier block max: red must be a slot nobody reads or writes between two calls that are
 // separated by at least one other __syncthreads (the per-iteration error uses alternating slots)
 template <int NT>
 __device__ float block_max1(float v, float* red) {
-  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, shfl_xor(v, m));
-  if (lane_id() == 0) red[wave_id()] = v;
+  v = wave_max63(v);
+  if (lane_id() == 63) red[wave_id()] = v;
   __syncthreads();
   float r = red[0];
 #pragma unroll
@@ -38,9 +55,9 @@ __device__ float block_max1(float v, float* red) {
 
 template <int NT>
 __device__ float block_max(float v, float* red) {
-  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, shfl_xor(v, m));
+  v = wave_max63(v);
   __syncthreads();
-  if (lane_id() == 0) red[wave_id()] = v;
+  if (lane_id() == 63) red[wave_id()] = v;
   __syncthreads();
   float r = red[0];
 #pragma unroll

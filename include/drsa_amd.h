@@ -94,7 +94,11 @@ int drsa_amd_drsa_objective(const float* A, const float* C, int64_t N, int d, in
  * (steps+1 floats) receives the objective before every update and after the last;
  * U_io holds U_0 on entry and U_steps on exit; U_tmp is d*d scratch; counter is one
  * device int.  use_graph != 0 replays a captured two-step hipGraph (needs a non-NULL
- * stream). */
+ * stream).  At padded size 128 (d > 64) each step's polar runs on 8 cooperating workgroups
+ * that hand X over through the workspace (bit-identical to drsa_amd_drsa_finish's single
+ * workgroup).  They wait on each other, so they must become resident together: work running
+ * concurrently on other streams only delays them, unless it holds more than 248 CUs while itself
+ * waiting on this stream (a wait that outlives 100 ms gives up and writes NaN into U_out). */
 int drsa_amd_drsa_run(const float* A, const float* C, int64_t N, int d, int K, float* U_io, float* U_tmp,
                       int steps, float* f_traj, int* counter, void* workspace, size_t workspace_bytes,
                       int use_graph, void* stream);
