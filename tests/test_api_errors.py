@@ -97,6 +97,12 @@ def test_c_abi_argument_validation_without_gpu():
     assert lib.drsa_amd_drsa_slab_floats(100, 4) == 128 * 128 + 4
     assert lib.drsa_amd_drsa_slab_floats(64, 4) == 64 * 64 + 4
     assert lib.drsa_amd_drsa_workspace_bytes(100, 128, 3) == 0
+    # padded size 128 carries the cooperative finish's hand-off area (two 128 x 128 X buffers, the
+    # per-workgroup scalars and the ticket) beyond the slabs: at N = 16 (one leaf) the partial slabs,
+    # the reduced slab and that area
+    slab = 4 * (128 * 128 + 4)
+    assert lib.drsa_amd_drsa_workspace_bytes(16, 128, 16) >= 2 * slab + 2 * 128 * 128 * 4
+    assert lib.drsa_amd_drsa_workspace_bytes(16, 64, 4) < 2 * 4 * (64 * 64 + 4) + 4096
     # compact den ring backward: pooled W >= 8 (W % 8 == 0) and H >= 2, as the forward's layout needs
     for H, W in ((4, 4), (0, 8), (4, 12)):
         with pytest.raises(_capi.DrsaAmdError, match="pooled H >= 2"):

@@ -80,11 +80,13 @@ def test_graph_and_eager_runs_identical():
 
 
 @pytest.mark.parametrize("N,d,K", [(20000, 64, 4), (9001, 64, 8), (3000, 48, 4), (777, 64, 16), (20000, 128, 16),
-                                   (3000, 100, 4), (2048, 128, 8)])
+                                   (3000, 100, 4), (2048, 128, 8), (4000, 128, 2), (1500, 72, 9), (777, 66, 2)])
 def test_fused_run_equals_partial_finish_loop_bitwise(N, d, K):
-    """drsa_run at DP = 64 / 128 takes the fused step (drsa_fused_step_kernel: the previous step's finish
-    redone in every workgroup, then the partial on the new U from LDS).  Its trajectory and U must
-    equal, bit for bit, the explicit three-launch loop of the partial and finish entry points."""
+    """drsa_run at DP = 64 takes the fused step (drsa_fused_step_kernel: the previous step's finish
+    redone in every workgroup, then the partial on the new U from LDS), at DP = 128 the cooperative
+    finish (drsa_finish_coop_kernel: the polar over 8 workgroups of 16 columns, including concept
+    width 64 and heavily padded d = 66 / 72).  Its trajectory and U must equal, bit for bit, the
+    explicit loop of the partial and the one-workgroup finish entry points."""
     from drsa_audio_amd import _capi
     from drsa_audio_amd.xai.drsa.drsa import DrsaWorkspace, drsa_run
     steps = 6
