@@ -10,7 +10,7 @@
 // ---------------------------------------------------------------------------
 namespace drsa_conv {
 extern const Table kTableFwdA, kTableFwdB, kTableFwdC, kTableFwdD, kTableFwdE, kTableBwdA, kTableBwdB, kTableBwdC,
-    kTableFwdBfA, kTableFwdBfB, kTableFwdBfC, kTableFwdP4, kTableBwdBfA, kTableBwdBfB;
+    kTableFwdBfA, kTableFwdBfB, kTableFwdBfC, kTableFwdP4, kTableBwdBfA, kTableBwdBfB, kTableSmall;
 }
 
 namespace {
@@ -61,10 +61,31 @@ const Entry* find(int cin_p, int cout_p, int W, int ng, int amode, int epi, int 
   return nullptr;
 }
 
-int launch(const Entry* e, const ConvArgs& args, int batch, hipStream_t s) {   // batch = grid.y
+// 4 x 8 tiles (conv_small.hip) replace an 8 x 8 entry whose grid would have fewer workgroups than
+// this (two per CU): twice the workgroups for the small maps at small batches.  VGGish (B = 32):
+// conv_fwd:features.24 / .28 0.108 / 0.103 -> 0.064 / 0.061 ms, conv_bwd:features.31 0.060 ->
+// 0.044, fp32 standard LRP 8.2k -> 8.6k samples/s; at GTZAN's 512 workgroups (features.12, B = 512)
+// 8 x 8 stays faster (4 x 8: 0.093 -> 0.119 ms forward, 0.051 -> 0.080 backward)
+#ifndef DRSA_CONV_SMALL_WG
+#define DRSA_CONV_SMALL_WG 512
+#endif
+const Entry* small_tile(const Entry* e, int H, int W, int batch) {
+  if (e->th != 8 || e->tw != 8) return e;
+  if ((int64_t)((H + 7) / 8) * ((W + 7) / 8) * batch >= DRSA_CONV_SMALL_WG) return e;
+  for (int i = 0; i < drsa_conv::kTableSmall.n; ++i) {
+    const Entry& c = drsa_conv::kTableSmall.entries[i];
+    if (c.cin_p == e->cin_p && c.cout_p == e->cout_p && c.ng == e->ng && c.amode == e->amode && c.epi == e->epi &&
+        c.et == e->et && c.pw == e->pw)
+      return &c;
+  }
+  return e;
+}
+
+int launch(const Entry* e0, const ConvArgs& args, int batch, hipStream_t s) {   // batch = grid.y
   // the kernels address one sample's planes with 32-bit offsets from a per-sample base
   DRSA_REQUIRE((int64_t)(args.cin > args.cout ? args.cin : args.cout) * args.H * args.W < ((int64_t)1 << 31),
                "conv: one sample's channels x H x W must stay below 2^31");
+  const Entry* e = small_tile(e0, args.H, args.W, batch);
   DRSA_SMEM(e->fn, e->lds);   // per device, thread-safe
   const int tiles = ((args.H + e->th - 1) / e->th) * ((args.W + e->tw - 1) / e->tw);
   hipLaunchKernelGGL(e->fn, dim3(tiles, batch), dim3(kThreads), e->lds, s, args);
