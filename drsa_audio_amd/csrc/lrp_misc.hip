@@ -163,6 +163,68 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(LinArgs a) {
 #undef LFWD_LOAD
 }
 
+// Long K (the classifier input, K = 2048) with few output tiles (GTZAN: 512 x 128 = 256 16 x 16
+// tiles): one wave per 16 x 16 output tile, so the grid covers the chip instead of 64 four-wave
+// workgroups; K in 128-wide chunks staged through the wave's own LDS (a wave barrier, no workgroup
+// barrier), the next chunk's 16 float4 loads in flight under the current chunk's 32 MFMAs.  The
+// same single k-ordered chain per output as linear_fwd_kernel (bias added last): the same bits.
+constexpr int L1K = 128;
+
+__global__ __launch_bounds__(64) void linear_fwd_w1_kernel(LinArgs a) {
+  __shared__ __attribute__((aligned(16))) float As[16][L1K + 4];   // [m][k]
+  __shared__ float Bs[L1K][16 + 1];                                 // [k][n]
+  const int lane = threadIdx.x;
+  const int m0 = blockIdx.x * 16, n0 = blockIdx.y * 16;
+  constexpr int NV = 16 * L1K / 4 / 64;   // float4 per lane per operand (8)
+  float4 ra[NV], rb[NV];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int idx = lane + i * 64, r = idx / (L1K / 4), k = k0 + (idx % (L1K / 4)) * 4;
+      const int m = m0 + r, n = n0 + r;
+      const bool oa = m < a.M && k < a.K, ob = n < a.N && k < a.K;
+      const float4 va = *reinterpret_cast<const float4*>(a.A + (oa ? (size_t)m * a.K + k : 0));
+      const float4 vb = *reinterpret_cast<const float4*>(a.W + (ob ? (size_t)n * a.K + k : 0));
+      ra[i] = oa ? va : make_float4(0.f, 0.f, 0.f, 0.f);
+      rb[i] = ob ? vb : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  load(0);
+  for (int k0 = 0; k0 < a.K; k0 += L1K) {
+    __builtin_amdgcn_wave_barrier();   // the previous chunk's LDS reads done (one wave: in order)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int idx = lane + i * 64, r = idx / (L1K / 4), c = (idx % (L1K / 4)) * 4;
+      *reinterpret_cast<float4*>(&As[r][c]) = ra[i];
+      Bs[c][r] = rb[i].x; Bs[c + 1][r] = rb[i].y; Bs[c + 2][r] = rb[i].z; Bs[c + 3][r] = rb[i].w;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the stores landed before this wave reads them
+    __builtin_amdgcn_wave_barrier();
+    if (k0 + L1K < a.K) load(k0 + L1K);
+    // every operand of the chunk read before its chain (left to the scheduler each MFMA waits on
+    // its own LDS round trip: one wave per SIMD has nothing else to hide it behind)
+    float av[L1K / 4], bv[L1K / 4];
+#pragma unroll
+    for (int q = 0; q < L1K / 4; ++q) {
+      av[q] = As[lane & 15][4 * q + (lane >> 4)];
+      bv[q] = Bs[4 * q + (lane >> 4)][lane & 15];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < L1K / 4; ++q) acc = mfma16(av[q], bv[q], acc);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = m0 + (lane >> 4) * 4 + r, n = n0 + (lane & 15);
+    if (m >= a.M || n >= a.N) continue;
+    const size_t o = (size_t)m * a.N + n;
+    const float zz = acc[r] + (a.bias ? a.bias[n] : 0.f);
+    a.out[o] = zz;
+    if (a.out_relu) a.out_relu[o] = zz > 0.f ? zz : (zz != zz ? zz : 0.f);
+  }
+}
+
 // ===========================================================================
 // projection forward: h = a_vec U, a' = h U^T, optional 2x2 max-pool of a'
 //   a [B][d][H][W] -> h [B][d][H*W] (channel-major), ap [B][d][H][W], pooled + argmax
@@ -1416,7 +1478,9 @@ int drsa_amd_linear_fwd(const float* x, const float* Wt, const float* bias, floa
   LinArgs a{};
   a.A = x; a.W = Wt; a.bias = bias; a.out = z_out; a.out_relu = relu_out; a.M = M; a.N = N; a.K = K; a.bwd = 0;
   // int64_t K (float4-aligned rows): the prefetching kernel; same chain order, same results
-  if (K % 4 == 0 && K >= LFK)
+  if (K % 4 == 0 && K >= L1K)
+    hipLaunchKernelGGL(linear_fwd_w1_kernel, dim3((M + 15) / 16, (N + 15) / 16), dim3(64), 0, (hipStream_t)stream, a);
+  else if (K % 4 == 0 && K >= LFK)
     hipLaunchKernelGGL(linear_fwd_kernel, dim3((M + LT - 1) / LT, (N + LT - 1) / LT), dim3(256), 0, (hipStream_t)stream, a);
   else
     hipLaunchKernelGGL(linear_kernel, dim3((M + LT - 1) / LT, (N + LT - 1) / LT), dim3(256), 0, (hipStream_t)stream, a);
