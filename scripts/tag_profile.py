@@ -19,7 +19,7 @@ import json
 import sys
 from collections import defaultdict
 
-OURS = ("conv3x3_kernel", "linear_kernel", "linear_fwd_kernel", "projection_fwd_kernel", "projection_bwd_kernel",
+OURS = ("conv3x3_kernel", "linear_kernel", "linear_fwd_kernel", "linear_fwd_w1_kernel", "projection_fwd_kernel", "projection_bwd_kernel",
         "projection_bwd_rc_kernel", "first_conv_pool_kernel", "first_layer_bwd", "heatmap_sort_kernel",
         "heatmap_sort_cached_kernel")
 
