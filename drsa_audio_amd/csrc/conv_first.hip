@@ -4,9 +4,11 @@
 // and spends its time in the LDS staging and the epilogue; the layer is HBM-bound on its
 // pooled outputs (y, argmax, den: 9 B per pooled cell and channel).  This kernel keeps the
 // whole 4x10 input patch of four adjacent pool windows in registers, runs every output
-// pixel's 9-tap fma chain on the VALU (same k order as the MFMA kernel and
-// oracle/lrp_exact.c:conv2d_exact, so the result is bit-identical), and writes float4 rows of
-// y and den plus one packed uint32 of argmax bytes per channel.
+// pixel's 9-tap fma chain on the VALU as packed fmas (v_pk_fma_f32: a window column's upper and
+// lower pixel per instruction; weights and bias as scalar operands) in the k order of the MFMA
+// kernel and oracle/lrp_exact.c:conv2d_exact, so the result is bit-identical, pools with
+// branch-free selects, and writes float4 rows of y and den plus one packed uint32 of argmax
+// bytes per channel.
 //
 // Reference: cxai/model/create_model.py:100-137 (conv -> ReLU -> MaxPool2d) and the rule
 // denominators of SURVEY App. A (WSquare map / Epsilon z / Gamma z+ + z-).
@@ -18,10 +20,18 @@
 namespace {
 
 constexpr int kThreads = 256;
+#ifndef DRSA_FIRST_FWD_PK
+#define DRSA_FIRST_FWD_PK 1
+#endif
+typedef float fp2 __attribute__((ext_vector_type(2)));
 
 // DEN: 0 none, 1 input-independent map (WSquare / Flat), 2 computed from the rule's sets
 template <int NG, int DEN>
-__global__ __launch_bounds__(kThreads) void first_conv_pool_kernel(ConvArgs a, int cout_p, int total) {
+#ifndef DRSA_FIRST_FWD_WPE
+#define DRSA_FIRST_FWD_WPE 1
+#endif
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(DRSA_FIRST_FWD_WPE))) void first_conv_pool_kernel(ConvArgs a, const float* __restrict__ wts, const float* __restrict__ bias,
+                                                            const float* __restrict__ den_map, int cout_p, int total) {
   const int t = blockIdx.x * kThreads + threadIdx.x;
   if (t >= total) return;
   const int H = a.H, W = a.W, H2 = H >> 1, W2 = W >> 1, gq = W2 >> 2;
@@ -61,6 +71,17 @@ __global__ __launch_bounds__(kThreads) void first_conv_pool_kernel(ConvArgs a, i
   // blockIdx.y: channel slice (more waves in flight for the store stream)
   const int cper = (a.cout + gridDim.y - 1) / gridDim.y;
   const int c_lo = blockIdx.y * cper, c_hi = min(a.cout, c_lo + cper);
+#if DRSA_FIRST_FWD_PK
+  // vertical pixel pairs of the patch: pr[ky][c] = (x[ky][c], x[ky + 1][c]), so one packed fma
+  // (v_pk_fma_f32) advances the chains of the window's upper and lower pixel of one column
+  fp2 pr[3][10];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+    for (int c = 0; c < 10; ++c) pr[ky][c] = fp2{xin[ky][c], xin[ky + 1][c]};
+#endif
+  // 32-bit offsets of the den map (C * H * W < 2^31, checked by the host)
+  const int mrow = (2 * qy) * W + 8 * g4;
 #ifndef DRSA_FIRST_FWD_CUNROLL
 #define DRSA_FIRST_FWD_CUNROLL 4
 #endif
@@ -72,8 +93,8 @@ __global__ __launch_bounds__(kThreads) void first_conv_pool_kernel(ConvArgs a, i
 #pragma unroll
     for (int g = 0; g < NG; ++g)
 #pragma unroll
-      for (int k = 0; k < 9; ++k) w[g][k] = a.wts[(size_t)(g * 9 + k) * cout_p + co];
-    const float b0 = a.bias ? a.bias[co] : 0.f;
+      for (int k = 0; k < 9; ++k) w[g][k] = wts[(g * 9 + k) * cout_p + co];
+    const float b0 = bias ? bias[co] : 0.f;
 
     float ym[4], dn[4];
     uint32_t amw = 0;
@@ -81,6 +102,22 @@ __global__ __launch_bounds__(kThreads) void first_conv_pool_kernel(ConvArgs a, i
     for (int j = 0; j < 4; ++j) {
       // window pixels in torch's row-major order: s = 2 * py + px
       float yy[4];
+#if DRSA_FIRST_FWD_PK
+      // the window's two columns as two interleaved chains (independent packed fmas back to back)
+      fp2 acc[2] = {fp2{0.f, 0.f}, fp2{0.f, 0.f}};
+#pragma unroll
+      for (int k = 0; k < 9; ++k)
+#pragma unroll
+        for (int px = 0; px < 2; ++px)
+          acc[px] = __builtin_elementwise_fma(pr[k / 3][2 * j + px + k % 3], fp2{w[0][k], w[0][k]}, acc[px]);
+#pragma unroll
+      for (int px = 0; px < 2; ++px) {
+        const fp2 z = acc[px] + fp2{b0, b0};
+        // relu with NaN passed through: !(z <= 0) ? z : 0
+        yy[px] = z.x <= 0.f ? 0.f : z.x;
+        yy[2 + px] = z.y <= 0.f ? 0.f : z.y;
+      }
+#else
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const int py = s >> 1, px = s & 1;
@@ -88,24 +125,27 @@ __global__ __launch_bounds__(kThreads) void first_conv_pool_kernel(ConvArgs a, i
 #pragma unroll
         for (int k = 0; k < 9; ++k) acc = __builtin_fmaf(xin[py + k / 3][2 * j + px + k % 3], w[0][k], acc);
         const float z = acc + b0;
-        float y = z > 0.f ? z : 0.f;
-        if (z != z) y = z;   // relu(NaN) = NaN
-        yy[s] = y;
+        yy[s] = z <= 0.f ? 0.f : z;   // relu(NaN) = NaN
       }
-      // torch max_pool2d: first maximum in window order; NaN wins
+#endif
+      // torch max_pool2d: first maximum in window order; NaN wins (branch-free selects)
       int am = 0;
       float m = yy[0];
 #pragma unroll
-      for (int s = 1; s < 4; ++s)
-        if (yy[s] > m || (yy[s] != yy[s] && m == m)) { m = yy[s]; am = s; }
+      for (int s = 1; s < 4; ++s) {
+        // (y > m) | (isnan(y) & !isnan(m))  ==  !(y <= m) & !isnan(m)
+        const bool take = !(yy[s] <= m) & (m == m);
+        m = take ? yy[s] : m;
+        am = take ? s : am;
+      }
       ym[j] = m;
       amw |= (uint32_t)am << (8 * j);
       if constexpr (DEN == 1) {
         // off the ring (den_ring) nothing is stored: those lanes read one address (an L1
         // broadcast) instead of their scattered map pixel
         const int py = am >> 1, px = am & 1;
-        const size_t mi = ((size_t)co * H + 2 * qy + py) * W + 8 * g4 + 2 * j + px;
-        dn[j] = a.den_map[(den_ring && !on_ring) ? 0 : mi];
+        const int mi = co * H * W + mrow + py * W + 2 * j + px;
+        dn[j] = den_map[(den_ring && !on_ring) ? 0 : mi];
       } else if constexpr (DEN == 2) {
         // the rule's denominator at the argmax pixel only (every chain is per pixel)
         float xs[9];
@@ -116,9 +156,9 @@ __global__ __launch_bounds__(kThreads) void first_conv_pool_kernel(ConvArgs a, i
           const float c2 = xin[1 + k / 3][2 * j + k % 3], c3 = xin[1 + k / 3][2 * j + 1 + k % 3];
           xs[k] = am == 0 ? c0 : (am == 1 ? c1 : (am == 2 ? c2 : c3));
         }
-        const float bpos = a.bias ? a.bias[cout_p + co] : 0.f;
+        const float bpos = bias ? bias[cout_p + co] : 0.f;
         if constexpr (NG >= 2) {
-          const float bneg = a.bias ? a.bias[2 * cout_p + co] : 0.f;
+          const float bneg = bias ? bias[2 * cout_p + co] : 0.f;
           float a1 = 0.f;
 #pragma unroll
           for (int k = 0; k < 9; ++k) a1 = __builtin_fmaf(NG == 3 ? fmaxf(xs[k], 0.f) : xs[k], w[1][k], a1);
@@ -159,9 +199,9 @@ int launch_ng(const ConvArgs& a, int cout_p, int B, hipStream_t s) {
   // (store-bound), so one split
   const int cs = 1;
   const dim3 grid((total + kThreads - 1) / kThreads, cs);
-  if (!a.out_den) hipLaunchKernelGGL((first_conv_pool_kernel<NG, 0>), grid, dim3(kThreads), 0, s, a, cout_p, total);
-  else if (a.den_map) hipLaunchKernelGGL((first_conv_pool_kernel<NG, 1>), grid, dim3(kThreads), 0, s, a, cout_p, total);
-  else hipLaunchKernelGGL((first_conv_pool_kernel<NG, 2>), grid, dim3(kThreads), 0, s, a, cout_p, total);
+  if (!a.out_den) hipLaunchKernelGGL((first_conv_pool_kernel<NG, 0>), grid, dim3(kThreads), 0, s, a, a.wts, a.bias, a.den_map, cout_p, total);
+  else if (a.den_map) hipLaunchKernelGGL((first_conv_pool_kernel<NG, 1>), grid, dim3(kThreads), 0, s, a, a.wts, a.bias, a.den_map, cout_p, total);
+  else hipLaunchKernelGGL((first_conv_pool_kernel<NG, 2>), grid, dim3(kThreads), 0, s, a, a.wts, a.bias, a.den_map, cout_p, total);
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;
 }
@@ -170,6 +210,7 @@ int launch_ng(const ConvArgs& a, int cout_p, int B, hipStream_t s) {
 
 // Cin = 1, pooled output, W % 8 == 0 (checked by the caller, drsa_amd_conv_fwd)
 int drsa_first_conv_pool(const ConvArgs& a, int cout_p, int ng, int B, hipStream_t s) {
+  DRSA_REQUIRE((long long)a.cout * a.H * a.W < (1LL << 31), "conv_fwd: cout*H*W must be < 2^31 (32-bit den-map offsets)");
   if (ng == 1) return launch_ng<1>(a, cout_p, B, s);
   if (ng == 2) return launch_ng<2>(a, cout_p, B, s);
   return launch_ng<3>(a, cout_p, B, s);

@@ -42,7 +42,8 @@ def _at_argmax(full, am):
     return torch.gather(win, -1, am.long().unsqueeze(-1)).squeeze(-1)
 
 
-@pytest.mark.parametrize("ng,den", [(1, "none"), (1, "map"), (1, "eps"), (2, "gamma"), (3, "gamma")])
+@pytest.mark.parametrize("ng,den", [(1, "none"), (1, "map"), (1, "map_unaligned"), (1, "eps"), (2, "gamma"),
+                                    (3, "gamma")])
 @pytest.mark.parametrize("shape", [(3, 32, 16, 24), (2, 64, 128, 128), (1, 32, 8, 8)])
 def test_first_conv_pool_bit_exact(ng, den, shape):
     B, cout, H, W = shape
@@ -71,7 +72,7 @@ def test_first_conv_pool_bit_exact(ng, den, shape):
     y = torch.where(torch.isnan(z), z, z.clamp(min=0))
     y_ref, am_ref = _pool(y)
     den_map = None
-    if den == "map":
+    if den.startswith("map"):
         den_map = torch.rand(cout, H, W, generator=g) + 0.5
         den_full = den_map.unsqueeze(0).expand(B, -1, -1, -1).contiguous()
     elif den == "eps":
@@ -88,6 +89,9 @@ def test_first_conv_pool_bit_exact(ng, den, shape):
     # keep every device operand referenced until the kernel has run
     wd, bd = wdev.to(DEV), bdev.to(DEV)
     dm = None if den_map is None else den_map.to(DEV).contiguous()
+    if den == "map_unaligned":            # a map pointer off the 16-byte grid (the map is gathered per pixel)
+        dm = torch.cat([torch.zeros(1), den_map.flatten()]).to(DEV)[1:]
+        assert dm.data_ptr() % 16 != 0
     _capi.call("drsa_amd_conv_fwd", xd.data_ptr(), wd.data_ptr(), bd.data_ptr(), _capi.ptr(dm), out.data_ptr(),
                amax.data_ptr(), _capi.ptr(out_den), B, 1, cout, H, W, ng, 1, _capi.stream_ptr(DEV))
     torch.cuda.synchronize()
