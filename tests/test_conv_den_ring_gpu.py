@@ -54,7 +54,7 @@ def _first_layer(S, C, H2, W2, seed):
     return dmap, c4, outs
 
 
-@pytest.mark.parametrize("C,H2,W2", [(32, 64, 64), (32, 8, 16), (16, 6, 8), (8, 2, 8)])
+@pytest.mark.parametrize("C,H2,W2", [(32, 64, 64), (32, 8, 16), (16, 6, 8), (8, 2, 8), (64, 8, 16), (40, 4, 8)])
 def test_first_layer_ring_forward_and_map_interior(C, H2, W2):
     dmap, c4, outs = _first_layer(3, C, H2, W2, seed=C + H2)
     inner = dmap[:, 1:-1, 1:-1]
