@@ -31,6 +31,9 @@ template <int NG, int DEN>
 #ifndef DRSA_FIRST_FWD_RING2
 #define DRSA_FIRST_FWD_RING2 1
 #endif
+#ifndef DRSA_FIRST_FWD_RUNROLL
+#define DRSA_FIRST_FWD_RUNROLL 8   // ring pass: 8 channels of gathers in flight (4: +3 %, 16: +1 %, micro-benchmark)
+#endif
 #ifndef DRSA_FIRST_FWD_WPE
 #define DRSA_FIRST_FWD_WPE 1
 #endif
@@ -205,7 +208,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(DRSA_F
     }
     if constexpr (DEN == 3) {
       if (on_ring) {
-#pragma unroll 4
+#pragma unroll DRSA_FIRST_FWD_RUNROLL
         for (int co = cc; co < ce; ++co) {
           const uint32_t amw = am_sh[co - cc][threadIdx.x];
           float dn[4];
