@@ -139,7 +139,9 @@ size_t drsa_amd_conv_weight_floats(int cin, int cout, int ng);
  * create_model.py:61); pooled: out = window max, out_amax = row-major index of its first
  * maximum (NaN wins, torch max_pool2d), out_den = the denominator at that pixel.
  * Replaces the model forward (create_model.py:91-97) plus the modified forwards zennit's
- * BasicHook re-runs in backward (attribute.py:98-107 via zennit.core.BasicHook). */
+ * BasicHook re-runs in backward (attribute.py:98-107 via zennit.core.BasicHook).
+ * Like every conv entry point below, it needs one sample's channels x H x W < 2^31 (the kernels
+ * address a sample's planes with 32-bit offsets); otherwise it returns an error. */
 int drsa_amd_conv_fwd(const float* in, const float* wts, const float* bias, const float* den_map, float* out,
                       uint8_t* out_amax, float* out_den, int B, int cin, int cout, int H, int W, int ng,
                       int pool, void* stream);

@@ -88,6 +88,9 @@ def test_c_abi_argument_validation_without_gpu():
     assert lib.drsa_amd_drsa_vectors(p, p, q, q, 1, 4, 5, 4, 2, 2, 2, 0, p, p, None) == -1
     # pool kernel must divide the map
     assert lib.drsa_amd_maxpool_capture(p, None, p, q, None, 1, 4, 6, 8, 4, 4, None) == -1
+    # Cin = 1 forward: one sample's cout x H x W past 2^31 (32-bit offsets)
+    assert lib.drsa_amd_conv_fwd(p, p, p, p, p, q, p, 1, 1, 1 << 16, 256, 256, 1, 1, None) == -1
+    assert b"2^31" in lib.drsa_amd_last_error()
     # joint DRSA: no problems
     assert lib.drsa_amd_drsa_run_multi(0, None, 10, 1, None) == -1
     # workspace size query rejects unsupported problems
