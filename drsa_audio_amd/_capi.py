@@ -33,6 +33,8 @@ SIGNATURES = {
     "drsa_amd_drsa_fused_step_counted": (_i32, [_fp, _fp, _i64, _i32, _i32, _fp, _i64, _fp, _fp, _fp, _ip, _fp, _vp,
                                                 _sz, _vp]),
     "drsa_amd_drsa_finish_counted": (_i32, [_fp, _i64, _i32, _i32, _fp, _fp, _fp, _ip, _vp]),
+    "drsa_amd_drsa_coop_status": (_i32, [_vp, _i64, _i32, _i32, _ip, _vp]),
+    "drsa_amd_debug_coop_spin_budget": (_i32, [C.c_longlong]),
     "drsa_amd_drsa_objective": (_i32, [_fp, _fp, _i64, _i32, _i32, _fp, _fp, _vp, _sz, _vp]),
     "drsa_amd_drsa_run": (_i32, [_fp, _fp, _i64, _i32, _i32, _fp, _fp, _i32, _fp, _ip, _vp, _sz, _i32, _vp]),
     "drsa_amd_drsa_run_multi": (_i32, [_i32, _vp, _i32, _i32, _vp]),

@@ -30,6 +30,7 @@ int cu_count();
 #define DRSA_EINVAL (-1)
 #define DRSA_EWORKSPACE (-2)
 #define DRSA_EUNSUPPORTED (-3)
+#define DRSA_ETIMEOUT (-4)   /* a cooperative kernel's cross-workgroup hand-off timed out (results NaN) */
 
 #define DRSA_REQUIRE(cond, ...)           \
   do {                                    \

@@ -895,12 +895,19 @@ __global__ __launch_bounds__(fin_threads<polar_dim<DP>()>()) void drsa_finish_ke
 //   * the X T of an iteration whose error stops the loop is computed speculatively (the error is
 //     exchanged with its result) and dropped, so the returned X is the one polar_ns returns.
 // The workgroups spin on each other: the launch needs kCoopWG co-resident workgroups (one per CU,
-// 141 KB of LDS each), which the callers guarantee by launching nothing else that waits on them; a
-// spin that outlives kCoopSpinTicks (100 ms) gives up and poisons U_out with NaN instead of hanging.
+// 141 KB of LDS each), which the callers guarantee by launching nothing else that waits on them.
+// Failure is loud, never a hang and never silent: a spin that outlives both the wall-clock budget
+// (100 ms) and kCoopMinPolls polls (so a queue preempted mid-spin, whose wall clock jumps, still
+// polls ~20 ms after it resumes) gives up, sets the workspace's sticky status word, and poisons
+// U_out and f with NaN; every later finish of the run sees the word at its start and skips straight
+// to the poison (no further spinning, no diverged ticket to wait on).  drsa_amd_drsa_run /
+// _run_multi read the word back and return DRSA_ETIMEOUT; drsa_amd_drsa_coop_status reads it for a
+// run the caller captured into its own graph.  coop_reset clears ticket and status per run.
 // ---------------------------------------------------------------------------
 constexpr int kCoopWG = 8;
 constexpr int kCoopBW = 128 / kCoopWG;   // columns per workgroup (16x16x4 MFMA tiles)
-constexpr long long kCoopSpinTicks = 10000000;   // s_memrealtime runs at 100 MHz
+constexpr long long kCoopSpinTicks = 10000000;   // s_memrealtime runs at 100 MHz: 100 ms
+constexpr int kCoopMinPolls = 20000;             // >= ~20 ms of polling (one sc1 load + s_sleep each)
 
 // diagnostic build (-DDRSA_COOP_STAMP, scripts/probe_coop.py): phase times of the last launch's
 // workgroups, read back by drsa_amd_debug_coop_stamps; nothing in the kernel reads them
@@ -914,8 +921,9 @@ __device__ unsigned long long g_coop_stamps[kCoopWG][64];
 struct CoopXchg {
   float xb[2][128 * 128];        // X' by iteration parity (column block j written by workgroup j)
   float sc[2][kCoopWG][4];       // per parity and workgroup: error max, inf-norm partial
-  unsigned ticket;               // hand-off counter: kCoopWG arrivals per exchange, never reset
-  unsigned pad[63];
+  unsigned ticket;               // hand-off counter: kCoopWG arrivals per exchange, reset per run
+  unsigned status;               // sticky: 1 once any hand-off of the run timed out, reset per run
+  unsigned pad[62];
 };
 
 __device__ __forceinline__ void coop_st(float* p, float v) {
@@ -926,8 +934,18 @@ __device__ __forceinline__ float coop_ld(const float* p) {
 }
 
 // every thread calls after its agent-scope stores; returns false if the other workgroups did not
-// arrive within kCoopSpinTicks
-__device__ bool coop_exchange(unsigned* ticket, int* ok_sh) {
+// arrive within the spin budget (then the run's status word is set).
+// Visibility without release/acquire fences (MI355X_MICROARCH.md "Valid forms besides Guideline
+// 16's R1/R2" and the sc1 hand-off table's first row, which this matches cell for cell): every byte
+// handed over is stored by coop_st (a relaxed agent-scope atomic store = global_store_dword sc1,
+// 4 B) and read by coop_ld (global_load_dword sc1 to registers); every storing wave waits
+// vmcnt(0) before the workgroup barrier; ONE lane per workgroup then signals for all its stores
+// with one agent-scope atomic add on the ticket and polls it with relaxed agent-scope (sc1) loads;
+// the other waves load only after the barrier that lane joins; one workgroup per CU, hipMalloc'd
+// workspace.  (An agent release fence costs ~1.7 us and an acquire ~1.7 us per exchange here,
+// 5 exchanges per finish, for no change in what the table guarantees.)
+__device__ bool coop_exchange(unsigned* ticket, unsigned* status, int* ok_sh, long long spin_ticks,
+                              int min_polls) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -935,12 +953,13 @@ __device__ bool coop_exchange(unsigned* ticket, int* ok_sh) {
     const unsigned target = (old / kCoopWG + 1) * kCoopWG;
     const long long t0 = wall_clock64();
     int ok = 1;
-    for (;;) {
+    for (int polls = 0;; ++polls) {
       const unsigned v = __hip_atomic_load(ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if ((int)(v - target) >= 0) break;
-      if (wall_clock64() - t0 > kCoopSpinTicks) { ok = 0; break; }
+      if (polls >= min_polls && wall_clock64() - t0 > spin_ticks) { ok = 0; break; }
       __builtin_amdgcn_s_sleep(1);
     }
+    if (!ok) __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *ok_sh = ok;
   }
   __syncthreads();
@@ -955,7 +974,7 @@ constexpr size_t coop_lds_bytes() {
 __global__ __launch_bounds__(1024) void drsa_finish_coop_kernel(
     const float* __restrict__ gs, double n_total, int d, int K, int DKP, const float* __restrict__ U,
     float* __restrict__ U_out, float* __restrict__ f_out, int* __restrict__ step_counter, int f_stride_by_counter,
-    float tol, int max_iter, CoopXchg* __restrict__ xc) {
+    float tol, int max_iter, CoopXchg* __restrict__ xc, long long spin_ticks, int min_polls) {
   constexpr int DP = 128, LD = ns_ld<DP>(), NT = 1024, TLD = kCoopTLD, TPR = NT / DP;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* X = smem;                 // current X (full)
@@ -971,6 +990,21 @@ __global__ __launch_bounds__(1024) void drsa_finish_coop_kernel(
   const int tid = threadIdx.x, lane = lane_id(), w = wave_id(), j = blockIdx.x;
   const int lo = lane & 15, hi = lane >> 4;   // 16x16x4: A/B lane l -> index l & 15 at k = k0 + (l >> 4)
   const int dk = d / K;
+  // a hand-off of an earlier step of this run timed out: poison this step too, without spinning
+  if (tid == 0) ok_sh = __hip_atomic_load(&xc->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+  __syncthreads();
+  if (!ok_sh) {
+    for (int e = tid; e < DP * BW; e += NT) {
+      const int i = e / BW, pc = BW * j + e % BW, kc = pc / DKP, l = pc % DKP;
+      if (i < d && kc < K && l < dk) U_out[i * d + kc * dk + l] = __builtin_nanf("");
+    }
+    if (j == 0 && tid == 0) {
+      const int slot = f_stride_by_counter ? *step_counter : 0;
+      f_out[slot] = __builtin_nanf("");
+      if (f_stride_by_counter) *step_counter = slot + 1;
+    }
+    return;   // uniform per workgroup
+  }
   COOP_STAMP(0);
   const double f = finish_prologue<DP>(gs, n_total, d, K, DKP, U, X, true, dterm, cvec, &fsh);
   bool ok = true;
@@ -1064,7 +1098,7 @@ __global__ __launch_bounds__(1024) void drsa_finish_coop_kernel(
   }
   if (tid == 0) coop_st(&xc->sc[0][j][1], rmax_j);
   COOP_STAMP(3);
-  ok = coop_exchange(&xc->ticket, &ok_sh);
+  ok = coop_exchange(&xc->ticket, &xc->status, &ok_sh, spin_ticks, min_polls);
   COOP_STAMP(4);
   {
     const float dv = coop_ld(&xc->xb[0][(tid & (DP - 1)) * (DP + 1)]);
@@ -1105,7 +1139,7 @@ __global__ __launch_bounds__(1024) void drsa_finish_coop_kernel(
     xt_block(par);                   // speculative: dropped below if err stops the loop
     if (tid == 0) coop_st(&xc->sc[par][j][0], err);
     COOP_STAMP(6 + 5 * it);
-    ok = coop_exchange(&xc->ticket, &ok_sh);
+    ok = coop_exchange(&xc->ticket, &xc->status, &ok_sh, spin_ticks, min_polls);
     COOP_STAMP(7 + 5 * it);
     if (!ok) break;
     float ev[kCoopWG];
@@ -1138,7 +1172,7 @@ __global__ __launch_bounds__(1024) void drsa_finish_coop_kernel(
   }
   if (j == 0 && tid == 0) {
     const int slot = f_stride_by_counter ? *step_counter : 0;
-    f_out[slot] = (float)f;
+    f_out[slot] = ok ? (float)f : __builtin_nanf("");
     if (f_stride_by_counter) *step_counter = slot + 1;
   }
   COOP_STAMP(61);
@@ -1433,9 +1467,33 @@ CoopXchg* ws_xchg(void* ws, int64_t N, const Geom& g) {
   return (CoopXchg*)((e + 255) / 256 * 256);
 }
 
-// the exchange counter starts at 0 (kCoopWG arrivals per hand-off from there)
+// the exchange counter starts at 0 (kCoopWG arrivals per hand-off from there), the status word clear
 int coop_reset(CoopXchg* xc, hipStream_t s) {
-  if (xc) DRSA_HIP(hipMemsetAsync(&xc->ticket, 0, sizeof(unsigned), s));
+  static_assert(offsetof(CoopXchg, status) == offsetof(CoopXchg, ticket) + sizeof(unsigned), "ticket, status");
+  if (xc) DRSA_HIP(hipMemsetAsync(&xc->ticket, 0, 2 * sizeof(unsigned), s));
+  return DRSA_OK;
+}
+
+// spin budget of the cooperative finish (drsa_amd_debug_coop_spin_budget; default 100 ms + 20k polls)
+long long g_coop_spin_ticks = kCoopSpinTicks;
+int g_coop_min_polls = kCoopMinPolls;
+
+bool stream_capturing(hipStream_t s) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
+// reads the run's sticky status word back (synchronises stream s); DRSA_ETIMEOUT if it is set
+int coop_check(const CoopXchg* xc, hipStream_t s, const char* what) {
+  if (!xc) return DRSA_OK;
+  unsigned st = 0;
+  DRSA_HIP(hipMemcpyAsync(&st, &xc->status, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  DRSA_HIP(hipStreamSynchronize(s));
+  if (st) {
+    drsa::set_error("%s: a cooperative finish hand-off timed out (the %d workgroups were not co-resident "
+                    "within the spin budget); U and f are NaN from that step on", what, kCoopWG);
+    return DRSA_ETIMEOUT;
+  }
   return DRSA_OK;
 }
 
@@ -1445,7 +1503,7 @@ int launch_finish_coop(const float* gs, double n_total, const Geom& g, const flo
   const size_t lds = coop_lds_bytes();
   DRSA_SMEM(drsa_finish_coop_kernel, lds);
   hipLaunchKernelGGL(drsa_finish_coop_kernel, dim3(kCoopWG), dim3(1024), lds, s, gs, n_total, g.d, g.K, g.DKp, U, U_out,
-                     f_out, counter, by_counter, kPolarTol, kPolarMaxIter, xc);
+                     f_out, counter, by_counter, kPolarTol, kPolarMaxIter, xc, g_coop_spin_ticks, g_coop_min_polls);
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;
 }
@@ -1470,6 +1528,34 @@ int drsa_amd_debug_coop_stamps(unsigned long long* host_out) {
   return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_coop_stamps), sizeof(g_coop_stamps));
 }
 #endif
+
+int drsa_amd_drsa_coop_status(const void* ws, int64_t N, int d, int K, int* status_out, void* stream) {
+  const Geom g = geom(d, K);
+  DRSA_REQUIRE(g.ok && N > 0, "drsa_coop_status: unsupported d=%d K=%d or N <= 0", d, K);
+  DRSA_REQUIRE(ws && status_out, "drsa_coop_status: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  DRSA_REQUIRE(!(s && stream_capturing(s)), "drsa_coop_status: the stream is being captured");
+  *status_out = 0;
+  const CoopXchg* xc = ws_xchg(const_cast<void*>(ws), N, g);
+  if (!xc) return DRSA_OK;
+  unsigned st = 0;
+  DRSA_HIP(hipMemcpyAsync(&st, &xc->status, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  DRSA_HIP(hipStreamSynchronize(s));
+  *status_out = st ? 1 : 0;
+  return DRSA_OK;
+}
+
+int drsa_amd_debug_coop_spin_budget(long long ticks) {
+  DRSA_REQUIRE(ticks >= -1, "debug_coop_spin_budget: ticks must be >= -1");
+  if (ticks < 0) {
+    g_coop_spin_ticks = kCoopSpinTicks;
+    g_coop_min_polls = kCoopMinPolls;
+  } else {
+    g_coop_spin_ticks = ticks;
+    g_coop_min_polls = 0;
+  }
+  return DRSA_OK;
+}
 
 size_t drsa_amd_drsa_workspace_bytes(int64_t N, int d, int K) {
   const Geom g = geom(d, K);
@@ -1586,10 +1672,10 @@ int drsa_amd_drsa_run(const float* A, const float* C, int64_t N, int d, int K, f
   DRSA_REQUIRE(A && C && U_io && U_tmp && f_traj && counter, "drsa_run: null pointer");
   hipStream_t s = (hipStream_t)stream;
   float* gs = ws_gs(ws, N, g);
-  if (use_graph && s) {   // already inside a stream capture (e.g. a torch CUDA graph): record the plain sequence
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) use_graph = 0;
-  }
+  // already inside a stream capture (e.g. a torch CUDA graph): record the plain sequence, and leave
+  // the cooperative finish's status check to the caller (drsa_amd_drsa_coop_status)
+  const bool capturing = s && stream_capturing(s);
+  if (capturing) use_graph = 0;
   DRSA_HIP(hipMemsetAsync(counter, 0, sizeof(int), s));
   CoopXchg* xc = ws_xchg(ws, N, g);
   if (int rc = coop_reset(xc, s)) return rc;
@@ -1643,7 +1729,9 @@ int drsa_amd_drsa_run(const float* A, const float* C, int64_t N, int d, int K, f
     int rc = drsa_amd_drsa_partial(A, C, N, d, K, U_io, gs, ws, ws_size, stream);
     if (rc) return rc;
   }
-  return dispatch_finish(gs, (double)N, g, U_io, nullptr, f_traj, counter, 1, 1, kPolarTol, kPolarMaxIter, nullptr, s);
+  int rc = dispatch_finish(gs, (double)N, g, U_io, nullptr, f_traj, counter, 1, 1, kPolarTol, kPolarMaxIter, nullptr, s);
+  if (rc || capturing || steps == 0) return rc;
+  return coop_check(xc, s, "drsa_run");
 }
 
 // P independent problems (e.g. the C5 joint optimisation of two layers, optsubspaces.py:18-23
@@ -1776,6 +1864,11 @@ int drsa_amd_drsa_run_multi(int P, const drsa_amd_problem_t* probs, int steps, i
   // make sure nothing is pending on the side streams before they are destroyed
   for (int p = 0; p < P; ++p) (void)hipStreamSynchronize(side[p]);
   cleanup();
+  if (steps == 0 || stream_capturing(s)) return DRSA_OK;
+  for (int p = 0; p < P; ++p) {
+    const drsa_amd_problem_t& q = probs[p];
+    if (int rc2 = coop_check(ws_xchg(q.ws, q.N, geom(q.d, q.K)), s, "drsa_run_multi")) return rc2;
+  }
   return DRSA_OK;
 }
 

@@ -5,7 +5,8 @@
 //
 //   forward  (FWD_POOL / FWD_RELU):  z = conv(x; W) + b  ->  y = relu(z)  [-> 2x2 max-pool + argmax]
 //            plus, in the same pass over the input tile, the LRP denominator of the layer's rule:
-//            Gamma  (zennit 0.5.1):  den = (conv(x+; W+) + b+) + (conv(x-; W-) + b-)
+//            Gamma  (zennit 0.5.1):  den = (conv(x+; W+) + b+) + (conv(x-; W-) + b2)
+//            (the plan passes b2 = 0: zennit zeroes the x- term's bias)
 //            Epsilon:                               den = z
 //            WSquare / Flat:                        den = precomputed input-independent map
 //            den is stored only where the relevance can arrive: at the pool argmax.

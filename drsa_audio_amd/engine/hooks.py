@@ -113,12 +113,13 @@ def rule_relevance(rule, m: nn.Module, x: torch.Tensor, R: torch.Tensor) -> torc
             wp, wn = w + gam * w.clamp(min=0), w + gam * w.clamp(max=0)
             bp, bn = mod(b, lambda t: t + gam * t.clamp(min=0)), mod(b, lambda t: t + gam * t.clamp(max=0))
             z = _aff(m, x, w, b)
-            den_p = _aff(m, xp, wp, bp) + _aff(m, xn, wn, bn)
-            den_n = _aff(m, xp, wn, bn) + _aff(m, xn, wp, bp)
+            b0 = mod(b, torch.zeros_like)     # zennit 0.5.1: the x- terms carry no bias (zero_bias)
+            den_p = _aff(m, xp, wp, bp) + _aff(m, xn, wn, b0)
+            den_n = _aff(m, xp, wn, bn) + _aff(m, xn, wp, b0)
             gp = R * (z > 0) / _stab(den_p, rule.stabilizer)
             gn = R * (z < 0) / _stab(den_n, rule.stabilizer)
-            fs = [lambda t: _aff(m, t, wp, bp), lambda t: _aff(m, t, wn, bn),
-                  lambda t: _aff(m, t, wn, bn), lambda t: _aff(m, t, wp, bp)]
+            fs = [lambda t: _aff(m, t, wp, bp), lambda t: _aff(m, t, wn, b0),
+                  lambda t: _aff(m, t, wn, bn), lambda t: _aff(m, t, wp, b0)]
             return sum(_grad(fs, [xp, xn, xp, xn], [gp, gp, gn, gn]))
         wp, wn = w.clamp(min=0), w.clamp(max=0)
         bp, bn, b0 = mod(b, lambda t: t.clamp(min=0)), mod(b, lambda t: t.clamp(max=0)), mod(b, torch.zeros_like)

@@ -374,9 +374,11 @@ class LRPEngine:
         k = st.rule_kind
         if k == "gamma":
             g = st.rule.gamma
+            # zennit 0.5.1 Gamma: den+ = (conv(x+; W+) + b+) + conv(x-; W-), the x- term's
+            # modifier zeroing the bias (zero_bias), as for ZPlus below. Only den+ is
+            # formed: R reaches the conv through its ReLU, so g- = R [z < 0] / den- is 0
             Wp, Wn = W + g * W.clamp(min=0), W + g * W.clamp(max=0)
-            bp, bn = bd + g * bd.clamp(min=0), bd + g * bd.clamp(max=0)
-            bias3[1, :st.cout], bias3[2, :st.cout] = bp, bn
+            bias3[1, :st.cout], bias3[2, :st.cout] = bd + g * bd.clamp(min=0), 0.0
             sets = [W, Wp] + ([Wn] if not st.input_nonneg else [])
             st.ng_fwd = len(sets)
             st.den_kind = "gamma"

@@ -72,6 +72,16 @@ class DrsaWorkspace:
     def nbytes(self) -> int:
         return self.buf.numel()
 
+    def coop_status(self) -> int:
+        """1 if the cooperative finish of the last run on this workspace timed out (U, f NaN from
+        that step on), else 0.  drsa_run raises on it by itself; this is for a run the caller
+        captured into its own graph (drsa_amd_drsa_coop_status; synchronises the stream)."""
+        import ctypes
+        st = ctypes.c_int(0)
+        _capi.call("drsa_amd_drsa_coop_status", self.ptr, self.N, self.d, self.K, ctypes.addressof(st),
+                   _capi.stream_ptr(self.buf.device))
+        return st.value
+
 
 def _check_problem(A: torch.Tensor, C: torch.Tensor, U: torch.Tensor, K: int):
     dt = A.dtype if A.dtype in (torch.bfloat16, torch.float16) else torch.float32

@@ -2,7 +2,8 @@
 
 Semantics (reference name maps ``constants.py:27-51``):
   Epsilon(ε)   R_in = x ⊙ Jᵀ_W(R / stab_ε(z))
-  Gamma(γ, ε)  W± = W + γ·W.clamp(min/max=0) (bias likewise); positive/negative output split
+  Gamma(γ, ε)  W± = W + γ·W.clamp(min/max=0) (bias likewise); positive/negative output split;
+               den± = f(x+; W±, b±) + f(x-; W∓, 0) (zennit 0.5.1 zero_bias on the x- terms)
   WSquare(ε)   R_in = Jᵀ_{W²}(R / stab_ε(conv(1; W², b²)))
   Flat(ε)      as WSquare with W -> 1, b -> 0
   Pass()       R_in = R_out (activation layers only)

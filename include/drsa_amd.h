@@ -27,6 +27,7 @@ extern "C" {
 #define DRSA_EINVAL (-1)
 #define DRSA_EWORKSPACE (-2)
 #define DRSA_EUNSUPPORTED (-3)
+#define DRSA_ETIMEOUT (-4)   /* a cooperative kernel's cross-workgroup hand-off timed out (results NaN) */
 
 const char* drsa_amd_last_error(void);
 int drsa_amd_version(void);
@@ -98,10 +99,24 @@ int drsa_amd_drsa_objective(const float* A, const float* C, int64_t N, int d, in
  * that hand X over through the workspace (bit-identical to drsa_amd_drsa_finish's single
  * workgroup).  They wait on each other, so they must become resident together: work running
  * concurrently on other streams only delays them, unless it holds more than 248 CUs while itself
- * waiting on this stream (a wait that outlives 100 ms gives up and writes NaN into U_out). */
+ * waiting on this stream.  A wait that outlives 100 ms (and 20k polls) gives up: U and f are NaN
+ * from that step on, the run's later finishes skip straight to NaN, and drsa_amd_drsa_run returns
+ * DRSA_ETIMEOUT (it reads the workspace's status word back, synchronising the stream, at d > 64).
+ * Inside a caller's stream capture that read is skipped: check drsa_amd_drsa_coop_status after
+ * the replay. */
 int drsa_amd_drsa_run(const float* A, const float* C, int64_t N, int d, int K, float* U_io, float* U_tmp,
                       int steps, float* f_traj, int* counter, void* workspace, size_t workspace_bytes,
                       int use_graph, void* stream);
+
+/* Status of the cooperative finish of the last drsa_amd_drsa_run / _run_multi on this workspace
+ * (same N, d, K): *status_out = 1 if a hand-off timed out (U, f NaN), else 0 (always 0 at d <= 64).
+ * Synchronises `stream`; not callable while it is being captured. */
+int drsa_amd_drsa_coop_status(const void* workspace, int64_t N, int d, int K, int* status_out, void* stream);
+
+/* Test hook: the cooperative finish's spin budget in 100 MHz ticks for launches enqueued from now on
+ * (0: give up at the first poll that finds a workgroup missing, with no minimum poll count);
+ * -1 restores the default (100 ms and 20k polls). */
+int drsa_amd_debug_coop_spin_budget(long long ticks);
 
 /* orthogonalize (drsa.py:201-221): U_out = V (V^T V)^{-1/2}, Newton-Schulz on device, d <= 128.
  * Stop rule (polar_ns.h): iterate X <- X (3I - X^T X)/2 from the scaled V until max|X^T X - I| is
@@ -134,7 +149,8 @@ size_t drsa_amd_conv_weight_floats(int cin, int cout, int ng);
 
 /* Forward conv3x3 'same' + bias + ReLU [+ max-pool with argmax] and the layer's LRP
  * denominator (Gamma: ng = 2 for x >= 0, where set 1 is applied to x as is, or ng = 3 with
- * the x+ / x- split; Epsilon: ng = 1; WSquare/Flat: den_map).
+ * the x+ / x- split; den = (z1 + bias[1]) + (z2 + bias[2]), and zennit 0.5.1's Gamma passes
+ * bias[2] = 0 because its x- terms' modifiers zero the bias; Epsilon: ng = 1; WSquare/Flat: den_map).
  * pool: 0 = none (out and out_den at full resolution), 1 = 2x2, 2 = 2x4 (VGGish's (2,4) pool,
  * create_model.py:61); pooled: out = window max, out_amax = row-major index of its first
  * maximum (NaN wins, torch max_pool2d), out_den = the denominator at that pixel.
@@ -330,6 +346,7 @@ int drsa_amd_drsa_partial_f16(const uint16_t* A, const uint16_t* C, int64_t N, i
 
 /* P independent problems advanced S steps together (C5: two layers, K=16 each, one graph).
  * Replaces the sequential per-layer loop of optsubspaces.py:18-23 / drsa.main. */
+/* Returns DRSA_ETIMEOUT like drsa_amd_drsa_run when a problem's cooperative finish timed out. */
 int drsa_amd_drsa_run_multi(int P, const drsa_amd_problem_t* probs, int steps, int use_graph, void* stream);
 
 /* P independent fp32 problems sharing one padded geometry (same pow2(d) and concept width; N may

@@ -20,7 +20,9 @@ Rule arithmetic (z = f(x; W, b), Jᵀ_W g = input-gradient of f with weights W):
   stab_ε(t)  = t + ε·(sign(t) + [t == 0])
   Epsilon    : R_in = x ⊙ Jᵀ_W( R / stab_ε(z) )
   Gamma(γ)   : W± = W + γ·W.clamp(min/max=0) (bias likewise);
-               z0 = f(x⁺;W⁺,b⁺), z1 = f(x⁻;W⁻,b⁻), z2 = f(x⁺;W⁻,b⁻), z3 = f(x⁻;W⁺,b⁺)
+               z0 = f(x⁺;W⁺,b⁺), z1 = f(x⁻;W⁻,0), z2 = f(x⁺;W⁻,b⁻), z3 = f(x⁻;W⁺,0)
+               (zennit 0.5.1 zeroes the bias of the x⁻ terms' GammaMod with zero_bias(), as
+               for ZPlus / AlphaBeta: each denominator holds the bias once)
                g₊ = R·[z>0]/stab(z0+z1),  g₋ = R·[z<0]/stab(z2+z3)
                R_in = x⁺⊙Jᵀ_{W⁺}g₊ + x⁻⊙Jᵀ_{W⁻}g₊ + x⁺⊙Jᵀ_{W⁻}g₋ + x⁻⊙Jᵀ_{W⁺}g₋
   WSquare    : R_in = Jᵀ_{W²}( R / stab(f(1; W², b²)) )            (no x⊙)
@@ -415,11 +417,14 @@ def rule_backward_analytic(L: Layer, rule: RuleSpec, x: torch.Tensor, z: torch.T
         wn = w + gam * w.clamp(max=0)
         bp = _mod(b, lambda t: t + gam * t.clamp(min=0))
         bn = _mod(b, lambda t: t + gam * t.clamp(max=0))
+        b0 = _mod(b, torch.zeros_like)
         xp, xn = x.clamp(min=0), x.clamp(max=0)
+        # zennit 0.5.1 Gamma: the x- terms' modifiers are GammaMod(..., zero_params=zero_bias(...)),
+        # so the bias enters each denominator once (as in ZPlus / AlphaBeta below)
         z0 = _aff(L, xp, wp, bp, ops)
-        z1 = _aff(L, xn, wn, bn, ops)
+        z1 = _aff(L, xn, wn, b0, ops)
         z2 = _aff(L, xp, wn, bn, ops)
-        z3 = _aff(L, xn, wp, bp, ops)
+        z3 = _aff(L, xn, wp, b0, ops)
         gpos = R * (z > 0) / stabilize(z0 + z1, eps)
         gneg = R * (z < 0) / stabilize(z2 + z3, eps)
         return (xp * _aff_jt(L, x.shape, wp, gpos, ops) + xn * _aff_jt(L, x.shape, wn, gpos, ops)
@@ -483,8 +488,10 @@ def rule_backward_zennit(L: Layer, rule: RuleSpec, x: torch.Tensor, z: torch.Ten
         wn = w + gam * w.clamp(max=0)
         bp = _mod(b, lambda t: t + gam * t.clamp(min=0))
         bn = _mod(b, lambda t: t + gam * t.clamp(max=0))
+        b0 = _mod(b, torch.zeros_like)
         inputs = [x.clamp(min=0), x.clamp(max=0), x.clamp(min=0), x.clamp(max=0), x]
-        params = [(wp, bp), (wn, bn), (wn, bn), (wp, bp), (w, b)]
+        # GammaMod(min=0), GammaMod(max=0, zero_bias), GammaMod(max=0), GammaMod(min=0, zero_bias), NoMod
+        params = [(wp, bp), (wn, b0), (wn, bn), (wp, b0), (w, b)]
         ins, outs = run(inputs, params)
         o = [t.detach() for t in outs]
         gpos = R * (o[4] > 0) / stabilize(o[0] + o[1], eps)

@@ -114,6 +114,42 @@ def test_fused_run_equals_partial_finish_loop_bitwise(N, d, K):
     assert torch.equal(U_run, U)
 
 
+def test_coop_finish_timeout_is_loud_and_recoverable():
+    """VERDICT r05 item 2 / ADVICE r05: the cooperative DP = 128 finish must never fail silently.
+    With the spin budget forced to 0 (drsa_amd_debug_coop_spin_budget) some workgroup gives up at its
+    first poll that finds a partner missing: drsa_run must raise DrsaAmdError (DRSA_ETIMEOUT), the
+    workspace's status word must read 1, U must be NaN, and the run's later finishes must skip
+    straight to NaN (no 100 ms spins: the 40-step run ends in well under a second).  With the budget
+    restored the next run on the same workspace succeeds and equals a fresh workspace's run bit
+    for bit (coop_reset clears the ticket and the status per run)."""
+    import time
+    from drsa_audio_amd import _capi
+    from drsa_audio_amd.xai.drsa.drsa import DrsaWorkspace, drsa_run
+    N, d, K, steps = 4096, 128, 16, 40
+    A, C = drsa_inputs(N, d, 5)
+    Ag, Cg, Ug = _gpu(A, C, _u0(d, 2))
+    ws = DrsaWorkspace(N, d, K, DEV)
+    side = torch.cuda.Stream()
+    _capi.call("drsa_amd_debug_coop_spin_budget", 0)
+    try:
+        t0 = time.time()
+        with torch.cuda.stream(side):
+            with pytest.raises(_capi.DrsaAmdError, match="timed out"):
+                drsa_run(Ag, Cg, Ug, K, steps, ws=ws)
+        torch.cuda.synchronize()
+        assert time.time() - t0 < 5.0
+        assert ws.coop_status() == 1
+    finally:
+        _capi.call("drsa_amd_debug_coop_spin_budget", -1)
+    with torch.cuda.stream(side):
+        U1, t1 = drsa_run(Ag, Cg, Ug, K, steps, ws=ws)
+        U2, t2 = drsa_run(Ag, Cg, Ug, K, steps)
+    torch.cuda.synchronize()
+    assert ws.coop_status() == 0
+    assert torch.isfinite(U1).all() and torch.isfinite(t1).all()
+    assert torch.equal(U1, U2) and torch.equal(t1, t2)
+
+
 def test_sharded_fused_step_equals_two_call_form_bitwise():
     """sharded_run's fused path (drsa_amd_drsa_fused_step: finish + the next partial in one
     launch, caller-owned buffers) equals the partial / finish two-call form bit for bit."""

@@ -91,14 +91,14 @@ def _hand_lrp(W1, b1, W2, b2, x, c, gam, eps):
     """float64 loops: conv3x3(1->2)+ReLU+maxpool2 -> Linear(8->3); Gamma on conv, Epsilon on linear."""
     H = x.shape[0]
     z = np.zeros((2, H, H)); zp = np.zeros((2, H, H))
-    Wp = W1 + gam * np.maximum(W1, 0); bp = b1 + gam * np.maximum(b1, 0); bn = b1 + gam * np.minimum(b1, 0)
+    Wp = W1 + gam * np.maximum(W1, 0); bp = b1 + gam * np.maximum(b1, 0)
     xp = np.pad(x, 1)
     for o in range(2):
         for i in range(H):
             for j in range(H):
                 patch = xp[i:i + 3, j:j + 3]
                 z[o, i, j] = (patch * W1[o]).sum() + b1[o]
-                zp[o, i, j] = (np.maximum(patch, 0) * Wp[o]).sum() + bp[o] + (np.minimum(patch, 0) * (W1[o] + gam * np.minimum(W1[o], 0))).sum() + bn[o]
+                zp[o, i, j] = (np.maximum(patch, 0) * Wp[o]).sum() + bp[o] + (np.minimum(patch, 0) * (W1[o] + gam * np.minimum(W1[o], 0))).sum()
     a = np.maximum(z, 0)
     P = np.zeros((2, H // 2, H // 2)); arg = {}
     for o in range(2):
@@ -305,3 +305,66 @@ def test_zplus_is_the_large_gamma_limit_on_nonnegative_input():
     Rzp = lrp_ref.rule_backward_analytic(L, ("zplus", 1e-12), x, z, R)
     Rg = lrp_ref.rule_backward_analytic(L, ("gamma", 1e7, 1e-12), x, z, R)
     assert (Rzp - Rg).abs().max() <= 1e-5 * Rzp.abs().max()
+
+
+def _gamma_conv_1px(b):
+    """Conv2d(1->1, 3x3, padding 1) on a 1x1 input: only the centre tap w_c = 1.5 meets the input."""
+    conv = nn.Conv2d(1, 1, 3, padding=1).double()
+    with torch.no_grad():
+        conv.weight.copy_(torch.tensor([[[[0.3, -0.7, 0.2], [0.9, 1.5, -0.4], [0.1, 0.6, -0.2]]]]))
+        conv.bias.fill_(b)
+    return conv, lrp_ref.Layer("c", conv, "conv")
+
+
+@pytest.mark.parametrize("mode", ["analytic", "zennit"])
+def test_gamma_bias_known_answer(mode):
+    """Known answer separating the two candidate Gamma bias conventions.
+
+    zennit 0.5.1 ``rules.Gamma`` builds its five modified forwards from ``GammaMod(γ, min=0)``,
+    ``GammaMod(γ, max=0, zero_params=zero_bias(...))``, ``GammaMod(γ, max=0)``,
+    ``GammaMod(γ, min=0, zero_params=zero_bias(...))`` and the plain layer, i.e. the x⁻ terms
+    carry no bias (the same ``zero_bias`` form as its ZPlus / AlphaBeta).  On x = 2 ≥ 0,
+    w_c = 1.5, b = -0.5, γ = 0.25, R = 1:
+      W⁺_c = 1.5 + 0.25·1.5 = 1.875,  b⁺ = -0.5,  b⁻ = -0.5 + 0.25·(-0.5) = -0.625
+      z = 2·1.5 - 0.5 = 2.5 > 0
+      zennit:            den₊ = 2·1.875 + b⁺          = 3.25   → R_in = 3.75 / 3.25  = 15/13
+      bias in both terms: den₊ = 2·1.875 + b⁺ + b⁻    = 2.625  → R_in = 3.75 / 2.625 = 10/7
+    """
+    conv, L = _gamma_conv_1px(-0.5)
+    x = torch.full((1, 1, 1, 1), 2.0, dtype=torch.float64)
+    z = conv(x).detach()
+    assert float(z) == 2.5
+    fn = lrp_ref.rule_backward_analytic if mode == "analytic" else lrp_ref.rule_backward_zennit
+    Rin = fn(L, ("gamma", 0.25, 1e-12), x, z, torch.ones_like(z))
+    assert abs(float(Rin) - 15 / 13) < 1e-10
+    assert abs(float(Rin) - 10 / 7) > 0.2
+
+
+def test_gamma_bias_known_answer_slow_path_and_plan_bias():
+    """The same known answer through the custom-Hook slow path's per-module arithmetic, and the
+    plan's Gamma bias rows (engine/plan.py): row 1 = b⁺, row 2 (the x⁻ term's bias) = 0."""
+    from drsa_audio_amd.engine.hooks import rule_relevance
+    from drsa_audio_amd.zennit.rules import Gamma
+    conv, _ = _gamma_conv_1px(-0.5)
+    x = torch.full((1, 1, 1, 1), 2.0, dtype=torch.float64)
+    Rin = rule_relevance(Gamma(0.25, 1e-12), conv, x, torch.ones(1, 1, 1, 1, dtype=torch.float64))
+    assert abs(float(Rin) - 15 / 13) < 1e-10
+    # a signed input exercises the x⁻ terms: den₊ = (x⁺·W⁺ + b⁺) + x⁻·W⁻ (no bias)
+    torch.manual_seed(4)
+    m = nn.Conv2d(2, 3, 3, padding=1).double()
+    with torch.no_grad():
+        m.bias.copy_(torch.tensor([-0.3, 0.2, -0.1]))
+    xs = torch.randn(1, 2, 5, 5, dtype=torch.float64)
+    zs = m(xs).detach()
+    R = torch.rand_like(zs) * (zs > 0)
+    L = lrp_ref.Layer("c", m, "conv")
+    want = lrp_ref.rule_backward_analytic(L, ("gamma", 0.3, 1e-9), xs, zs, R)
+    got = rule_relevance(Gamma(0.3, 1e-9), m, xs, R)
+    torch.testing.assert_close(got, want, rtol=1e-10, atol=1e-12)
+    w, b, g = m.weight.detach(), m.bias.detach(), 0.3
+    c2 = nn.functional.conv2d
+    bp = (b + g * b.clamp(min=0)).view(1, -1, 1, 1)
+    den = (c2(xs.clamp(min=0), w + g * w.clamp(min=0), padding=1) + bp
+           + c2(xs.clamp(max=0), w + g * w.clamp(max=0), padding=1))
+    expect = (R * (den - bp) / lrp_ref.stabilize(den, 1e-9)).sum()   # conservation: the bias absorbs b⁺ once
+    assert abs(float(want.sum() - expect)) <= 1e-9 * float(R.abs().sum())
