@@ -194,6 +194,37 @@ def cpu_drsa_baseline(reps=7):
 
 
 # --------------------------------------------------------------------------- DRSA
+def graph_replays(fn, device, steps, reps=7):
+    """Steady-state timing of a whole fixed-step DRSA run (median of >= 20 steady-state
+    steps): `fn` (one run of `steps` steps) runs once eagerly (library, side-stream
+    pool, workspaces warm), is captured ONCE into a CUDA graph on a side stream (the C ABI records its
+    plain sequence inside a caller's capture), and the graph is replayed `reps` times, each replay
+    timed with HIP events on that stream.  Returns (per-step ms: median, min, max; fn's outputs as
+    left by the last replay)."""
+    s = torch.cuda.Stream(device)
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.synchronize(device)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        out = fn()
+    ts = []
+    with torch.cuda.stream(s):
+        g.replay()
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            g.replay()
+            e1.record(s)
+            torch.cuda.synchronize(device)
+            ts.append(e0.elapsed_time(e1) / steps)
+    return float(np.median(ts)), float(min(ts)), float(max(ts)), out
+
+
+def _spread(med, lo, hi, reps=7):
+    return {"median": med, "min": lo, "max": hi, "replays": reps}
+
+
 def drsa_bench(device, steps=200):
     from drsa_audio_amd.utils.synthetic import drsa_inputs
     from drsa_audio_amd import _capi
@@ -203,14 +234,10 @@ def drsa_bench(device, steps=200):
     U0 = np.load(os.path.join(ROOT, "tests", "golden", "u64_seed42.npy"))
     Ag, Cg, Ug = (torch.from_numpy(v).to(device) for v in (A, C, U0))
     ws = DrsaWorkspace(N, d, K, device)
+    med, lo, hi, (U, traj) = graph_replays(lambda: drsa_run(Ag, Cg, Ug, K, steps, ws), device, steps)
+    dt = med * 1e-3 * steps
     s = torch.cuda.Stream(device)
     with torch.cuda.stream(s):
-        drsa_run(Ag, Cg, Ug, K, 4, ws)                       # warm-up (graph instantiate)
-        torch.cuda.synchronize(device)
-        t0 = time.perf_counter()
-        U, traj = drsa_run(Ag, Cg, Ug, K, steps, ws)
-        torch.cuda.synchronize(device)
-        dt = time.perf_counter() - t0
         # the reference's 2000-step C3 run (tests/golden/drsa_long_fixture.npz): max deviation
         fx = np.load(os.path.join(ROOT, "tests", "golden", "drsa_long_fixture.npz"))
         _, t2000 = drsa_run(Ag, Cg, Ug, K, 2000, ws)
@@ -238,8 +265,9 @@ def drsa_bench(device, steps=200):
     ms = dt / steps * 1e3
     tflops = flop / (ms * 1e-3) / 1e12
     tp_ms = float(np.median(tp))
-    return {"config": "C3: N=20000, d=64, K=4 (synthetic normalised A=|N(0,1)|, C~N(0,1)), whole S-step loop "
-                      "as one replayed hipGraph", "ms_per_step": ms, "vector_steps_per_s": N * steps / dt,
+    return {"config": f"C3: N=20000, d=64, K=4 (synthetic normalised A=|N(0,1)|, C~N(0,1)), a {steps}-step run "
+                      "captured once as a graph, replayed 7 times (HIP events); ms_per_step = median replay / steps",
+            "ms_per_step": ms, "ms_per_step_spread": _spread(med, lo, hi), "vector_steps_per_s": N * steps / dt,
             "steps": steps, "objective_final": float(traj[-1]),
             "traj_dev_2000_vs_reference": dev2000,
             "roofline": {"bound": "mfma", "kernel": "drsa_partial (+ slab reduce)",
@@ -289,44 +317,30 @@ def drsa_joint_bench(device, steps=200):
         A, C = drsa_inputs(N, d, seed)
         U0 = np.linalg.qr(np.random.default_rng(seed).standard_normal((d, d)))[0].astype(np.float32)
         probs.append(tuple(torch.from_numpy(v).to(device) for v in (A, C, U0)) + (K,))
-    s = torch.cuda.Stream(device)
-    with torch.cuda.stream(s):
-        drsa_run_joint(probs, 4)
-        torch.cuda.synchronize(device)
-        t0 = time.perf_counter()
-        out = drsa_run_joint(probs, steps)
-        torch.cuda.synchronize(device)
-        dt = time.perf_counter() - t0
-        t0 = time.perf_counter()
-        for A, C, U0, K_ in probs:
-            drsa_run(A, C, U0, K_, steps)
-        torch.cuda.synchronize(device)
-        dt_seq = time.perf_counter() - t0
-        # bf16 inputs + bf16 MFMA projection (C5; fp32 accumulate)
-        probs16 = [(A.to(torch.bfloat16), C.to(torch.bfloat16), U0, K_) for A, C, U0, K_ in probs]
-        drsa_run_joint(probs16, 4)
-        torch.cuda.synchronize(device)
-        t0 = time.perf_counter()
-        out16 = drsa_run_joint(probs16, steps)
-        torch.cuda.synchronize(device)
-        dt16 = time.perf_counter() - t0
-        # fp16 inputs + fp16 MFMA projection (C5 "fp16 MFMA projection")
-        probsh = [(A.to(torch.float16), C.to(torch.float16), U0, K_) for A, C, U0, K_ in probs]
-        drsa_run_joint(probsh, 4)
-        torch.cuda.synchronize(device)
-        t0 = time.perf_counter()
-        outh = drsa_run_joint(probsh, steps)
-        torch.cuda.synchronize(device)
-        dth = time.perf_counter() - t0
+    # every leg: one fixed-step run captured once, replayed 7 times (graph_replays)
+    j = graph_replays(lambda: drsa_run_joint(probs, steps), device, steps)
+    out = j[3]
+    sq = graph_replays(lambda: [drsa_run(A, C, U0, K_, steps) for A, C, U0, K_ in probs], device, steps)
+    # bf16 inputs + bf16 MFMA projection (C5; fp32 accumulate)
+    probs16 = [(A.to(torch.bfloat16), C.to(torch.bfloat16), U0, K_) for A, C, U0, K_ in probs]
+    b = graph_replays(lambda: drsa_run_joint(probs16, steps), device, steps)
+    out16 = b[3]
+    # fp16 inputs + fp16 MFMA projection (C5 "fp16 MFMA projection")
+    probsh = [(A.to(torch.float16), C.to(torch.float16), U0, K_) for A, C, U0, K_ in probs]
+    h = graph_replays(lambda: drsa_run_joint(probsh, steps), device, steps)
+    outh = h[3]
+    dt, dt_seq, dt16, dth = (x[0] * 1e-3 * steps for x in (j, sq, b, h))
     flop = 2 * 8.0 * N * d * d
     rel16 = max(abs(float(a[1][-1]) - float(b[1][-1])) / abs(float(b[1][-1])) for a, b in zip(out16, out))
     relh = max(abs(float(a[1][-1]) - float(b[1][-1])) / abs(float(b[1][-1])) for a, b in zip(outh, out))
-    return {"config": "C5 joint: 2 problems (VGGish j=26, j=33) x N=20000, d=128, K=16, one graph",
-            "ms_per_joint_step": dt / steps * 1e3, "ms_per_step_sequential_runs": dt_seq / steps * 1e3,
-            "bf16": {"ms_per_joint_step": dt16 / steps * 1e3, "objective_rel_diff_vs_fp32_after_steps": rel16,
-                     "tolerance": 1e-2},
-            "fp16": {"ms_per_joint_step": dth / steps * 1e3, "objective_rel_diff_vs_fp32_after_steps": relh,
-                     "tolerance": 1e-2},
+    return {"config": f"C5 joint: 2 problems (VGGish j=26, j=33) x N=20000, d=128, K=16; each leg a {steps}-step "
+                      "run captured once as a graph and replayed 7 times (HIP events), median / min / max per step",
+            "ms_per_joint_step": dt / steps * 1e3, "ms_per_joint_step_spread": _spread(*j[:3]),
+            "ms_per_step_sequential_runs": dt_seq / steps * 1e3, "sequential_spread": _spread(*sq[:3]),
+            "bf16": {"ms_per_joint_step": dt16 / steps * 1e3, "spread": _spread(*b[:3]),
+                     "objective_rel_diff_vs_fp32_after_steps": rel16, "tolerance": 1e-2},
+            "fp16": {"ms_per_joint_step": dth / steps * 1e3, "spread": _spread(*h[:3]),
+                     "objective_rel_diff_vs_fp32_after_steps": relh, "tolerance": 1e-2},
             "vector_steps_per_s": 2 * N * steps / dt, "tflops_algorithmic": flop * steps / dt / 1e12,
             "objective_final": [float(t[-1]) for _, t in out]}
 

@@ -1764,27 +1764,37 @@ int drsa_amd_drsa_run_multi(int P, const drsa_amd_problem_t* probs, int steps, i
     return DRSA_OK;
   }
   hipStream_t s = (hipStream_t)stream;
-  hipStream_t side[64] = {nullptr};
-  hipEvent_t ev_fork = nullptr, ev_join[64] = {nullptr};
-  int rc = DRSA_OK;
-  auto cleanup = [&]() {
-    for (int p = 0; p < P; ++p) {
-      if (side[p]) (void)hipStreamDestroy(side[p]);
-      if (ev_join[p]) (void)hipEventDestroy(ev_join[p]);
-    }
-    if (ev_fork) (void)hipEventDestroy(ev_fork);
+  // inside a caller's stream capture (a torch CUDA graph of the whole run): record the forked plain
+  // sequence into it (no graph of our own, no host synchronisation, no status read-back)
+  const bool capturing = s && stream_capturing(s);
+  if (capturing) use_graph = 0;
+  // side streams and fork/join events come from a per-thread, per-device pool that lives as long
+  // as the thread: a captured graph's forks must not be destroyed before the capture ends
+  struct SidePool {
+    hipStream_t st[64] = {nullptr};
+    hipEvent_t join[64] = {nullptr};
+    hipEvent_t fork = nullptr;
   };
+  thread_local SidePool pools[16];
+  int dev = 0;
+  DRSA_HIP(hipGetDevice(&dev));
+  DRSA_REQUIRE(dev >= 0 && dev < 16, "drsa_run_multi: device index %d >= 16", dev);
+  SidePool& pool = pools[dev];
+  hipStream_t* side = pool.st;
+  hipEvent_t* ev_join = pool.join;
+  int rc = DRSA_OK;
+  auto cleanup = [&]() {};
   auto hip_ok = [&](hipError_t e, const char* what) -> bool {
     if (e == hipSuccess) return true;
     drsa::set_error("drsa_run_multi: %s: %s", what, hipGetErrorString(e));
     rc = (int)e;
     return false;
   };
-  if (!hip_ok(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming), "event")) { cleanup(); return rc; }
+  if (!pool.fork && !hip_ok(hipEventCreateWithFlags(&pool.fork, hipEventDisableTiming), "event")) return rc;
+  hipEvent_t ev_fork = pool.fork;
   for (int p = 0; p < P; ++p) {
-    if (!hip_ok(hipStreamCreateWithFlags(&side[p], hipStreamNonBlocking), "stream") ||
-        !hip_ok(hipEventCreateWithFlags(&ev_join[p], hipEventDisableTiming), "event")) {
-      cleanup();
+    if ((!side[p] && !hip_ok(hipStreamCreateWithFlags(&side[p], hipStreamNonBlocking), "stream")) ||
+        (!ev_join[p] && !hip_ok(hipEventCreateWithFlags(&ev_join[p], hipEventDisableTiming), "event"))) {
       return rc;
     }
     const drsa_amd_problem_t& q = probs[p];
@@ -1861,10 +1871,7 @@ int drsa_amd_drsa_run_multi(int P, const drsa_amd_problem_t* probs, int steps, i
   }
   int r = forked(0, true);
   if (r) { cleanup(); return r; }
-  // make sure nothing is pending on the side streams before they are destroyed
-  for (int p = 0; p < P; ++p) (void)hipStreamSynchronize(side[p]);
-  cleanup();
-  if (steps == 0 || stream_capturing(s)) return DRSA_OK;
+  if (steps == 0 || capturing) return DRSA_OK;
   for (int p = 0; p < P; ++p) {
     const drsa_amd_problem_t& q = probs[p];
     if (int rc2 = coop_check(ws_xchg(q.ws, q.N, geom(q.d, q.K)), s, "drsa_run_multi")) return rc2;

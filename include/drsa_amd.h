@@ -346,7 +346,10 @@ int drsa_amd_drsa_partial_f16(const uint16_t* A, const uint16_t* C, int64_t N, i
 
 /* P independent problems advanced S steps together (C5: two layers, K=16 each, one graph).
  * Replaces the sequential per-layer loop of optsubspaces.py:18-23 / drsa.main. */
-/* Returns DRSA_ETIMEOUT like drsa_amd_drsa_run when a problem's cooperative finish timed out. */
+/* Returns DRSA_ETIMEOUT like drsa_amd_drsa_run when a problem's cooperative finish timed out.
+ * Capturable: inside a caller's stream capture it records the per-problem chains on forked side
+ * streams (a per-thread pool that outlives the call) joined back into `stream`, and skips its own
+ * graph and the status read-back (drsa_amd_drsa_coop_status per problem after the replay). */
 int drsa_amd_drsa_run_multi(int P, const drsa_amd_problem_t* probs, int steps, int use_graph, void* stream);
 
 /* P independent fp32 problems sharing one padded geometry (same pow2(d) and concept width; N may

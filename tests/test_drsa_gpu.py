@@ -150,6 +150,34 @@ def test_coop_finish_timeout_is_loud_and_recoverable():
     assert torch.equal(U1, U2) and torch.equal(t1, t2)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_joint_run_captured_in_caller_graph_equals_eager(dtype):
+    """drsa_amd_drsa_run_multi inside a caller's stream capture (bench.py's steady-state timing,
+    VERDICT r05 item 2): it records its forked per-problem chains into the caller's graph; two
+    replays of that graph give the eager joint run's trajectories and U bit for bit (d = 128 takes
+    the cooperative finish, whose status word stays 0)."""
+    from drsa_audio_amd.xai.drsa.drsa import drsa_run_joint
+    N, d, K, steps = 3000, 128, 16, 7
+    probs = []
+    for seed in (1, 2):
+        A, C = drsa_inputs(N, d, seed)
+        Ag, Cg, Ug = _gpu(A, C, _u0(d, seed))
+        probs.append((Ag.to(dtype), Cg.to(dtype), Ug, K))
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        ref = drsa_run_joint(probs, steps)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        out = drsa_run_joint(probs, steps)
+    for _ in range(2):
+        with torch.cuda.stream(side):
+            g.replay()
+        torch.cuda.synchronize()
+        for (U, t), (Ur, tr) in zip(out, ref):
+            assert torch.equal(t, tr) and torch.equal(U, Ur)
+
+
 def test_sharded_fused_step_equals_two_call_form_bitwise():
     """sharded_run's fused path (drsa_amd_drsa_fused_step: finish + the next partial in one
     launch, caller-owned buffers) equals the partial / finish two-call form bit for bit."""
