@@ -766,9 +766,49 @@ __device__ __forceinline__ void reduce_grouped(const float* __restrict__ partial
   }
 }
 
+// The per-leaf slab reduce of drsa_run / the fused and sharded steps (LG = kLeafGroup), spread over
+// the chip: RW = 256 / CW thread rows per workgroup of CW columns, each thread computing the group
+// sums G_q of QPT = kMaxGroups / RW groups with all QPT * kLeafGroup slab loads issued first; the
+// same additions in the same order as reduce_grouped (bit-identical), on E / CW workgroups instead of
+// E / 64 (C3: 129 instead of 65 CUs, 32 loads per thread in flight instead of 8 rounds of 8;
+// A/B at C3 (gpurun_out/r6e): CW 8 / 16 / 32 = 33.9 / 32.4 / 31.7 us per step).
+#ifndef DRSA_REDUCE_CW
+#define DRSA_REDUCE_CW 32
+#endif
+// (CW = 64 for the DP = 128 slabs: E / 16 = 1025 workgroups measured slower than E / 64 = 257)
+template <int CW>
 __global__ __launch_bounds__(256) void drsa_reduce_kernel(const float* __restrict__ partials, int P, int E, int ES,
                                                           float* __restrict__ out) {
-  reduce_grouped(partials, P, kLeafGroup, ES, E, out);
+  constexpr int RW = 256 / CW, QPT = kMaxGroups / RW;
+  static_assert(kMaxGroups % RW == 0, "groups per thread");
+  __shared__ float part[kMaxGroups][CW];
+  const int c = threadIdx.x % CW, r = threadIdx.x / CW;
+  const int e = blockIdx.x * CW + c;
+  const int ng = (P + kLeafGroup - 1) / kLeafGroup;
+  const int ec = e < E ? e : 0;
+  float v[QPT][kLeafGroup];
+#pragma unroll
+  for (int j = 0; j < QPT; ++j)
+#pragma unroll
+    for (int i = 0; i < kLeafGroup; ++i) {
+      const int p = (r + RW * j) * kLeafGroup + i;
+      v[j][i] = partials[(size_t)(p < P ? p : 0) * ES + ec];
+    }
+#pragma unroll
+  for (int j = 0; j < QPT; ++j) {
+    const int qq = r + RW * j;
+    float G = 0.f;
+#pragma unroll
+    for (int i = 0; i < kLeafGroup; ++i)
+      if (qq * kLeafGroup + i < P) G += v[j][i];
+    if (qq < ng) part[qq][c] = G;
+  }
+  __syncthreads();
+  if (r == 0 && e < E) {
+    float T = 0.f;
+    for (int qq = 0; qq < ng; ++qq) T += part[qq][c];
+    out[e] = T;
+  }
 }
 
 // the polar runs at PD = max(32, DP) (32x32 MFMA tiles; a d <= 16 problem is embedded once more)
@@ -776,9 +816,9 @@ template <int DP>
 constexpr int polar_dim() { return DP < 32 ? 32 : DP; }
 template <int DP>
 constexpr size_t finish_lds() {
-  // polar_ns16 (DP <= 64) needs no k-split scratch
+  // polar_ns16 (DP <= 64): the second X buffer; polar_ns: the k-split scratch
   constexpr int PD = polar_dim<DP>();
-  constexpr size_t scr = (PD <= 64 && DRSA_NS16) ? 0 : ns_scratch_floats<PD>();
+  constexpr size_t scr = ns_scratch_floats<PD>();
   return (2 * (size_t)PD * ns_ld<PD>() + 64 + scr) * sizeof(float);
 }
 
@@ -1380,7 +1420,14 @@ constexpr int kPolarMaxIter = 40;
 
 int launch_reduce(const float* partials, const PartialPlan& pl, const Geom& g, float* gs_out, hipStream_t s) {
   const size_t E = slab_floats(g), ES = slab_stride(g);
-  hipLaunchKernelGGL(drsa_reduce_kernel, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, s, partials, pl.grid, (int)E,
+  if (E <= 8192) {
+    constexpr int CW = DRSA_REDUCE_CW;
+    hipLaunchKernelGGL(drsa_reduce_kernel<CW>, dim3((unsigned)((E + CW - 1) / CW)), dim3(256), 0, s, partials, pl.grid,
+                       (int)E, (int)ES, gs_out);
+    DRSA_LAUNCH_CHECK();
+    return DRSA_OK;
+  }
+  hipLaunchKernelGGL(drsa_reduce_kernel<64>, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, s, partials, pl.grid, (int)E,
                      (int)ES, gs_out);
   DRSA_LAUNCH_CHECK();
   return DRSA_OK;

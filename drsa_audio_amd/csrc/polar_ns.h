@@ -73,9 +73,13 @@ __device__ __forceinline__ int t32_row(int r, int hi) { return (r & 3) + 8 * (r 
 // ascending) through LDS scratch.
 template <int DP>
 constexpr int ns_ks() { return DP >= 128 ? 1 : 4; }
+// scratch after X, T and the 64-float reduction slots: the k-split partial tiles of polar_ns, or
+// the second X buffer of polar_ns16 (DP <= 64)
 template <int DP>
 constexpr size_t ns_scratch_floats() {
-  return ns_ks<DP>() == 1 ? 0 : (size_t)(DP / 32) * (DP / 32) * ns_ks<DP>() * 1024;
+  return (DP <= 64 && DRSA_NS16) ? (size_t)DP * ns_ld<DP>()
+         : ns_ks<DP>() == 1      ? 0
+                                 : (size_t)(DP / 32) * (DP / 32) * ns_ks<DP>() * 1024;
 }
 
 // (So the caller's tol does not bound the returned U after such a last update; the bound below does,
@@ -239,8 +243,11 @@ __device__ __forceinline__ int polar_ns(float* X, float* T, float* red, float* s
 // DP <= 64: the same iteration on 16x16x4 MFMA tiles, one output tile per wave (no k-split, so no
 // LDS scratch round trip and no extra barrier per product).  16x16 D layout: lane l, reg r ->
 // row 4(l>>4) + r, col l&15; A/B operands: lane l holds k = k0 + (l>>4), row/col l&15.
+// X is double-buffered (X, Xn swap per update): X T goes straight into the buffer nobody reads in
+// this iteration, so an iteration has two barriers (X complete; T and the error complete) instead of
+// three; on return X points at the buffer holding the result.  Same arithmetic, same bits.
 template <int DP>
-__device__ __forceinline__ int polar_ns16(float* X, float* T, float* red, float tol, int max_iter) {
+__device__ __forceinline__ int polar_ns16(float*& X, float* Xn, float* T, float* red, float tol, int max_iter) {
   constexpr int NT = fin_threads<DP>(), LD = ns_ld<DP>(), NB = DP / 16, NWV = NT / 64;
   constexpr int NSYM = NB * (NB + 1) / 2, NFULL = NB * NB;
   constexpr int TPR = NT / DP;
@@ -314,12 +321,15 @@ __device__ __forceinline__ int polar_ns16(float* X, float* T, float* red, float 
         const int k = k0 + hi;
         acc = mfma16(X[(16 * fib + lo) * LD + k], T[k * LD + 16 * fjb + lo], acc);
       }
-    }
-    __syncthreads();   // every read of X done
-    DRSA_NS_STAMP(4 * it + 3);
-    if (w < NFULL) {
+      // no barrier: Xn was last read in the previous iteration, before this one's first barrier
 #pragma unroll
-      for (int r = 0; r < 4; ++r) X[(16 * fib + 4 * hi + r) * LD + 16 * fjb + lo] = acc[r];
+      for (int r = 0; r < 4; ++r) Xn[(16 * fib + 4 * hi + r) * LD + 16 * fjb + lo] = acc[r];
+    }
+    DRSA_NS_STAMP(4 * it + 3);
+    {
+      float* t = X;
+      X = Xn;
+      Xn = t;
     }
     if (last) { ++it; break; }
   }
@@ -328,9 +338,10 @@ __device__ __forceinline__ int polar_ns16(float* X, float* T, float* red, float 
 }
 
 // the production polar: 16x16 tiles below DP = 128, 32x32 (k-split where needed) otherwise
+// (DP <= 64: scr holds the second X buffer, ns_scratch_floats; X may come back pointing at it)
 template <int DP>
-__device__ __forceinline__ int polar_run(float* X, float* T, float* red, float* scr, float tol, int max_iter) {
-  if constexpr (DP <= 64 && DRSA_NS16) return polar_ns16<DP>(X, T, red, tol, max_iter);
+__device__ __forceinline__ int polar_run(float*& X, float* T, float* red, float* scr, float tol, int max_iter) {
+  if constexpr (DP <= 64 && DRSA_NS16) return polar_ns16<DP>(X, scr, T, red, tol, max_iter);
   else return polar_ns<DP>(X, T, red, scr, tol, max_iter);
 }
 
