@@ -726,16 +726,15 @@ def main():
             kernels[tag]["tflops"] = 2.0 * m / (avg * 1e-3) / 1e12
     dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
     dom_ach = kernels[dom].get("tflops", 0.0)
-    traffic = traffic_src = clock = None
+    traffic = traffic_src = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         try:
             with open(pmc_path) as fh:
                 pm = json.load(fh)
             traffic = pm.get("per_launch_bytes", {}).get(dom)
-            # the same profile's clock pass: the clock the chip held during the dominant kernel and
-            # the fraction of those cycles its MFMA pipes were busy (frac ~= mfma_busy * clock / 2.4 GHz)
-            clock = pm.get("clock", {}).get(dom)
+            # (no clock figure: GRBM_GUI_ACTIVE / 8 over a PMC-serialised dispatch read 2.4-6.7 GHz,
+            # above the 2.4 GHz behind the peak, so it is not physical)
             # PMC counters cannot be read inside this process: the bytes come from the committed
             # rocprofv3 --pmc passes (scripts/pmc_run.sh) of the same kernel, named here
             traffic_src = f"profiles/pmc_traffic.json ({pm.get('profile', 'unlabelled')}), not measured in this run"
@@ -863,7 +862,7 @@ def main():
                        "one_device_rehearsal": one_dev, "backend": backend if world > 1 else None},
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": dom_ach, "peak": FP32_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": dom_ach / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic,
-                         "traffic_source": traffic_src, "clock_pmc": clock},
+                         "traffic_source": traffic_src},
             "whole_path": {"algorithmic_gflop_per_sample": 2.0 * total_macs / B / 1e9,
                            "achieved_tflops": 2.0 * total_macs * value / B / world / 1e12},
             "kernels": kernels,
