@@ -11,9 +11,5 @@ for c in FETCH_SIZE WRITE_SIZE; do
     python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-drsa --tag-order $OUT/tags_$c.json \
     > $OUT/pmc_$c.log 2>&1
 done
-# effective clock and MFMA-pipe occupancy per kernel (two counters of different blocks in one pass)
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES --output-format csv \
-  -d $OUT/pmc_CLOCK -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-drsa \
-  --tag-order $OUT/tags_CLOCK.json > $OUT/pmc_CLOCK.log 2>&1
 cp $OUT/tags_FETCH_SIZE.json $OUT/tags.json
 python scripts/tag_profile.py pmc $OUT $OUT/tags.json $OUT/pmc_traffic.json > /dev/null
