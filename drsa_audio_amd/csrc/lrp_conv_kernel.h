@@ -38,6 +38,17 @@
 #ifndef DRSA_CONV_BWD_WPE
 #define DRSA_CONV_BWD_WPE 3
 #endif
+// small-chunk rule backward (SMALL_BWD: GTZAN conv_bwd:features.3 / .6): its MFMA operand ring is
+// pinned (a sched_barrier per k-step keeps step k + PD's LDS reads ahead of step k's MFMAs; the
+// scheduler otherwise sinks each read next to its MFMA behind an lgkmcnt(0) wait) at distance 3.
+// Measured in the step (gpurun_out/r6j, r6k): features.3 1.373-1.383 -> 1.335 ms, .6 0.632 ->
+// 0.613; pinning the forwards or the wider backwards as well made them 2-6 % slower.
+#ifndef DRSA_CONV_PIN_SMALL
+#define DRSA_CONV_PIN_SMALL 1
+#endif
+#ifndef DRSA_CONV_PD_SMALL
+#define DRSA_CONV_PD_SMALL 3
+#endif
 #ifndef DRSA_CONV_PRE_D
 #define DRSA_CONV_PRE_D 0
 #endif
@@ -148,7 +159,8 @@ struct ConvCfg {
                                 : EPI != EPI_BWD && CIC <= 8 && NG <= 2 && COUT == 64 ? DRSA_CONV_FWD_WPE_WIDE
                                 : EPI != EPI_BWD && CIC <= 4 && NG <= 2 && COUT == 128 && TW == 8 ? DRSA_CONV_FWD_WPE_128 : 1);
   // operand prefetch distance of the MFMA loop (k-steps)
-  static constexpr int PD = DRSA_CONV_PD_BWD > 0 && EPI >= EPI_BWD ? DRSA_CONV_PD_BWD : 1;
+  static constexpr bool PIN = SMALL_BWD && DRSA_CONV_PIN_SMALL;
+  static constexpr int PD = PIN ? DRSA_CONV_PD_SMALL : DRSA_CONV_PD_BWD > 0 && EPI >= EPI_BWD ? DRSA_CONV_PD_BWD : 1;
   static_assert(TH % MTH == 0 && TW % MTW == 0, "tile must be a multiple of the M-tile");
   static_assert(COUT % 32 == 0, "COUT must be padded to 32");
   static_assert(CIN % CIC == 0, "CIN must be a multiple of the chunk");
@@ -437,14 +449,25 @@ __device__ __forceinline__ void mfma_chunk(const float* halo, const float* wl, c
   constexpr int MPW = Cfg::MPW, NPW = Cfg::NPW, NG = Cfg::NG_, COUT = Cfg::COUT_;
   constexpr int KC = Cfg::KC, KCP = Cfg::KCP, PLANE = Cfg::PLANE, RS = Cfg::RS, EPI = Cfg::EPI_;
   const int h = lane >> 5;
+  // Halo offset of k = k0 + h (k = ci * 9 + tap):  off(k0) + h * delta(k0 % 9), with off(k0) a
+  // compile-time immediate (the loop is unrolled) and delta one of three values: +1 inside a tap
+  // row, RS - 2 from the row's last tap to the next row, PLANE - 2 RS - 2 from tap 8 to the next
+  // channel's tap 0.  So each m-tile needs three per-lane base registers (pix_off + h * delta)
+  // instead of one per k-step pattern, and every operand read is base + immediate.
+  constexpr int DLT[3] = {1, RS - 2, PLANE - 2 * RS - 2};
+  int xb[MPW][3];
+#pragma unroll
+  for (int u = 0; u < MPW; ++u)
+#pragma unroll
+    for (int t = 0; t < 3; ++t) xb[u][t] = pix_off[u] + h * DLT[t];
   auto read_x = [&](int k0, float (&xv)[MPW]) {
-    const int jj = (k0 / 2) % 9, mm = (k0 / 2) / 9;
-    const int kk = 2 * jj + h;
-    const int off = (kk / 9) * PLANE + ((kk % 9) / 3) * RS + (kk % 3) + mm * 2 * PLANE;
+    const int r9 = k0 % 9;
+    const int off = (k0 / 9) * PLANE + (r9 / 3) * RS + (r9 % 3);
+    const int t = (r9 == 8) ? 2 : (r9 == 2 || r9 == 5) ? 1 : 0;
 #pragma unroll
     for (int u = 0; u < MPW; ++u) {
-      if constexpr (KC % 2 == 0) xv[u] = halo[off + pix_off[u]];
-      else xv[u] = (k0 + h < KC) ? halo[off + pix_off[u]] : 0.f;
+      if constexpr (KC % 2 == 0) xv[u] = halo[xb[u][t] + off];
+      else xv[u] = (k0 + h < KC) ? halo[xb[u][t] + off] : 0.f;
     }
   };
   auto read_w = [&](int k0, float (&wv)[NG][NPW]) {
@@ -468,6 +491,7 @@ __device__ __forceinline__ void mfma_chunk(const float* halo, const float* wl, c
       read_x(k0 + 2 * PD, xr[nxt]);
       read_w(k0 + 2 * PD, wr[nxt]);
     }
+    if constexpr (Cfg::PIN) __builtin_amdgcn_sched_barrier(0);   // keep the ring (see DRSA_CONV_PIN_SMALL)
 #pragma unroll
     for (int v = 0; v < NPW; ++v)
 #pragma unroll
@@ -782,12 +806,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
   auto gchs = [&](int cl, int v, int sub) { return ES == 1 ? gch(cl, v) : v * 32 + sub * TCH + cl; };
   typename std::conditional<Cfg::BF, StagerBF<Cfg>, Stager<Cfg>>::type stg;
   stg.load(a, 0, tid, ty0, tx0, bq, bs);
+  CONV_STAMP(11);
   // backward: all chunks but the last here, the last one peeled below (after the epilogue
   // addressing is set up, so that none of it is live across the loop)
   for (int chunk = 0; chunk + (EPI == EPI_BWD ? 1 : 0) < Cfg::NCHUNK; ++chunk) {
     __syncthreads();
+    if (chunk == 0) CONV_STAMP(9);
     if constexpr (Cfg::BF) stg.store(halo, wl, tid, ty0, tx0);
     else stg.store(halo, wl, tid);
+    if (chunk == 0) CONV_STAMP(10);
     __syncthreads();
     CONV_STAMP(1 + 2 * chunk);
     if (chunk + 1 < Cfg::NCHUNK) stg.load(a, (chunk + 1) * CIC, tid, ty0, tx0, bq, bs);

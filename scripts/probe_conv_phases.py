@@ -47,6 +47,8 @@ cu = (xcc << 8) | (((hw >> 13) & 7) << 4) | ((hw >> 8) & 15)   # xcc, se, cu
 life = a[:, 13] - a[:, 0]
 
 first = a[:, 1] - a[:, 0]                                  # first chunk loaded + staged
+# first chunk split: 11 loads issued, 9 past the first barrier, 10 stored (loads landed)
+f_issue, f_bar1, f_store, f_bar2 = a[:, 11] - a[:, 0], a[:, 9] - a[:, 11], a[:, 10] - a[:, 9], a[:, 1] - a[:, 10]
 mf = [a[:, 2 + 2 * c] - a[:, 1 + 2 * c] for c in range(NCH)]          # chunk c MFMA issue span
 stg = [a[:, 1 + 2 * c] - a[:, 2 * c] for c in range(1, NCH)]          # chunk c staging (after c-1's MFMAs)
 epi = a[:, 13] - a[:, 2 * NCH]
@@ -54,7 +56,10 @@ res = {"workgroups": int(len(a)), "cus": int(len(set(cu.tolist()))),
        "median_cycles": {"lifetime": float(np.median(life)), "first_stage": float(np.median(first)),
                          **{f"mfma_{c}": float(np.median(mf[c])) for c in range(NCH)},
                          **{f"stage_{c + 1}": float(np.median(stg[c])) for c in range(NCH - 1)},
-                         "epilogue": float(np.median(epi))}}
+                         "epilogue": float(np.median(epi)),
+                       "first_issue": float(np.median(f_issue)), "first_barrier1": float(np.median(f_bar1)),
+                       "first_store_wait": float(np.median(f_store)), "first_barrier2": float(np.median(f_bar2))},
+       "first_store_wait_pct": {str(q): float(np.percentile(f_store, q)) for q in (10, 25, 50, 75, 90, 99)}}
 # per CU: concurrency (workgroups alive) over time and the fraction of time with k workgroups in an
 # MFMA span
 by = collections.defaultdict(list)
