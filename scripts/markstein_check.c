@@ -1,5 +1,6 @@
 // Markstein quotient check: y = RN(1/b), q0 = RN(a y), r = fma(-q0, b, a), q = fma(r, y, q0)
 // against the IEEE quotient a / b on random fp32 pairs.  gcc -O2 -ffp-contract=off scripts/markstein_check.c -lm
+#include <stdlib.h>
 #include <math.h>
 #include <stdio.h>
 #include <stdint.h>
