@@ -95,6 +95,9 @@ class DrsaProblem(C.Structure):
                 ("f_traj", _vp), ("counter", _vp), ("ws", _vp), ("ws_size", _sz), ("dtype", _i32)]
 
 
+# status codes (include/drsa_amd.h)
+DRSA_OK, DRSA_EINVAL, DRSA_EWORKSPACE, DRSA_EUNSUPPORTED, DRSA_ETIMEOUT = 0, -1, -2, -3, -4
+
 XM_NONE, XM_MUL, XM_SPLIT = 0, 1, 2
 POST_NONE, POST_DIV, POST_MASK, POST_DIV_RING = 0, 1, 2, 3
 POST_DIV_MAP = 4   # host-side plan tag only: POST_DIV on an input-independent map (drsa_amd_conv_bwd_den_map)

@@ -119,3 +119,15 @@ def test_alphabeta_parameter_checks_like_zennit():
     for a, b in ((-1.0, -2.0), (1.0, -0.0 - 1.0), (2.0, 0.5), (0.5, 0.0)):
         with pytest.raises(ValueError):
             AlphaBeta(a, b)
+
+
+def test_coop_status_and_spin_budget_argument_errors():
+    """drsa_amd_drsa_coop_status / drsa_amd_debug_coop_spin_budget reject bad arguments before any
+    device work (the status itself is read on the GPU: tests/test_drsa_gpu.py)."""
+    lib = _capi.lib()
+    st = ctypes.c_int(7)
+    assert lib.drsa_amd_drsa_coop_status(None, 100, 128, 16, ctypes.addressof(st), None) == _capi.DRSA_EINVAL
+    assert lib.drsa_amd_drsa_coop_status(ctypes.c_void_p(16), 100, 128, 3, ctypes.addressof(st), None) == _capi.DRSA_EINVAL
+    assert lib.drsa_amd_drsa_coop_status(ctypes.c_void_p(16), 0, 128, 16, ctypes.addressof(st), None) == _capi.DRSA_EINVAL
+    assert lib.drsa_amd_debug_coop_spin_budget(-2) == _capi.DRSA_EINVAL
+    assert lib.drsa_amd_debug_coop_spin_budget(-1) == 0
