@@ -49,6 +49,12 @@
 #ifndef DRSA_CONV_PD_SMALL
 #define DRSA_CONV_PD_SMALL 3
 #endif
+#ifndef DRSA_CONV_SMALL_WPE
+#define DRSA_CONV_SMALL_WPE 4      // small-chunk backward: 4 workgroups (16 waves) per CU
+#endif
+#ifndef DRSA_CONV_SMALL_ES
+#define DRSA_CONV_SMALL_ES 2       // small-chunk backward: epilogue in 2 channel passes of 16
+#endif
 #ifndef DRSA_CONV_PRE_D
 #define DRSA_CONV_PRE_D 0
 #endif
@@ -146,7 +152,7 @@ struct ConvCfg {
   // small-chunk rule backward (CIC <= 8, 32 output channels): 24.6 KB LDS and <= 128 VGPRs, so
   // 4 workgroups (16 waves) per CU
   static constexpr bool SMALL_BWD = EPI == EPI_BWD && NG == 1 && CIC <= 8 && COUT <= 32;
-  static constexpr int ES = (EPI == EPI_BWD && WN == 1) ? (SMALL_BWD ? 2 : DRSA_CONV_BWD_ES) : 1;
+  static constexpr int ES = (EPI == EPI_BWD && WN == 1) ? (SMALL_BWD ? DRSA_CONV_SMALL_ES : DRSA_CONV_BWD_ES) : 1;
   static constexpr int TCH = WN * 32 / ES;                     // channels staged per epilogue pass
   static constexpr size_t staging_floats =
       BF ? bf_halo_floats + bf_w_floats : (size_t)CIC * PLANE + (size_t)NG * KCP * COUT;
@@ -154,7 +160,7 @@ struct ConvCfg {
   static constexpr size_t lds_floats = staging_floats > epi_floats ? staging_floats : epi_floats;
   // minimum waves per SIMD the register allocation must allow (1 block = 1 wave per SIMD)
   static constexpr int WPE = BF ? (COUT <= 64 ? DRSA_CONV_BF_WPE : 1)
-                             : (EPI == EPI_BWD && NG == 1) ? (SMALL_BWD ? 4 : DRSA_CONV_BWD_WPE)
+                             : (EPI == EPI_BWD && NG == 1) ? (SMALL_BWD ? DRSA_CONV_SMALL_WPE : DRSA_CONV_BWD_WPE)
                              : (EPI != EPI_BWD && CIC <= 8 && COUT <= 32 && NG <= 2 ? DRSA_CONV_FWD_WPE
                                 : EPI != EPI_BWD && CIC <= 8 && NG <= 2 && COUT == 64 ? DRSA_CONV_FWD_WPE_WIDE
                                 : EPI != EPI_BWD && CIC <= 4 && NG <= 2 && COUT == 128 && TW == 8 ? DRSA_CONV_FWD_WPE_128 : 1);
@@ -781,9 +787,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
   constexpr int CT = (NCELL + kThreads - 1) / kThreads;
   float* T = smem;
   constexpr int ES = Cfg::ES;
-  static_assert(ES == 1 || ES == 2, "epilogue split must be 1 or 2");
+  static_assert(ES == 1 || ES == 2 || ES == 4, "epilogue split must be 1, 2 or 4");
   // pass `sub` of ES stages the registers whose channel lies in [sub*TCH, (sub+1)*TCH)
-  // (ES = 2: r >> 3 == sub, since channel = (r&3) + 8(r>>2) + 4h)
+  // (channel = (r&3) + 8(r>>2) + 4h: ES = 2 takes r >> 3 == sub, ES = 4 r >> 2 == sub)
   auto stage = [&](int v, auto valfn, int sub = 0) {
     __syncthreads();
     if (active) {
@@ -795,7 +801,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ConvCf
           if constexpr (ES == 1) {
             T[((wn * 32 + cf) * TH + pix_y[u]) * TWP + pix_x[u]] = valfn(u, r);
           } else {
-            if ((r >> 3) == sub) T[((cf - TCH * sub) * TH + pix_y[u]) * TWP + pix_x[u]] = valfn(u, r);
+            if ((r >> (ES == 2 ? 3 : 2)) == sub) T[((cf - TCH * sub) * TH + pix_y[u]) * TWP + pix_x[u]] = valfn(u, r);
           }
         }
     }

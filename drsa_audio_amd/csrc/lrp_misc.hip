@@ -746,6 +746,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
 #ifndef DRSA_PROJ_DBG
 #define DRSA_PROJ_DBG 0
 #endif
+    // the clones share a and den: stabilise the denominators once per tile (without den the
+    // quotient is x / 1 = x exactly), so the clone epilogue below is branch-free
+    if constexpr (PF) {
+#pragma unroll
+      for (int i = 0; i < NB * 4; ++i) dv[i] = has_den ? stab(dv[i], eps_den) : 1.f;
+    }
     for (int qi = 0; qi < ((DRSA_PROJ_DBG & 2) ? 0 : nq); ++qi) {   // ablation bit 2: no clone stage
       const int q = fanout == 1 ? qi : fanout == 2 ? qi + 1 : b % (K + 1);
       const int j0 = q == 0 ? 0 : (q - 1) * dk, j1 = q == 0 ? d : q * dk;
@@ -754,12 +760,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
       f32x4 acc[NB];
 #pragma unroll
       for (int cb = 0; cb < NB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // operands read unconditionally from an in-range row and zeroed afterwards: one LDS round
+      // trip per k-step instead of an exec branch and a wait per read
+      if (j1 - j0 == 16) {
+        // d_k = 16 (GTZAN j = 7: d = 64, K = 4): all four k-steps' operands in one round trip
+        float g0[4], u0[4][NB];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int j = j0 + 4 * s + rg;
+          g0[s] = RB[j * PW + pc];
+#pragma unroll
+          for (int cb = 0; cb < NB; ++cb) u0[s][cb] = Us[(cb * 16 + pc) * LD + j];
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int cb = 0; cb < NB; ++cb) acc[cb] = mfma16(u0[s][cb], g0[s], acc[cb]);
+      } else
+#pragma unroll 2
       for (int k0 = j0; k0 < j1; k0 += 4) {
         const int j = k0 + rg;
         const bool ok = j < j1;
-        const float gb = ok ? RB[j * PW + pc] : 0.f;
+        const int jc = ok ? j : j0;
+        const float g0 = RB[jc * PW + pc];
+        float u0[NB];
 #pragma unroll
-        for (int cb = 0; cb < NB; ++cb) acc[cb] = mfma16(ok ? Us[(cb * 16 + pc) * LD + j] : 0.f, gb, acc[cb]);
+        for (int cb = 0; cb < NB; ++cb) u0[cb] = Us[(cb * 16 + pc) * LD + jc];
+        const float gb = ok ? g0 : 0.f;
+#pragma unroll
+        for (int cb = 0; cb < NB; ++cb) acc[cb] = mfma16(ok ? u0[cb] : 0.f, gb, acc[cb]);
       }
 #pragma unroll
       for (int cb = 0; cb < NB; ++cb)
@@ -769,17 +798,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DP <= 64 ? 
           const bool cok = c < d;
           const int os = (cok ? c : 0) * HW + pixl;
           const float ax = av[cb * 4 + r];
-          float dx = 1.f;
-          if constexpr (PF) dx = dv[cb * 4 + r];
-          else if (has_den) dx = den_b[os];
-          const float Rv = ax * acc[cb][r];
-          float gq;
-          if (has_den) {
-            const float qd = div_nb(Rv, stab(dx, eps_den));   // every lane, then the select
-            gq = (ax > 0.f) ? qd : 0.f;
+          float sd;
+          if constexpr (PF) {
+            sd = dv[cb * 4 + r];
           } else {
-            gq = (ax > 0.f) ? Rv : 0.f;
+            const float dx = den_b[os];   // den_b is a valid row (a) without den
+            sd = has_den ? stab(dx, eps_den) : 1.f;
           }
+          const float qd = div_nb(ax * acc[cb][r], sd);   // every lane, then the select
+          const float gq = (ax > 0.f) ? qd : 0.f;
 #if DRSA_PROJ_DBG & 1
           if (cok && gq == 12345.f) G_q[c * HW + pixl] = gq;   // ablation: no G stores
 #else
@@ -994,14 +1021,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRSA_FQ_WPE
       for (int k = 0; k < FQ_KR; ++k) {
         const int ry = wv4 + 4 * k, cy = qy0 - 1 + ry, c = c0 + ci;
         const bool ok = ry < FQ_RY && c < C && cy >= 0 && cy < H2 && cx < W2;
-        const int o = ok ? c * iplane + cy * W2 + cx : 0;   // 32-bit offsets: saddr + voffset loads
+        const unsigned o = ok ? c * iplane + cy * W2 + cx : 0;   // unsigned 32-bit offsets: saddr + voffset loads
         v[ci * FQ_KR + k] = gb[o];
         sb[ci * FQ_KR + k] = (int)ab[o];
       }
     {
       const int c = c0 + hci, cy = qy0 - 1 + hry, cxh = qx0 - 1 + hrx;
       const bool ok = hact && c < C && cy >= 0 && cy < H2 && cxh >= 0 && cxh < W2;
-      const int o = ok ? c * iplane + cy * W2 + cxh : 0;
+      const unsigned o = ok ? c * iplane + cy * W2 + cxh : 0;
       v[FQ_NS - 1] = gb[o];
       sb[FQ_NS - 1] = (int)ab[o];
     }

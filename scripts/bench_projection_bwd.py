@@ -10,6 +10,7 @@ import torch
 from drsa_audio_amd import _capi
 
 dev = torch.device("cuda")
+torch.manual_seed(0)
 B, D, H, W, K = 512, 64, 32, 32, 4
 g = torch.randn(B, D, H // 2, W // 2, device=dev)
 amax = torch.randint(0, 4, (B, D, H // 2, W // 2), device=dev, dtype=torch.uint8)
@@ -43,4 +44,7 @@ e1.record()
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / 20
 byts = (g.numel() + 4 * a.numel() + G.numel()) * 4 + amax.numel()
-print(json.dumps({"lib": os.environ.get("DRSA_AMD_LIB", "default"), "rc": RC, "ms": ms, "GBs": byts / ms / 1e6, "tflops": 2 * 3 * B * H * W * D * D / ms / 1e9}))
+nq = K if FAN == 2 else K + 1
+Gi = G[:B * nq].view(torch.int32).to(torch.int64)
+chk = int((Gi * (torch.arange(Gi.numel(), device=dev, dtype=torch.int64).view_as(Gi) % 1000003 + 1)).sum())
+print(json.dumps({"lib": os.environ.get("DRSA_AMD_LIB", "default"), "rc": RC, "ms": ms, "bits_checksum": chk, "GBs": byts / ms / 1e6, "tflops": 2 * 3 * B * H * W * D * D / ms / 1e9}))
