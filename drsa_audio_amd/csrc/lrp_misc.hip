@@ -965,6 +965,10 @@ __global__ __launch_bounds__(256) void first_layer_bwd_kernel(const float* __res
 #ifndef DRSA_FQ_WPE
 #define DRSA_FQ_WPE 8
 #endif
+// 1: cells staged through range-checked buffer loads into a pixel image that keeps its zeros
+#ifndef DRSA_FQ_INC
+#define DRSA_FQ_INC 1
+#endif
 // 1: the 6 x 6 patch streamed row by row (one row of pairs live: fewer VGPRs, more waves)
 #ifndef DRSA_FQ_STREAM
 #define DRSA_FQ_STREAM 1
@@ -1129,6 +1133,72 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRSA_FQ_WPE
     __syncthreads();
     if (c0 + 3 * FQ_C < C) fetch(c0 + 3 * FQ_C, v2, sb2);
     compute(c0 + FQ_C);
+  }
+#elif DRSA_FQ_INC
+  static_assert(FQ_C == 1, "incremental staging: one channel per group");
+  // Cells through buffer loads: a per-channel descriptor (uniform) over the channel's plane, so a
+  // cell above / below the image reads 0 (value and argmax byte) by the hardware range check, and
+  // a cell left / right of it is pushed out of range by its lane offset; the per-k lane offsets
+  // are one base + k rows.  The pixel image keeps its zeros between channels: each staged cell
+  // clears the one pixel it set for the previous channel and sets the argmax pixel of this one
+  // (LDS writes of a lane land in order), 3 VALU per cell instead of 4 compares + 4 selects.
+  const int cxl = qx0 + lane;
+  const unsigned OOR = 0x80000000u;   // >= any plane's byte size: the range check returns 0
+  const unsigned lane_off = cxl < W2 ? (unsigned)(((qy0 - 1 + wv4) * W2 + cxl) * 4) : OOR;
+  const int cxh = qx0 - 1 + hrx;
+  const unsigned halo_off =
+      (hact && cxh >= 0 && cxh < W2) ? (unsigned)(((qy0 - 1 + hry) * W2 + cxh) * 4) : OOR;
+  const unsigned row4 = (unsigned)(4 * 4 * W2);   // 4 cell rows in bytes
+  const unsigned pbytes = (unsigned)(iplane * 4);
+  float vi[FQ_NS];
+  unsigned si[FQ_NS];
+  auto fetch_b = [&](int c) {
+    // re-derive the per-k offsets every channel (5 adds) instead of holding 10 of them live
+    unsigned lo = lane_off, ho = halo_off;
+    asm volatile("" : "+v"(lo), "+v"(ho));
+    const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(gb + (size_t)c * plane), 0, (int)pbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(ab + (size_t)c * plane), 0, (int)(pbytes / 4), 0x00020000);
+#pragma unroll
+    for (int k = 0; k < FQ_KR; ++k) {
+      const unsigned o = lo + (unsigned)k * row4;   // stays >= 2^31 when lane_off is OOR
+      vi[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, o, 0, 0));
+      si[k] = __builtin_amdgcn_raw_buffer_load_b8(ra, o >> 2, 0, 0);
+    }
+    vi[FQ_NS - 1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, ho, 0, 0));
+    si[FQ_NS - 1] = __builtin_amdgcn_raw_buffer_load_b8(ra, ho >> 2, 0, 0);
+  };
+  // LDS byte address of each staged cell's top-left pixel and of the pixel set last channel
+  typedef __attribute__((address_space(3))) char lds_char;
+  typedef __attribute__((address_space(3))) float lds_float;
+  lds_char* const imgb = (lds_char*)img;
+  int cell0[FQ_NS];
+  lds_float* prev[FQ_NS];
+#pragma unroll
+  for (int k = 0; k < FQ_KR; ++k) cell0[k] = 4 * (2 * (wv4 + 4 * k) * FQ_PX + 2 * (1 + lane) + FQ_C0);
+  cell0[FQ_NS - 1] = 4 * (2 * hry * FQ_PX + 2 * hrx + FQ_C0);
+#pragma unroll
+  for (int k = 0; k < FQ_NS; ++k) prev[k] = (lds_float*)(imgb + cell0[k]);
+  auto act = [&](int k) { return k == FQ_NS - 1 ? hact : (wv4 + 4 * k < FQ_RY); };
+  for (int i = tid; i < FQ_PY * FQ_PX; i += 256) img[i] = 0.f;
+  fetch_b(0);
+  for (int c0 = 0; c0 < C; ++c0) {
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < FQ_NS; ++k) {
+      if (act(k)) {
+        // argmax b = 2 row + col -> byte offset 4 col + 4 FQ_PX row = 4 b + (4 FQ_PX - 8) (b & 2)
+        const int b = (int)(si[k] & 3u);
+        lds_float* const nw = (lds_float*)(imgb + (cell0[k] + 4 * b + (4 * FQ_PX - 8) / 2 * (b & 2)));
+        *prev[k] = 0.f;
+        *nw = vi[k];
+        prev[k] = nw;
+      }
+    }
+    __syncthreads();
+    if (c0 + 1 < C) fetch_b(c0 + 1);
+    compute(c0);
   }
 #else
   fetch(0, v, sb);

@@ -9,6 +9,7 @@ import torch
 from drsa_audio_amd import _capi
 
 dev = torch.device("cuda")
+torch.manual_seed(0)
 DENSE = os.environ.get("FL_DENSE", "0") == "1"   # VGGish conv0: dense g, B = 32, 64 channels, 128 x 256
 if DENSE:
     Bs, clones, C, H, W = 32, 1, 64, 128, 256
@@ -38,4 +39,6 @@ e1.record()
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / 20
 byts = g.numel() * 4 + out.numel() * 4 + (0 if DENSE else amax.numel())
-print(json.dumps({"ms": ms, "GBs": byts / ms / 1e6, "tflops": 2 * Bq * H * W * C * 9 / ms / 1e9}))
+oi = out.view(torch.int32).to(torch.int64)
+chk = int((oi * (torch.arange(oi.numel(), device=dev, dtype=torch.int64).view_as(oi) % 1000003 + 1)).sum())
+print(json.dumps({"lib": os.environ.get("DRSA_AMD_LIB", "default"), "bits_checksum": chk, "ms": ms, "GBs": byts / ms / 1e6, "tflops": 2 * Bq * H * W * C * 9 / ms / 1e9}))
