@@ -993,6 +993,9 @@ __device__ __forceinline__ void fq_put(float* img, int ci, int ry, int rx, float
   d[FQ_PX + 1] = sb == 3 ? v : 0.f;
 }
 
+// W2C > 0: the pooled width as a compile-time constant (GTZAN: 64), so the per-k row offsets of the
+// staging loads are instruction immediates instead of adds
+template <int W2C>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRSA_FQ_WPE))) void first_layer_bwd_pooled_kernel(const float* __restrict__ g,
                                                                      const uint8_t* __restrict__ amax,
                                                                      const float* __restrict__ w2,
@@ -1000,7 +1003,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRSA_FQ_WPE
                                                                      int clones) {
   extern __shared__ __attribute__((aligned(16))) float img[];    // [FQ_C][FQ_PY][FQ_PX]
   const int tid = threadIdx.x, lane = tid & 63, wv4 = tid >> 6;
-  const int H2 = H / 2, W2 = W / 2;
+  const int H2 = H / 2, W2 = W2C > 0 ? W2C : W / 2;
   const int tiles_x = (W2 + FQ_X - 1) / FQ_X;
   const int qy0 = (blockIdx.x / tiles_x) * FQ_Y, qx0 = (blockIdx.x % tiles_x) * FQ_X;
   const int bq = blockIdx.y, bs = bq / clones;
@@ -1156,15 +1159,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRSA_FQ_WPE
     // re-derive the per-k offsets every channel (5 adds) instead of holding 10 of them live
     unsigned lo = lane_off, ho = halo_off;
     asm volatile("" : "+v"(lo), "+v"(ho));
+    // row k = 0 may lie above the image (a negative offset, out of range as unsigned); rows k >= 1
+    // hang off a base that is never negative, so their offsets add as instruction immediates (the
+    // hardware sums voffset + immediate without a 32-bit wrap)
+    const unsigned lo1 = lo + row4;
+    const unsigned la0 = lo >> 2, la1 = lo1 >> 2;   // the argmax plane's (byte) offsets are the cell indices
     const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(gb + (size_t)c * plane), 0, (int)pbytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t*>(ab + (size_t)c * plane), 0, (int)(pbytes / 4), 0x00020000);
 #pragma unroll
     for (int k = 0; k < FQ_KR; ++k) {
-      const unsigned o = lo + (unsigned)k * row4;   // stays >= 2^31 when lane_off is OOR
-      vi[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, o, 0, 0));
-      si[k] = __builtin_amdgcn_raw_buffer_load_b8(ra, o >> 2, 0, 0);
+      // stays >= 2^31 (2^29 for the argmax plane) when lane_off is OOR
+      const unsigned og = k == 0 ? lo : lo1 + (unsigned)(k - 1) * row4;
+      const unsigned oa = k == 0 ? la0 : la1 + (unsigned)(k - 1) * (row4 / 4);
+      vi[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, og, 0, 0));
+      si[k] = __builtin_amdgcn_raw_buffer_load_b8(ra, oa, 0, 0);
     }
     vi[FQ_NS - 1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, ho, 0, 0));
     si[FQ_NS - 1] = __builtin_amdgcn_raw_buffer_load_b8(ra, ho >> 2, 0, 0);
@@ -1713,9 +1723,12 @@ int drsa_amd_first_layer_bwd(const float* g, const uint8_t* amax, const float* w
     const int H2 = H / 2, W2 = W / 2;
     const dim3 grid(((H2 + FQ_Y - 1) / FQ_Y) * ((W2 + FQ_X - 1) / FQ_X), Bq);
     constexpr size_t lds = sizeof(float) * FQ_C * FQ_PY * FQ_PX;
-    DRSA_SMEM(first_layer_bwd_pooled_kernel, lds);
-    hipLaunchKernelGGL(first_layer_bwd_pooled_kernel, grid, dim3(256), lds, (hipStream_t)stream, g, amax, w2f, out,
-                       C, H, W, clones);
+#ifndef DRSA_FL_W2C_OFF
+#define DRSA_FL_W2C_OFF 0
+#endif
+    auto kf = W == 128 && !DRSA_FL_W2C_OFF ? first_layer_bwd_pooled_kernel<64> : first_layer_bwd_pooled_kernel<0>;
+    DRSA_SMEM(kf, lds);
+    hipLaunchKernelGGL(kf, grid, dim3(256), lds, (hipStream_t)stream, g, amax, w2f, out, C, H, W, clones);
   } else {
     const dim3 grid(((H + FL_TH - 1) / FL_TH) * ((W + FL_TW - 1) / FL_TW), Bq);
     if (W % 4 == 0)

@@ -22,7 +22,7 @@ def _unpool(gp, amax, clones):
     return up
 
 
-@pytest.mark.parametrize("H,W", [(128, 128), (64, 64), (34, 200), (2, 4), (96, 136)])
+@pytest.mark.parametrize("H,W", [(128, 128), (34, 128), (2, 128), (64, 64), (34, 200), (2, 4), (96, 136)])
 @pytest.mark.parametrize("C", [1, 5, 32])
 @pytest.mark.parametrize("clones", [1, 4])
 def test_pooled_equals_dense(H, W, C, clones):
