@@ -603,7 +603,7 @@ __global__ __launch_bounds__(256) void projection_bwd_kernel(
 //   region A [DP][16]: a, then g1;  region B [DP][16]: h, then g2   (wave-private LDS)
 // ===========================================================================
 #ifndef DRSA_PT_RC
-#define DRSA_PT_RC 4
+#define DRSA_PT_RC 2
 #endif
 constexpr int PT_RC = DRSA_PT_RC;   // tiles per workgroup (U staged once)
 #ifndef DRSA_PROJ_RC_WPE
